@@ -1,0 +1,706 @@
+// gi_device.h -- device-side geometry, RNG and shading for the MI355X path.
+//
+// Everything here runs inside HIP kernels (gfx950). Geometry and shading are fp64 like the
+// reference (RNScalar = double, RNBasics/RNScalar.h:14-18): the 1e-6 absolute tolerances of
+// RNScalar.h:225-316 are below fp32 resolution at scene scale. Each function cites the
+// reference function it re-expresses.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "gi_layout.h"
+
+namespace gi {
+
+#define GI_HD __host__ __device__ __forceinline__
+
+constexpr double kEps = 1.0e-6;     // RN_EPSILON, RNScalar.cpp:21
+constexpr double kInf = 1.0e6;      // RN_INFINITY, RNScalar.cpp:22
+constexpr double kPi = 3.14159265358979323846;
+
+// ---------------------------------------------------------------------------------------
+// RNG: keyed counter streams (replaces RNThreadableRandomScalar, RNScalar.cpp:99-131).
+// One stream per primary sample / spawned sample path / emitted photon, so results do not
+// depend on launch geometry, batch size or GPU count.
+// ---------------------------------------------------------------------------------------
+GI_HD uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+GI_HD uint64_t stream_key(uint64_t seed, uint64_t kind, uint64_t a, uint64_t b) {
+  uint64_t k = mix64(seed ^ (kind * 0xA0761D6478BD642FULL));
+  k = mix64(k + a * 0xE7037ED1A0B428DBULL + 0x8EBC6AF09C88C6E3ULL);
+  k = mix64(k + b * 0x589965CC75374CC3ULL + 0x1D8E4E27C47D124FULL);
+  return k;
+}
+enum { KIND_PRIMARY = 1, KIND_TRANS = 2, KIND_SPEC = 3, KIND_IND = 4,
+       KIND_PHOTON_GLOBAL = 5, KIND_PHOTON_CAUSTIC = 6 };
+struct Rng {
+  uint64_t key, ctr;
+  GI_HD void init(uint64_t seed, uint64_t kind, uint64_t a, uint64_t b) {
+    key = stream_key(seed, kind, a, b);
+    ctr = 0;
+  }
+  GI_HD double next() {
+    ctr++;
+    uint64_t u = mix64(key + ctr * 0x9E3779B97F4A7C15ULL);
+    return (double)(u >> 11) * (1.0 / 9007199254740992.0);
+  }
+};
+
+// ---------------------------------------------------------------------------------------
+// fp64 vectors
+// ---------------------------------------------------------------------------------------
+struct V {
+  double x, y, z;
+};
+GI_HD V mk(double a, double b, double c) { V r; r.x = a; r.y = b; r.z = c; return r; }
+GI_HD V ld3(const double *p) { return mk(p[0], p[1], p[2]); }
+GI_HD V operator+(V a, V b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+GI_HD V operator-(V a, V b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+GI_HD V operator-(V a) { return mk(-a.x, -a.y, -a.z); }
+GI_HD V operator*(V a, double s) { return mk(a.x * s, a.y * s, a.z * s); }
+GI_HD V operator*(double s, V a) { return mk(s * a.x, s * a.y, s * a.z); }
+GI_HD V operator/(V a, double s) { return mk(a.x / s, a.y / s, a.z / s); }
+GI_HD double dot(V a, V b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+GI_HD V cross(V a, V b) {
+  return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+GI_HD double len(V a) { return sqrt((a.x * a.x) + (a.y * a.y) + (a.z * a.z)); }
+GI_HD V normalize(V a) {  // R3Vector::Normalize, R3Vector.cpp:232-239
+  double l = len(a);
+  if (l == 0.0) return a;
+  return mk(a.x / l, a.y / l, a.z / l);
+}
+GI_HD double dist(V a, V b) { return len(a - b); }
+GI_HD double comp(V a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+
+// RGB in fp64 (RNRgb)
+struct C3 {
+  double r, g, b;
+};
+GI_HD C3 rgb(double a, double b, double c) { C3 o; o.r = a; o.g = b; o.b = c; return o; }
+GI_HD C3 ldc(const double *p) { return rgb(p[0], p[1], p[2]); }
+GI_HD C3 operator+(C3 a, C3 b) { return rgb(a.r + b.r, a.g + b.g, a.b + b.b); }
+GI_HD C3 operator*(C3 a, C3 b) { return rgb(a.r * b.r, a.g * b.g, a.b * b.b); }
+GI_HD C3 operator*(C3 a, double s) { return rgb(a.r * s, a.g * s, a.b * s); }
+GI_HD C3 operator*(double s, C3 a) { return rgb(s * a.r, s * a.g, s * a.b); }
+GI_HD C3 operator/(C3 a, double s) { return rgb(a.r / s, a.g / s, a.b / s); }
+GI_HD void operator+=(C3 &a, C3 b) { a.r += b.r; a.g += b.g; a.b += b.b; }
+GI_HD void operator*=(C3 &a, C3 b) { a.r *= b.r; a.g *= b.g; a.b *= b.b; }
+GI_HD void operator*=(C3 &a, double s) { a.r *= s; a.g *= s; a.b *= s; }
+GI_HD double maxch(C3 c) {  // MaxChannelVal, graphics_utils.cpp:39-46
+  double m = 0;
+  if (c.r > m) m = c.r;
+  if (c.g > m) m = c.g;
+  if (c.b > m) m = c.b;
+  return m;
+}
+
+// RNScalar.h tolerant predicates
+GI_HD bool isPos(double s) { return s > kEps; }
+GI_HD bool isNeg(double s) { return s < -kEps; }
+GI_HD bool isPosOrZero(double s) { return s >= -kEps; }
+GI_HD bool isNegOrZero(double s) { return s <= kEps; }
+GI_HD bool isZero(double s) { return isPosOrZero(s) && isNegOrZero(s); }
+
+// ---------------------------------------------------------------------------------------
+// Scene view passed to kernels by value
+// ---------------------------------------------------------------------------------------
+struct SceneView {
+  const DNode *nodes;
+  const DElement *elems;
+  const DShape *shapes;
+  const DTri *tris;
+  const DMaterial *mats;
+  const DLight *lights;
+  int32_t nnodes, nelems, nlights, pad;
+  double radius;
+  double centroid[3];
+  double ambient[3];
+  double background[3];
+  DCamera cam;
+};
+
+// ---------------------------------------------------------------------------------------
+// Intersection (R3Isect.cpp, R3Cont.cpp)
+// ---------------------------------------------------------------------------------------
+GI_HD bool box_contains(const double *mn, const double *mx, V p) {  // R3Cont.cpp:776-787
+  if (mn[0] > mx[0] || mn[1] > mx[1] || mn[2] > mx[2]) return false;
+  if (isNeg(p.x - mn[0]) || isNeg(p.y - mn[1]) || isNeg(p.z - mn[2])) return false;
+  if (isPos(p.x - mx[0]) || isPos(p.y - mx[1]) || isPos(p.z - mx[2])) return false;
+  return true;
+}
+
+// R3Intersects(ray, box), R3Isect.cpp:883-942
+__device__ __noinline__ bool ray_box(V o, V d, const double *mn, const double *mx, double *t_out,
+                                     V *n_out) {
+  if (mn[0] > mx[0] || mn[1] > mx[1] || mn[2] > mx[2]) return false;
+  bool inside = box_contains(mn, mx, o);
+  double oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
+#pragma unroll
+  for (int dim = 0; dim < 3; dim++) {
+    double tval;
+    if (isPos(dd[dim])) {
+      double bc = inside ? mx[dim] : mn[dim];
+      double delta = bc - oo[dim];
+      if (delta < 0.0) continue;
+      tval = delta / dd[dim];
+    } else if (isNeg(dd[dim])) {
+      double bc = inside ? mn[dim] : mx[dim];
+      double delta = bc - oo[dim];
+      if (delta > 0.0) continue;
+      tval = delta / dd[dim];
+    } else {
+      continue;
+    }
+    int d1 = (dim + 1) % 3, d2 = (dim + 2) % 3;
+    double p1 = oo[d1] + dd[d1] * tval;
+    double p2 = oo[d2] + dd[d2] * tval;
+    if (isNegOrZero(p1 - mx[d1]) && isPosOrZero(p1 - mn[d1]) && isNegOrZero(p2 - mx[d2]) &&
+        isPosOrZero(p2 - mn[d2])) {
+      if (t_out) *t_out = tval;
+      if (n_out) {
+        double ax[3] = {0, 0, 0};
+        ax[dim] = isNeg(dd[dim]) ? 1.0 : -1.0;
+        *n_out = mk(ax[0], ax[1], ax[2]);
+      }
+      return true;
+    }
+  }
+  return false;
+}
+
+// R3Intersects(ray, triangle) = plane (R3Isect.cpp:700-732) + R3Contains(triangle)
+// (R3Cont.cpp:491-512); edge planes precomputed on the host with the same arithmetic.
+GI_HD bool ray_tri(V o, V d, const DTri &tr, double &t, V &p) {
+  V n = ld3(tr.n);
+  double denom = dot(n, d);
+  if (isZero(denom)) return false;
+  double s = -(dot(o, n) + tr.d) / denom;
+  if (isNeg(s)) return false;
+  V q = o + d * s;
+  if (!box_contains(tr.bmin, tr.bmax, q)) return false;
+  if (!isZero(q.x * n.x + q.y * n.y + q.z * n.z + tr.d)) return false;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    if (isNeg(q.x * tr.ev[i][0] + q.y * tr.ev[i][1] + q.z * tr.ev[i][2] + tr.ed[i])) return false;
+  }
+  t = s;
+  p = q;
+  return true;
+}
+
+// R3Intersects(ray, sphere), R3Isect.cpp:975-1021
+GI_HD bool ray_sphere(V o, V d, V c, double r, double &t, V &p, V &nrm) {
+  V v0 = c - o;
+  double r2 = r * r;
+  double d2 = v0.x * v0.x + v0.y * v0.y + v0.z * v0.z;
+  bool inside = isNegOrZero(d2 - r2);
+  double v = dot(v0, d);
+  if (!inside && isNegOrZero(v)) return false;
+  double disc = r2 - (dot(v0, v0) - v * v);
+  if (isNeg(disc)) return false;
+  double dd = sqrt(disc);
+  t = inside ? v + dd : v - dd;
+  p = o + t * d;
+  nrm = (p - c) / r;
+  return true;
+}
+
+// R3Intersects(ray, circle), R3Isect.cpp:837-879
+GI_HD bool ray_circle(V o, V d, V c, V n, double r, double &t, V &p) {
+  if (r < 0) return false;
+  double pd = -(n.x * c.x + n.y * c.y + n.z * c.z);
+  double denom = dot(n, d);
+  if (isZero(denom)) return false;
+  double s = -(dot(o, n) + pd) / denom;
+  if (isNeg(s)) return false;
+  V q = o + d * s;
+  V v = c - q;
+  double dd = v.x * v.x + v.y * v.y + v.z * v.z;
+  if (isPos(dd - r * r)) return false;
+  t = s;
+  p = q;
+  return true;
+}
+
+// R3Shape::Intersects dispatch (R3Shape.cpp:328-329); SK_MESH is R3Intersects(ray,
+// R3TriangleArray) (R3Isect.cpp:800-833): min t over ALL triangles, t >= -1e-6 allowed (Q2).
+__device__ __noinline__ bool shape_intersect(const SceneView &S, const DShape &sh, V o, V d,
+                                             double &t, V &p, V &n) {
+  switch (sh.kind) {
+    case SK_TRI: {
+      const DTri &tr = S.tris[sh.tri_first];
+      if (!ray_tri(o, d, tr, t, p)) return false;
+      n = ld3(tr.n);
+      return true;
+    }
+    case SK_MESH: {
+      if (!ray_box(o, d, sh.bmin, sh.bmax, nullptr, nullptr)) return false;
+      bool found = false;
+      double mt = 3.40282346638528859811704183484516925440e+38;  // FLT_MAX
+      for (int i = 0; i < sh.tri_count; i++) {
+        const DTri &tr = S.tris[sh.tri_first + i];
+        double tt;
+        V pp;
+        if (ray_tri(o, d, tr, tt, pp)) {
+          if (tt < mt) {
+            found = true;
+            p = pp;
+            n = ld3(tr.n);
+            mt = tt;
+          }
+        }
+      }
+      t = mt;
+      return found;
+    }
+    case SK_SPHERE:
+      return ray_sphere(o, d, ld3(sh.c), sh.r, t, p, n);
+    case SK_BOX: {
+      double tt;
+      V nn;
+      if (!ray_box(o, d, sh.bmin, sh.bmax, &tt, &nn)) return false;
+      t = tt;
+      p = o + d * tt;
+      n = nn;
+      return true;
+    }
+    case SK_CIRCLE:
+      if (!ray_circle(o, d, ld3(sh.c), ld3(sh.n), sh.r, t, p)) return false;
+      n = ld3(sh.n);
+      return true;
+    default:
+      return false;
+  }
+}
+
+GI_HD V xf_point(const double *m, V p) {
+  return mk(m[0] * p.x + m[1] * p.y + m[2] * p.z + m[3], m[4] * p.x + m[5] * p.y + m[6] * p.z + m[7],
+            m[8] * p.x + m[9] * p.y + m[10] * p.z + m[11]);
+}
+GI_HD V xf_vec(const double *m, V v) {
+  return mk(m[0] * v.x + m[1] * v.y + m[2] * v.z, m[4] * v.x + m[5] * v.y + m[6] * v.z,
+            m[8] * v.x + m[9] * v.y + m[10] * v.z);
+}
+
+struct Hit {
+  V p, n;
+  double t;
+  int mat;
+};
+
+// R3Scene::Intersects (R3Scene.cpp:471-479) -> R3SceneNode::Intersects (R3SceneNode.cpp:
+// 420-510) -> R3SceneElement::Intersects (R3SceneElement.cpp:209-243), flattened: elements are
+// visited in the graph's pre-order; an element "hits" only if it strictly improves on the
+// current closest t (its "closest_t == max_t -> FALSE" rule), so earlier elements win ties.
+// Ray direction is renormalised per graph level (R3Line::InverseTransform, R3Line.cpp:140).
+__device__ __noinline__ bool scene_intersect(const SceneView &S, V org, V dir, Hit &h) {
+  double closest = kInf;  // world-frame t (rigid transforms keep t; scale handled below)
+  bool found = false;
+  V hp = mk(0, 0, 0), hn = mk(0, 0, 0);
+  int hnode = 0, hmat = -1;
+  for (int ni = 0; ni < S.nnodes; ni++) {
+    const DNode &nd = S.nodes[ni];
+    if (nd.elem_count == 0) continue;
+    // local ray: walk the parent chain (depth is tiny in .scn files)
+    int chain[8];
+    int depth = 0;
+    for (int c = ni; c >= 0 && depth < 8; c = S.nodes[c].parent) chain[depth++] = c;
+    V lo = org, ldir = dir;
+    double scale = 1.0;
+    bool ok = true;
+    for (int k = depth - 1; k >= 0; k--) {
+      const DNode &a = S.nodes[chain[k]];
+      double lv;
+      if (a.identity) {
+        lv = len(ldir);
+        ldir = normalize(ldir);
+      } else {
+        lv = len(xf_vec(a.T, ldir));
+        lo = xf_point(a.Tinv, lo);
+        ldir = normalize(xf_vec(a.Tinv, ldir));
+      }
+      if (isNegOrZero(lv)) { ok = false; break; }
+      if (!isZero(lv - 1.0)) scale *= lv;
+    }
+    if (!ok) continue;
+    for (int ei = 0; ei < nd.elem_count; ei++) {
+      const DElement &el = S.elems[nd.elem_first + ei];
+      double maxt = closest / scale;
+      if (!box_contains(el.bmin, el.bmax, lo)) {
+        double bt;
+        if (!ray_box(lo, ldir, el.bmin, el.bmax, &bt, nullptr)) continue;
+        if (isPos(bt - maxt)) continue;
+      }
+      double ec = maxt;
+      V ep = mk(0, 0, 0), en = mk(0, 0, 0);
+      for (int si = 0; si < el.shape_count; si++) {
+        double t;
+        V p, n;
+        if (shape_intersect(S, S.shapes[el.shape_first + si], lo, ldir, t, p, n)) {
+          if ((t >= 0.0) && (t <= ec)) {
+            ep = p;
+            en = n;
+            ec = t;
+          }
+        }
+      }
+      if (ec == maxt) continue;
+      found = true;
+      closest = ec * scale;
+      hp = ep;
+      hn = en;
+      hnode = ni;
+      hmat = el.material;
+    }
+  }
+  if (!found) return false;
+  // transform hit point / normal back to world (Q11: normal by the forward affine)
+  for (int c = hnode; c >= 0; c = S.nodes[c].parent) {
+    const DNode &a = S.nodes[c];
+    if (!a.identity) {
+      hp = xf_point(a.T, hp);
+      hn = xf_vec(a.T, hn);
+    }
+    hn = normalize(hn);
+  }
+  h.p = hp;
+  h.n = hn;
+  h.t = closest;
+  h.mat = hmat;
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------
+// Optics and sampling (utils/graphics_utils.cpp)
+// ---------------------------------------------------------------------------------------
+GI_HD double reflection_coeff(double ir_air, double cos_theta, double ir_mat) {  // :95-101
+  double r0 = pow((ir_air - ir_mat) / (ir_air + ir_mat), 2.0);
+  return (r0 + (1.0 - r0) * pow((1.0 - fabs(cos_theta)), 5.0));
+}
+GI_HD V reflective_bounce(V n, V view, double ct) {  // :104-117
+  if (ct < 0) { n = -n; ct *= -1.0; }
+  V perp = n * ct;
+  V r = view + perp * 2.0;
+  return normalize(r);
+}
+GI_HD V transmissive_bounce(double ir_air, V n, V view, double ct, double ir_mat) {  // :121-154
+  double eta;
+  if (ct < 0) {
+    eta = ir_mat / ir_air;
+    n = -n;
+    ct *= -1.0;
+  } else {
+    eta = ir_air / ir_mat;
+  }
+  double theta = acos(ct);
+  double sin_phi = eta * sin(theta);
+  if (sin_phi < -1.0 || 1.0 < sin_phi) return reflective_bounce(n, view, ct);
+  double phi = asin(sin_phi);
+  V par = normalize(view + n * ct);
+  V refr = par * tan(phi) - n;
+  return normalize(refr);
+}
+GI_HD V rotate(V v, V axis, double theta) {  // R3Vector::Rotate, R3Vector.cpp:352-363
+  double ct = cos(theta);
+  double d = dot(v, axis);
+  V cr = cross(v, axis);
+  v = v * ct;
+  v = v + axis * d * (1.0 - ct);
+  v = v - cr * sin(theta);
+  return v;
+}
+GI_HD V diffuse_sample(V n, double ct, Rng &rng) {  // Diffuse_ImportanceSample :162-185
+  if (ct < 0) n = -n;
+  double theta = acos(sqrt(rng.next()));
+  double phi = 2 * kPi * rng.next();
+  V perp = mk(n.y, -n.x, 0);
+  if (1.0 - fabs(n.z) < 0.1) perp = mk(n.z, 0, -n.x);
+  perp = normalize(perp);
+  V r = perp * sin(theta) + n * cos(theta);
+  r = rotate(r, n, phi);
+  return normalize(r);
+}
+GI_HD V specular_sample(V ex, double nsh, double ct, Rng &rng) {  // :189-216
+  double lim = (1.0 - acos(fabs(ct)) * 2.0 / kPi);
+  double alpha = acos(pow(rng.next(), 1.0 / (nsh + 1.0))) * lim;
+  double phi = 2.0 * kPi * rng.next();
+  V perp = mk(ex.y, -ex.x, 0);
+  if (1.0 - fabs(ex.z) < 0.1) perp = mk(ex.z, 0, -ex.x);
+  perp = normalize(perp);
+  V r = perp * sin(alpha) + ex * cos(alpha);
+  r = rotate(r, ex, phi);
+  return normalize(r);
+}
+
+// ---------------------------------------------------------------------------------------
+// Direct illumination (utils/illumination_utils.cpp, R3*Light::Reflection)
+// ---------------------------------------------------------------------------------------
+struct Flags {  // the rendering globals a kernel needs (photonmap.cpp:40-106)
+  int32_t ambient, direct, transmissive, specular, indirect, caustic, photon_viz, fast_global;
+  int32_t cache, shadows, soft_shadows, light_test, shadow_test, monte_carlo, max_monte_depth;
+  int32_t recursive_shadows, distrib_trans, trans_test, distrib_spec, spec_test, fresnel;
+  int32_t indirect_test, dof, dof_test, max_photon_depth, pad;
+  double ir_air, prob_absorb;
+  uint64_t seed;
+};
+
+struct Counts {  // per-thread -v counters (render.cpp:26-32)
+  uint32_t shadow, monte, trans, spec, indirect, caustic;
+};
+
+// RayIlluminationTest, illumination_utils.cpp:16-31 (Q13 distance equality)
+__device__ __noinline__ bool illum_test(const SceneView &S, V p_scene, V p_light, Counts &cnt) {
+  double unocc = dist(p_light, p_scene);
+  V d = normalize(p_scene - p_light);
+  Hit h;
+  double l = scene_intersect(S, p_light, d, h) ? dist(p_light, h.p) : kInf;
+  cnt.shadow++;
+  return fabs(l - unocc) < kEps;
+}
+
+// TestLightIntersection, illumination_utils.cpp:35-84
+GI_HD int light_self_test(V p, V eye, const DLight &L) {
+  if (L.kind == LK_AREA) {
+    V v = p - ld3(L.pos);
+    double vl = len(v);
+    v = normalize(v);
+    V nn = ld3(L.dir);
+    if (fabs(dot(v, nn)) < kEps && vl <= L.radius) return (dot(nn, eye - p) <= 0) ? -1 : 1;
+  } else if (L.kind == LK_RECT) {
+    V v = p - ld3(L.pos);
+    double c1 = dot(v, ld3(L.a1)), c2 = dot(v, ld3(L.a2));
+    v = normalize(v);
+    V nn = ld3(L.dir);
+    if (fabs(dot(v, nn)) < kEps && fabs(c1 * 2.0) <= L.len1 && fabs(c2 * 2.0) <= L.len2)
+      return (dot(nn, eye - p) <= 0) ? -1 : 1;
+  }
+  return 0;
+}
+
+// sample a point on an area (disk, rejection) or rect light (illumination_utils.cpp:150-157,
+// 315-319): ((r1*u + r2*v) + center) + n*eps
+GI_HD V light_sample_point(const DLight &L, Rng &rng) {
+  double r1, r2;
+  if (L.kind == LK_AREA) {
+    do {
+      r1 = (rng.next() * 2.0) - 1.0;
+      r2 = (rng.next() * 2.0) - 1.0;
+    } while (r1 * r1 + r2 * r2 > 1.0);
+  } else {
+    r1 = rng.next() - 0.5;
+    r2 = rng.next() - 0.5;
+  }
+  return ((r1 * ld3(L.su) + r2 * ld3(L.sv)) + ld3(L.pos)) + ld3(L.dir) * kEps;
+}
+
+// ComputeAreaLightReflection / ComputeRectLightReflection, illumination_utils.cpp:91-417
+// (Q1: the whole accumulated colour is scaled by the shadow hit rate)
+__device__ __noinline__ void soft_light(const SceneView &S, const DLight &L, C3 &color,
+                                        const DMaterial &m, V eye, V p, V nrm, int nls, int nes,
+                                        Rng &rng, Counts &cnt) {
+  if (!L.active) return;
+  V center = ld3(L.pos), ln = ld3(L.dir);
+  if (dot(ln, p - center) < 0) return;
+  int tot_s = 0, tot_h = 0;
+  if (m.flags & MF_DIFFUSE) {
+    double w = 0;
+    int hits = 0;
+    for (int i = 0; i < nls; i++) {
+      V sp = light_sample_point(L, rng);
+      if (illum_test(S, p, sp, cnt)) {
+        hits++;
+        double I = L.intensity;
+        double dd = dist(p, sp);
+        double den = L.ca;
+        den += dd * L.la;
+        den += dd * dd * L.qa;
+        if (isPos(den)) I /= den;
+        V Ld = normalize(sp - p);
+        I *= dot(ln, -Ld) * 2.0;
+        w += I * fabs(dot(nrm, Ld));
+      }
+    }
+    if (hits > 0) color += w * ldc(m.kd) * ldc(L.color) * L.area / (double)hits;
+    tot_h += hits;
+    tot_s += nls;
+  }
+  if (m.flags & MF_SPECULAR) {
+    double w = 0;
+    int hits = 0;
+    int n2 = nls * 2;
+    V Vv = normalize(eye - p);
+    for (int i = 0; i < n2; i++) {
+      V sp = light_sample_point(L, rng);
+      if (illum_test(S, p, sp, cnt)) {
+        hits++;
+        double I = L.intensity;
+        double dd = dist(p, sp);
+        double den = L.ca;
+        den += dd * L.la;
+        den += dd * dd * L.qa;
+        if (isPos(den)) I /= den;
+        V Ld = normalize(sp - p);
+        I *= dot(ln, -Ld) * 2.0;
+        double NL = dot(nrm, Ld);
+        V R = (2.0 * NL) * nrm - Ld;
+        double VR = dot(Vv, R);
+        if (isNegOrZero(VR)) continue;
+        w += (I * pow(VR, m.n));
+      }
+    }
+    if (hits > 0) color += w * ldc(m.ks) * ldc(L.color) * L.area / (double)hits;
+    tot_h += hits;
+    tot_s += n2;
+  }
+  int hits = 0;
+  for (int i = 0; i < nes; i++) {
+    V sp = light_sample_point(L, rng);
+    if (illum_test(S, p, sp, cnt)) hits++;
+  }
+  tot_h += hits;
+  tot_s += nes;
+  if (tot_s > 0) color *= ((double)tot_h) / tot_s;
+}
+
+// Light::Reflection: point/spot (R3PointLight.cpp:213-244, IntensityAtPoint :111-121,
+// R3SpotLight.cpp:105-115), directional (R3DirectionalLight.cpp:134-166), area/rect without
+// shadows (R3AreaLight.cpp:122-330, R3RectLight.cpp:150-340)
+__device__ __noinline__ C3 light_reflection(const DLight &L, const DMaterial &m, V eye, V p,
+                                            V nrm, int max_samples, Rng &rng) {
+  if (!L.active) return rgb(0, 0, 0);
+  C3 Dc = ldc(m.kd), Sc = ldc(m.ks), Ic = ldc(L.color);
+  double s = m.n;
+  if (L.kind == LK_POINT || L.kind == LK_SPOT) {
+    V lp = ld3(L.pos);
+    double dd = dist(p, lp);
+    double den = L.ca;
+    den += dd * L.la;
+    den += dd * dd * L.qa;
+    double I = isZero(den) ? L.intensity : (L.intensity / den);
+    if (L.kind == LK_SPOT) {
+      V ML = normalize(p - lp);
+      double ca = dot(ML, ld3(L.dir));
+      if (cos(L.cutoff) > ca) I = 0.0;
+      else I = I * pow(ca, L.dropoff);
+    }
+    V Ld = normalize(lp - p);
+    double NL = dot(nrm, Ld);
+    V R = (2.0 * NL) * nrm - Ld;
+    V Vv = normalize(eye - p);
+    double VR = dot(Vv, R);
+    C3 o = I * Dc * Ic * fabs(NL);
+    if (isPos(VR)) o += (I * pow(VR, s)) * Sc * Ic;
+    return o;
+  }
+  if (L.kind == LK_DIR) {
+    double I = L.intensity;
+    V Ld = -ld3(L.dir);
+    double NL = dot(nrm, Ld);
+    V R = (2.0 * NL) * nrm - Ld;
+    V Vv = normalize(eye - p);
+    double VR = dot(Vv, R);
+    C3 o = (I * fabs(NL)) * Dc * Ic;
+    if (isPos(VR)) o += (I * pow(VR, s) * Sc * Ic);
+    return o;
+  }
+  bool area = (L.kind == LK_AREA);
+  V dirn = ld3(L.dir), center = ld3(L.pos);
+  if (dot(dirn, p - center) < 0) return rgb(0, 0, 0);
+  V ax1 = ld3(L.nr_ax1), ax2 = ld3(L.nr_ax2);
+  C3 out = rgb(0, 0, 0);
+  for (int pass = 0; pass < 2; pass++) {
+    bool spec = (pass == 1);
+    int count = 0;
+    C3 sum = rgb(0, 0, 0);
+    int target = spec ? 2 * max_samples : max_samples;
+    for (int i = 0; (spec ? i < target : count < target); i++) {
+      double r1, r2;
+      if (area) {
+        r1 = (rng.next() * 2.0) - 1.0;
+        r2 = (rng.next() * 2.0) - 1.0;
+        if (r1 * r1 + r2 * r2 > 1) continue;
+      } else {
+        r1 = rng.next() - 0.5;
+        r2 = rng.next() - 0.5;
+      }
+      V sp = center;
+      sp = sp + r1 * ax1;
+      sp = sp + r2 * ax2;
+      count++;
+      double I = L.intensity;
+      double dd = dist(p, sp);
+      double den = L.ca;
+      den += dd * L.la;
+      den += dd * dd * L.qa;
+      if (isPos(den)) I /= den;
+      V Ld = normalize(sp - p);
+      I *= dot(dirn, -Ld) * 2.0;
+      double NL = dot(nrm, Ld);
+      if (!spec) {
+        sum += (I * fabs(NL)) * Dc * Ic;
+      } else {
+        V R = (2.0 * NL) * nrm - Ld;
+        V Vv = normalize(eye - p);
+        double VR = dot(Vv, R);
+        if (isNegOrZero(VR)) continue;
+        sum += (I * pow(VR, s) * Sc * Ic);
+      }
+    }
+    C3 mean = sum;
+    if (count > 0) mean = mean / (double)count;
+    out += L.area * mean;
+  }
+  return out;
+}
+
+// ComputeIllumination, illumination_utils.cpp:425-494
+__device__ __noinline__ void compute_illumination(const SceneView &S, const Flags &F, C3 &color,
+                                                  const DLight &L, const DMaterial &m, V eye,
+                                                  V p, V nrm, double ct, bool inMC, Rng &rng,
+                                                  Counts &cnt) {
+  bool shadows = F.shadows && (!inMC || (F.recursive_shadows && inMC));
+  int nls = F.light_test, nes = F.shadow_test;
+  if (inMC) { nls = 2; nes = 0; }  // Q14
+  if (!shadows) {
+    color += light_reflection(L, m, eye, p, nrm, nls, rng);
+    return;
+  }
+  V pol;
+  if (L.kind == LK_DIR) {
+    pol = p - ld3(L.dir) * S.radius * 3.0;
+  } else if (L.kind == LK_POINT || L.kind == LK_SPOT) {
+    pol = ld3(L.pos);
+  } else {
+    if (!F.soft_shadows) {
+      pol = ld3(L.pos) + kEps * ld3(L.dir);
+    } else {
+      soft_light(S, L, color, m, eye, p, nrm, nls, nes, rng, cnt);
+      return;
+    }
+  }
+  double side = dot(nrm, pol - p);
+  if ((side > 0 && ct < 0) || (side < 0 && ct > 0)) return;
+  if (illum_test(S, p, pol, cnt)) color += light_reflection(L, m, eye, p, nrm, nls, rng);
+}
+
+// DirectIllumination, raytracer.cpp:18-44
+__device__ __noinline__ void direct_illumination(const SceneView &S, const Flags &F, V p, V nrm,
+                                                 V eye, C3 &color, const DMaterial &m, double ct,
+                                                 bool inMC, Rng &rng, Counts &cnt) {
+  bool emit = true;
+  for (int k = 0; k < S.nlights; k++) {
+    const DLight &L = S.lights[k];
+    int li = light_self_test(p, eye, L);
+    if (li != 0) {
+      if (li == -1) emit = false;
+      continue;
+    }
+    compute_illumination(S, F, color, L, m, eye, p, nrm, ct, inMC, rng, cnt);
+  }
+  if (emit) color += ldc(m.e);
+}
+
+}  // namespace gi

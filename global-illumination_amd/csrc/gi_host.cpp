@@ -1,0 +1,1028 @@
+// gi_host.cpp -- host orchestration of the MI355X renderer and the C-ABI of include/gi.h.
+//
+// Replaces the reference's host-side driver code: MapPhotons (photonmap.cpp:260-436) and
+// RenderImage (render.cpp:155-259). The CPU threads of the reference become batched
+// wavefront launches; host code only sequences kernels, runs the adaptive photon-emission
+// bookkeeping and builds the kd-tree (kd build on the GPU is SURVEY.md §8(f) row f1).
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cfloat>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+#include "../../include/gi.h"
+#include "gi_kernels.h"
+#include "gi_scene.h"
+
+using namespace gi;
+
+namespace {
+
+// ---------------------------------------------------------------------------------------
+// small device-buffer helper
+// ---------------------------------------------------------------------------------------
+struct DBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap && p) return hipSuccess;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max(bytes, (size_t)256);
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T> T *as() const { return reinterpret_cast<T *>(p); }
+};
+
+// RNRgb_to_RGBE / RGBE_to_RNRgb (graphics_utils.cpp:50-77), host side
+void rgbe_enc(const double c[3], uint8_t *out) {
+  double mx = 0;
+  for (int i = 0; i < 3; i++)
+    if (c[i] > mx) mx = c[i];
+  if (!(mx > 0)) { out[0] = out[1] = out[2] = out[3] = 0; return; }
+  int e;
+  double m = frexp(mx, &e);
+  out[0] = (uint8_t)(256.0 * c[0] / mx * m);
+  out[1] = (uint8_t)(256.0 * c[1] / mx * m);
+  out[2] = (uint8_t)(256.0 * c[2] / mx * m);
+  out[3] = (uint8_t)(e + 128);
+}
+void rgbe_dec(const uint8_t *in, double c[3]) {
+  if (!in[3]) { c[0] = c[1] = c[2] = 0; return; }
+  double inv = ldexp(1.0, ((int)in[3]) - 128 - 8);
+  for (int i = 0; i < 3; i++) c[i] = (double)in[i] * inv;
+}
+
+// ---------------------------------------------------------------------------------------
+// photon map: host kd build of an implicit complete tree (leaf l holds photons
+// [l*n/L, (l+1)*n/L)); split = median of the node's range along its longest bbox axis.
+// Any kd-tree gives the same k-NN set (up to ties at the k-th distance, broken here by
+// (d2, kd-order index)); the reference's tree is R3Kdtree.cpp:1552-1671.
+// ---------------------------------------------------------------------------------------
+struct HostMap {
+  std::vector<gi_photon> storage;  // emission order
+  std::vector<int32_t> perm;       // kd order -> storage index
+  std::vector<float> pos4;
+  std::vector<uint32_t> rgbe;
+  std::vector<float> nodes;  // float2 per node
+  int nleaves = 1, levels = 0;
+  float bmin[3] = {0, 0, 0}, bmax[3] = {0, 0, 0};
+};
+
+void kd_rec(HostMap &M, int node, int a, int b, int depth_par) {
+  int64_t n = (int64_t)M.storage.size();
+  int L = M.nleaves;
+  if (node >= L) return;
+  int64_t lo = (int64_t)a * n / L, hi = (int64_t)b * n / L;
+  int midleaf = (a + b) / 2;
+  int64_t mid = (int64_t)midleaf * n / L;
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int64_t i = lo; i < hi; i++) {
+    const float *p = M.storage[M.perm[i]].pos;
+    for (int k = 0; k < 3; k++) { mn[k] = std::min(mn[k], p[k]); mx[k] = std::max(mx[k], p[k]); }
+  }
+  int axis = 0;
+  float ext = mx[0] - mn[0];
+  if (mx[1] - mn[1] > ext) { axis = 1; ext = mx[1] - mn[1]; }
+  if (mx[2] - mn[2] > ext) axis = 2;
+  float split = 0.f;
+  if (hi > lo && mid < hi) {
+    std::nth_element(M.perm.begin() + lo, M.perm.begin() + mid, M.perm.begin() + hi,
+                     [&](int x, int y) { return M.storage[x].pos[axis] < M.storage[y].pos[axis]; });
+    split = M.storage[M.perm[mid]].pos[axis];
+  } else if (hi > lo) {
+    split = mx[axis];
+  }
+  M.nodes[2 * node] = split;
+  int ai = axis;
+  memcpy(&M.nodes[2 * node + 1], &ai, 4);
+  if (depth_par > 0) {
+    std::thread t([&]() { kd_rec(M, 2 * node, a, midleaf, depth_par - 1); });
+    kd_rec(M, 2 * node + 1, midleaf, b, depth_par - 1);
+    t.join();
+  } else {
+    kd_rec(M, 2 * node, a, midleaf, 0);
+    kd_rec(M, 2 * node + 1, midleaf, b, 0);
+  }
+}
+
+void kd_build(HostMap &M, int leaf_size, int threads) {
+  int64_t n = (int64_t)M.storage.size();
+  M.nleaves = 1;
+  M.levels = 0;
+  while ((int64_t)M.nleaves * leaf_size < n) { M.nleaves *= 2; M.levels++; }
+  M.perm.resize(n);
+  for (int64_t i = 0; i < n; i++) M.perm[i] = (int32_t)i;
+  M.nodes.assign(2 * (size_t)M.nleaves, 0.0f);
+  int par = 0;
+  while ((1 << par) < threads && par < 4) par++;
+  if (n > 0) kd_rec(M, 1, 0, M.nleaves, par);
+  M.pos4.resize(4 * (size_t)n);
+  M.rgbe.resize(n);
+  for (int k = 0; k < 3; k++) { M.bmin[k] = FLT_MAX; M.bmax[k] = -FLT_MAX; }
+  for (int64_t i = 0; i < n; i++) {
+    const gi_photon &p = M.storage[M.perm[i]];
+    uint32_t w = (uint32_t)p.dir | ((uint32_t)p.flags << 16);
+    M.pos4[4 * i] = p.pos[0];
+    M.pos4[4 * i + 1] = p.pos[1];
+    M.pos4[4 * i + 2] = p.pos[2];
+    memcpy(&M.pos4[4 * i + 3], &w, 4);
+    memcpy(&M.rgbe[i], p.rgbe, 4);
+    for (int k = 0; k < 3; k++) {
+      M.bmin[k] = std::min(M.bmin[k], p.pos[k]);
+      M.bmax[k] = std::max(M.bmax[k], p.pos[k]);
+    }
+  }
+}
+
+struct DevMap {
+  DBuf pos4, rgbe, nodes;
+  int64_t n = 0;
+  int nleaves = 1, levels = 0;
+  KdView view() const {
+    KdView v;
+    v.pos4 = pos4.as<float>();
+    v.rgbe = rgbe.as<uint32_t>();
+    v.nodes = nodes.as<float>();
+    v.n = n;
+    v.nleaves = nleaves;
+    v.levels = levels;
+    for (int k = 0; k < 3; k++) v.bmin[k] = v.bmax[k] = 0;
+    return v;
+  }
+};
+
+}  // namespace
+
+// =======================================================================================
+struct gi_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  gi_params P;
+  bool have_params = false;
+  bool have_scene = false;
+  HostScene scene;
+  // device scene
+  DBuf d_nodes, d_elems, d_shapes, d_tris, d_mats, d_lights, d_lut, d_stats;
+  // photon maps
+  HostMap hmap[2];
+  DevMap dmap[2];
+  bool map_valid[2] = {false, false};
+  int leaf_size = 16;
+  // render scratch
+  DBuf spawn, npaths, path_off, cnt_g, cnt_c, goff, coff, base, gpos, cpos, gshade, cshade, gout,
+      cout, pixels, rgbf, rgb8, gheap_d2, gheap_idx, perm;
+  DBuf scan_lvl[8], scan_out[8];
+  // photon tracing scratch
+  DBuf pcounts, poffs, pbuf;
+  int64_t prim_per_batch = 1 << 17;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+#define HIPCHK(ctx, call)                                                        \
+  do {                                                                           \
+    hipError_t _e = (call);                                                      \
+    if (_e != hipSuccess) {                                                      \
+      (ctx)->err = std::string("HIP error: ") + hipGetErrorString(_e) + " at " + \
+                   __FILE__ + ":" + std::to_string(__LINE__);                    \
+      return GI_ERR_HIP;                                                         \
+    }                                                                            \
+  } while (0)
+
+namespace {
+
+int fail(gi_ctx *c, int code, const std::string &msg) {
+  c->err = msg;
+  return code;
+}
+
+Flags make_flags(const gi_params &P) {
+  Flags F;
+  memset(&F, 0, sizeof F);
+  F.ambient = P.ambient; F.direct = P.direct_illum; F.transmissive = P.transmissive_illum;
+  F.specular = P.specular_illum; F.indirect = P.indirect_illum; F.caustic = P.caustic_illum;
+  F.photon_viz = P.direct_photon_illum; F.fast_global = P.fast_global;
+  F.cache = P.irradiance_cache; F.shadows = P.shadows; F.soft_shadows = P.soft_shadows;
+  F.light_test = P.light_test; F.shadow_test = P.shadow_test; F.monte_carlo = P.monte_carlo;
+  F.max_monte_depth = P.max_monte_depth; F.recursive_shadows = P.recursive_shadows;
+  F.distrib_trans = P.distrib_transmissive; F.trans_test = P.transmissive_test;
+  F.distrib_spec = P.distrib_specular; F.spec_test = P.specular_test; F.fresnel = P.fresnel;
+  F.indirect_test = P.indirect_test; F.dof = P.depth_of_field; F.dof_test = P.dof_test;
+  F.max_photon_depth = P.max_photon_depth;
+  F.ir_air = P.ir_air;
+  F.prob_absorb = P.prob_absorb;
+  F.seed = P.seed;
+  return F;
+}
+
+SceneView make_view(gi_ctx *c) {
+  SceneView S;
+  memset(&S, 0, sizeof S);
+  const HostScene &H = c->scene;
+  S.nodes = c->d_nodes.as<DNode>();
+  S.elems = c->d_elems.as<DElement>();
+  S.shapes = c->d_shapes.as<DShape>();
+  S.tris = c->d_tris.as<DTri>();
+  S.mats = c->d_mats.as<DMaterial>();
+  S.lights = c->d_lights.as<DLight>();
+  S.nnodes = (int)H.nodes.size();
+  S.nelems = (int)H.elems.size();
+  S.nlights = (int)H.lights.size();
+  S.radius = H.radius;
+  for (int i = 0; i < 3; i++) {
+    S.centroid[i] = H.centroid[i];
+    S.ambient[i] = H.ambient[i];
+    S.background[i] = H.background[i];
+  }
+  // render.cpp:67-77
+  const gi_params &P = c->P;
+  double tx = tan(H.xfov), ty = tan(H.yfov);
+  double ul = sqrt(H.up[0] * H.up[0] + H.up[1] * H.up[1] + H.up[2] * H.up[2]);
+  double rl = sqrt(H.right[0] * H.right[0] + H.right[1] * H.right[1] + H.right[2] * H.right[2]);
+  for (int i = 0; i < 3; i++) {
+    S.cam.eye[i] = H.eye[i];
+    S.cam.far_org[i] = H.eye[i] + H.towards[i] * P.focus_depth;
+    S.cam.far_right[i] = H.right[i] * tx * P.focus_depth;
+    S.cam.far_up[i] = H.up[i] * ty * P.focus_depth;
+    S.cam.dof_u[i] = (ul == 0.0 ? H.up[i] : H.up[i] / ul) * P.aperture_radius;
+    S.cam.dof_v[i] = (rl == 0.0 ? H.right[i] : H.right[i] / rl) * P.aperture_radius;
+  }
+  return S;
+}
+
+// BuildDirectionLookupTable, photon_utils.cpp:253-272
+void build_lut(std::vector<double> &lut) {
+  lut.assign(65536 * 3, 0.0);
+  const double PI = 3.14159265358979323846;
+  for (int phi = 0; phi < 256; phi++)
+    for (int th = 0; th < 256; th++) {
+      double tp = (phi * (2.0 * PI) / 255.0) - PI;
+      double tt = (th * PI / 255.0);
+      double x = sin(tt) * cos(tp), y = sin(tt) * sin(tp), z = cos(tt);
+      double l = sqrt((x * x) + (y * y) + (z * z));
+      if (l != 0.0) { x /= l; y /= l; z /= l; }
+      int i = 256 * phi + th;
+      lut[3 * i] = x; lut[3 * i + 1] = y; lut[3 * i + 2] = z;
+    }
+}
+
+hipError_t upload(DBuf &b, const void *src, size_t bytes, hipStream_t st) {
+  hipError_t e = b.ensure(bytes);
+  if (e != hipSuccess) return e;
+  if (bytes) return hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, st);
+  return hipSuccess;
+}
+
+ScanTemp scan_temp(gi_ctx *c, int64_t n) {
+  ScanTemp t;
+  memset(&t, 0, sizeof t);
+  int64_t m = n;
+  for (int l = 0; l < 8; l++) {
+    m = (m + 1023) / 1024;
+    c->scan_lvl[l].ensure((size_t)(m + 2) * 4);
+    c->scan_out[l].ensure((size_t)(m + 2) * 4);
+    t.level[l] = c->scan_lvl[l].as<uint32_t>();
+    t.level_out[l] = c->scan_out[l].as<uint32_t>();
+  }
+  t.depth = 0;
+  return t;
+}
+
+int upload_map(gi_ctx *c, int mi) {
+  HostMap &H = c->hmap[mi];
+  DevMap &D = c->dmap[mi];
+  int64_t n = (int64_t)H.storage.size();
+  HIPCHK(c, upload(D.pos4, H.pos4.data(), H.pos4.size() * 4, c->stream));
+  HIPCHK(c, upload(D.rgbe, H.rgbe.data(), H.rgbe.size() * 4, c->stream));
+  HIPCHK(c, upload(D.nodes, H.nodes.data(), H.nodes.size() * 4, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  D.n = n;
+  D.nleaves = H.nleaves;
+  D.levels = H.levels;
+  c->map_valid[mi] = n > 0;
+  return GI_OK;
+}
+
+int set_map(gi_ctx *c, int mi, const gi_photon *ph, int64_t n) {
+  HostMap &H = c->hmap[mi];
+  H = HostMap();
+  H.storage.assign(ph, ph + n);
+  kd_build(H, c->leaf_size, std::max(1, c->P.threads));
+  return upload_map(c, mi);
+}
+
+// LightPower, graphics_utils.cpp:223-258
+double light_power(const HostScene &S, const DLight &L) {
+  const double PI = 3.14159265358979323846;
+  double area = 1.0, flux = 4.0 * PI;
+  if (L.kind == LK_DIR) {
+    area = PI * pow(S.radius, 2.0);
+    flux = 1.0;
+  } else if (L.kind == LK_AREA) {
+    area = PI * pow(L.radius, 2.0);
+    flux /= 2.0;
+  } else if (L.kind == LK_RECT) {
+    double a1[3], a2[3];
+    for (int i = 0; i < 3; i++) { a1[i] = L.a1[i] * L.len1; a2[i] = L.a2[i] * L.len2; }
+    double cx = a1[1] * a2[2] - a1[2] * a2[1], cy = a1[2] * a2[0] - a1[0] * a2[2],
+           cz = a1[0] * a2[1] - a1[1] * a2[0];
+    area = sqrt((cx * cx) + (cy * cy) + (cz * cz));
+    flux /= 2.0;
+  } else if (L.kind == LK_SPOT) {
+    double s = L.dropoff;
+    flux = (2.0 * PI) / (s + 1.0) * (1.0 - pow(cos(L.cutoff), s + 1.0));
+  }
+  return (L.color[0] + L.color[1] + L.color[2]) * area * flux;
+}
+
+// trace photons [e0, e0+n) of one light and append the stored ones (emission order)
+int trace_batch(gi_ctx *c, int caustic, int light, int64_t e0, int64_t n,
+                std::vector<gi_photon> &out) {
+  const int64_t CH = 1 << 22;
+  for (int64_t s = 0; s < n; s += CH) {
+    int64_t m = std::min(CH, n - s);
+    HIPCHK(c, c->pcounts.ensure((size_t)m * 4));
+    HIPCHK(c, c->poffs.ensure((size_t)(m + 1) * 4));
+    PhotonArgs a;
+    memset(&a, 0, sizeof a);
+    a.S = make_view(c);
+    a.F = make_flags(c->P);
+    a.light = light;
+    a.caustic = caustic;
+    a.e0 = e0 + s;
+    a.n = m;
+    a.counts = c->pcounts.as<uint32_t>();
+    a.offsets = c->poffs.as<uint32_t>();
+    launch_photons(a, false, c->stream);
+    HIPCHK(c, hipGetLastError());
+    ScanTemp t = scan_temp(c, m);
+    HIPCHK(c, launch_scan(c->pcounts.as<uint32_t>(), c->poffs.as<uint32_t>(), m, t, c->stream));
+    uint32_t total = 0;
+    HIPCHK(c, hipMemcpyAsync(&total, c->poffs.as<uint32_t>() + m, 4, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (total == 0) continue;
+    HIPCHK(c, c->pbuf.ensure((size_t)total * sizeof(gi_photon_dev)));
+    a.out = c->pbuf.as<gi_photon_dev>();
+    launch_photons(a, true, c->stream);
+    HIPCHK(c, hipGetLastError());
+    size_t old = out.size();
+    out.resize(old + total);
+    HIPCHK(c, hipMemcpyAsync(out.data() + old, c->pbuf.p, (size_t)total * sizeof(gi_photon),
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return GI_OK;
+}
+
+// adaptive emission rounds of Threadable_PhotonTracer (photonmap.cpp:145-257), one emitter
+int trace_map(gi_ctx *c, int caustic, int64_t goal, const std::vector<double> &powers,
+              double total_power, std::vector<gi_photon> &map, int64_t &emitted) {
+  int64_t stored = 0;
+  emitted = 0;
+  double rate = caustic ? (double)c->P.max_photon_depth : 4.0;
+  double slowdown = 1.0;
+  int attempts = 10;
+  int nl = (int)c->scene.lights.size();
+  while (stored < goal && attempts > 0) {
+    int emit_goal = (int)((double)(int)(goal - stored) / rate / slowdown + 1);
+    int64_t assigned = 0;
+    for (int i = 0; i < nl; i++) {
+      int num = (int)ceil(emit_goal * (powers[i] / total_power));
+      if (c->scene.lights[i].active && num) {
+        int rc = trace_batch(c, caustic, i, emitted + assigned, num, map);
+        if (rc) return rc;
+      }
+      assigned += num;
+    }
+    emitted += assigned;
+    stored = (int64_t)map.size();
+    if (stored > 0 && emitted > 0) {
+      rate = (double)stored / emitted;
+      double frac = caustic ? (double)stored / goal : (double)stored / emitted;
+      slowdown = (frac < 0.75) ? 2.0 : 1.0;
+    } else {
+      rate /= 2.0;
+      attempts--;
+    }
+  }
+  return GI_OK;
+}
+
+KnnArgs knn_args(gi_ctx *c, int mi) {
+  KnnArgs k;
+  memset(&k, 0, sizeof k);
+  k.map = c->dmap[mi].view();
+  k.mats = c->d_mats.as<DMaterial>();
+  k.lut = c->d_lut.as<double>();
+  const gi_params &P = c->P;
+  k.K = mi == GI_MAP_GLOBAL ? P.global_estimate_size : P.caustic_estimate_size;
+  double r = mi == GI_MAP_GLOBAL ? P.global_estimate_dist : P.caustic_estimate_dist;
+  k.filter = mi == GI_MAP_GLOBAL ? P.global_filter : P.caustic_filter;
+  k.r2f = (float)(r * r);
+  k.rmax = r;
+  k.fa = P.filter_const_a;
+  k.fb = P.filter_const_b;
+  k.fk = P.filter_const_k;
+  k.stats = c->d_stats.as<unsigned long long>();
+  return k;
+}
+
+// run a k-NN launch over nq queries (chunked when the heap lives in global scratch)
+int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
+  bool lds = k.K <= 64;
+  const int64_t CH = lds ? nq : (int64_t)(1 << 20);
+  for (int64_t s = 0; s < nq; s += CH) {
+    int64_t m = std::min(CH, nq - s);
+    KnnArgs a = k;
+    a.nq = m;
+    a.qpos = k.qpos + s;
+    a.qshade = k.qshade ? k.qshade + s : nullptr;
+    a.out = k.out ? k.out + 3 * s : nullptr;
+    a.out_n = k.out_n ? k.out_n + s : nullptr;
+    a.out_maxd2 = k.out_maxd2 ? k.out_maxd2 + s : nullptr;
+    a.out_idx = k.out_idx ? k.out_idx + (size_t)s * k.K : nullptr;
+    a.out_d2 = k.out_d2 ? k.out_d2 + (size_t)s * k.K : nullptr;
+    if (!lds) {
+      size_t slots = (size_t)((m + 63) / 64) * 64 * (size_t)k.K;
+      HIPCHK(c, c->gheap_d2.ensure(slots * 4));
+      HIPCHK(c, c->gheap_idx.ensure(slots * 4));
+      a.gheap_d2 = c->gheap_d2.as<float>();
+      a.gheap_idx = c->gheap_idx.as<int32_t>();
+    }
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    launch_knn(a, lds, c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    if (ms) {
+      HIPCHK(c, hipEventSynchronize(c->ev1));
+      float t = 0;
+      HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+      *ms += t;
+    }
+  }
+  return GI_OK;
+}
+
+// render the given output pixels into the device image buffers
+int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &pix_xy,
+                  gi_render_stats *rs) {
+  const gi_params &P = c->P;
+  int af = 1 << aa;
+  int dof = std::max(1, P.dof_test);
+  int64_t per_pix = (int64_t)af * af * dof;
+  int64_t npix_total = (int64_t)pix_xy.size() / 2;
+  int64_t pix_batch = std::max<int64_t>(1, c->prim_per_batch / per_pix);
+  double knn_ms = 0, launches = 0;
+  HIPCHK(c, upload(c->pixels, pix_xy.data(), pix_xy.size() * 4, c->stream));
+  for (int64_t p0 = 0; p0 < npix_total; p0 += pix_batch) {
+    int64_t npix = std::min(pix_batch, npix_total - p0);
+    int64_t nprim = npix * per_pix;
+    RenderArgs a;
+    memset(&a, 0, sizeof a);
+    a.S = make_view(c);
+    a.F = make_flags(P);
+    a.pixels = c->pixels.as<int2>() + p0;
+    a.npix = (int)npix;
+    a.af = af;
+    a.W = w * af;
+    a.H = h * af;
+    a.dof_test = dof;
+    a.out_w = w;
+    a.nprim = nprim;
+    a.stats = c->d_stats.as<unsigned long long>();
+    HIPCHK(c, c->spawn.ensure((size_t)nprim * sizeof(Spawn)));
+    HIPCHK(c, c->npaths.ensure((size_t)nprim * 4));
+    HIPCHK(c, c->path_off.ensure((size_t)(nprim + 1) * 4));
+    a.spawn = c->spawn.as<Spawn>();
+    a.npaths = c->npaths.as<uint32_t>();
+    a.path_off = c->path_off.as<uint32_t>();
+    launch_primary(a, c->stream);
+    HIPCHK(c, hipGetLastError());
+    ScanTemp t = scan_temp(c, nprim);
+    HIPCHK(c, launch_scan(a.npaths, c->path_off.as<uint32_t>(), nprim, t, c->stream));
+    uint32_t total_paths = 0;
+    HIPCHK(c, hipMemcpyAsync(&total_paths, c->path_off.as<uint32_t>() + nprim, 4,
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    a.total_paths = total_paths;
+    HIPCHK(c, c->cnt_g.ensure((size_t)total_paths * 4));
+    HIPCHK(c, c->cnt_c.ensure((size_t)total_paths * 4));
+    HIPCHK(c, c->goff.ensure((size_t)(total_paths + 1) * 4));
+    HIPCHK(c, c->coff.ensure((size_t)(total_paths + 1) * 4));
+    HIPCHK(c, c->base.ensure((size_t)total_paths * 24));
+    a.cnt_g = c->cnt_g.as<uint32_t>();
+    a.cnt_c = c->cnt_c.as<uint32_t>();
+    a.goff = c->goff.as<uint32_t>();
+    a.coff = c->coff.as<uint32_t>();
+    a.base = c->base.as<double>();
+    launch_path(a, false, c->stream);
+    HIPCHK(c, hipGetLastError());
+    t = scan_temp(c, total_paths);
+    HIPCHK(c, launch_scan(a.cnt_g, c->goff.as<uint32_t>(), total_paths, t, c->stream));
+    HIPCHK(c, launch_scan(a.cnt_c, c->coff.as<uint32_t>(), total_paths, t, c->stream));
+    uint32_t ng = 0, nc = 0;
+    HIPCHK(c, hipMemcpyAsync(&ng, c->goff.as<uint32_t>() + total_paths, 4, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipMemcpyAsync(&nc, c->coff.as<uint32_t>() + total_paths, 4, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, c->gpos.ensure((size_t)ng * 16));
+    HIPCHK(c, c->gshade.ensure((size_t)ng * sizeof(QShade)));
+    HIPCHK(c, c->gout.ensure((size_t)ng * 24));
+    HIPCHK(c, c->cpos.ensure((size_t)nc * 16));
+    HIPCHK(c, c->cshade.ensure((size_t)nc * sizeof(QShade)));
+    HIPCHK(c, c->cout.ensure((size_t)nc * 24));
+    a.gpos = c->gpos.as<float4>();
+    a.gshade = c->gshade.as<QShade>();
+    a.cpos = c->cpos.as<float4>();
+    a.cshade = c->cshade.as<QShade>();
+    launch_path(a, true, c->stream);
+    HIPCHK(c, hipGetLastError());
+    // photon-map estimates
+    if (ng) {
+      if (!c->map_valid[GI_MAP_GLOBAL]) {
+        HIPCHK(c, hipMemsetAsync(c->gout.p, 0, (size_t)ng * 24, c->stream));
+      } else {
+        KnnArgs k = knn_args(c, GI_MAP_GLOBAL);
+        k.qpos = a.gpos;
+        k.qshade = a.gshade;
+        k.out = c->gout.as<double>();
+        k.nq = ng;
+        if (P.irradiance_cache) {
+          launch_cached(k, c->stream);
+          HIPCHK(c, hipGetLastError());
+        } else {
+          int rc = run_knn(c, k, ng, rs ? &knn_ms : nullptr);
+          if (rc) return rc;
+          launches++;
+        }
+      }
+    }
+    if (nc) {
+      if (!c->map_valid[GI_MAP_CAUSTIC]) {
+        HIPCHK(c, hipMemsetAsync(c->cout.p, 0, (size_t)nc * 24, c->stream));
+      } else {
+        KnnArgs k = knn_args(c, GI_MAP_CAUSTIC);
+        k.qpos = a.cpos;
+        k.qshade = a.cshade;
+        k.out = c->cout.as<double>();
+        k.nq = nc;
+        int rc = run_knn(c, k, nc, rs ? &knn_ms : nullptr);
+        if (rc) return rc;
+        launches++;
+      }
+    }
+    a.gout = c->gout.as<double>();
+    a.cout = c->cout.as<double>();
+    a.rgbf = c->rgbf.as<float>();
+    a.rgb8 = c->rgb8.as<uint8_t>();
+    launch_reduce(a, c->stream);
+    HIPCHK(c, hipGetLastError());
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (rs) {
+    rs->knn_kernel_ms += knn_ms;
+    rs->knn_kernel_launches += launches;
+  }
+  return GI_OK;
+}
+
+int check_ready(gi_ctx *c) {
+  if (!c->have_scene) return fail(c, GI_ERR_STATE, "no scene loaded (gi_read_scene)");
+  if (c->scene.unsupported_shapes)
+    return fail(c, GI_ERR_UNSUPPORTED,
+                "scene contains cylinder/cone/line shapes: not yet on the device path");
+  return GI_OK;
+}
+
+}  // namespace
+
+// =======================================================================================
+// C-ABI
+// =======================================================================================
+extern "C" {
+
+int gi_create(gi_ctx **out, int dev) {
+  *out = nullptr;
+  gi_ctx *c = new gi_ctx();
+  c->device = dev;
+  gi_params_default(&c->P);
+  if (hipSetDevice(dev) != hipSuccess) { delete c; return GI_ERR_HIP; }
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return GI_ERR_HIP; }
+  hipEventCreate(&c->ev0);
+  hipEventCreate(&c->ev1);
+  std::vector<double> lut;
+  build_lut(lut);
+  if (upload(c->d_lut, lut.data(), lut.size() * 8, c->stream) != hipSuccess ||
+      c->d_stats.ensure(ST_COUNT * 8) != hipSuccess) {
+    delete c;
+    return GI_ERR_HIP;
+  }
+  hipStreamSynchronize(c->stream);
+  if (const char *s = getenv("GI_PRIM_PER_BATCH")) c->prim_per_batch = std::max(1LL, atoll(s));
+  if (const char *s = getenv("GI_LEAF_SIZE")) c->leaf_size = std::max(1, atoi(s));
+  *out = c;
+  return GI_OK;
+}
+
+void gi_destroy(gi_ctx *c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  DBuf *bufs[] = {&c->d_nodes, &c->d_elems, &c->d_shapes, &c->d_tris, &c->d_mats, &c->d_lights,
+                  &c->d_lut, &c->d_stats, &c->spawn, &c->npaths, &c->path_off, &c->cnt_g,
+                  &c->cnt_c, &c->goff, &c->coff, &c->base, &c->gpos, &c->cpos, &c->gshade,
+                  &c->cshade, &c->gout, &c->cout, &c->pixels, &c->rgbf, &c->rgb8, &c->gheap_d2,
+                  &c->gheap_idx, &c->perm, &c->pcounts, &c->poffs, &c->pbuf};
+  for (DBuf *b : bufs) b->release();
+  for (int l = 0; l < 8; l++) { c->scan_lvl[l].release(); c->scan_out[l].release(); }
+  for (int m = 0; m < 2; m++) {
+    c->dmap[m].pos4.release();
+    c->dmap[m].rgbe.release();
+    c->dmap[m].nodes.release();
+  }
+  if (c->ev0) hipEventDestroy(c->ev0);
+  if (c->ev1) hipEventDestroy(c->ev1);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char *gi_last_error(const gi_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int gi_set_params(gi_ctx *c, const gi_params *p) {
+  if (!c || !p) return GI_ERR_ARG;
+  c->P = *p;
+  c->have_params = true;
+  return GI_OK;
+}
+
+int gi_read_scene(gi_ctx *c, const char *path, int real) {
+  if (!c || !path) return GI_ERR_ARG;
+  std::string err;
+  HostScene S;
+  if (!load_scene(path, real != 0, S, err)) return fail(c, GI_ERR_IO, err);
+  c->scene = std::move(S);
+  HostScene &H = c->scene;
+  HIPCHK(c, upload(c->d_nodes, H.nodes.data(), H.nodes.size() * sizeof(DNode), c->stream));
+  HIPCHK(c, upload(c->d_elems, H.elems.data(), H.elems.size() * sizeof(DElement), c->stream));
+  HIPCHK(c, upload(c->d_shapes, H.shapes.data(), H.shapes.size() * sizeof(DShape), c->stream));
+  HIPCHK(c, upload(c->d_tris, H.tris.data(), H.tris.size() * sizeof(DTri), c->stream));
+  HIPCHK(c, upload(c->d_mats, H.mats.data(), H.mats.size() * sizeof(DMaterial), c->stream));
+  HIPCHK(c, upload(c->d_lights, H.lights.data(), H.lights.size() * sizeof(DLight), c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->have_scene = true;
+  c->map_valid[0] = c->map_valid[1] = false;
+  return GI_OK;
+}
+
+int gi_scene_info(gi_ctx *c, int *nnodes, int *nlights, int *nprims, double *radius) {
+  if (!c || !c->have_scene) return GI_ERR_STATE;
+  if (nnodes) *nnodes = (int)c->scene.nodes.size();
+  if (nlights) *nlights = (int)c->scene.lights.size();
+  if (nprims) *nprims = (int)c->scene.shapes.size();
+  if (radius) *radius = c->scene.radius;
+  return GI_OK;
+}
+
+// MapPhotons, photonmap.cpp:260-436
+int gi_map_photons(gi_ctx *c, gi_photon_stats *st) {
+  if (!c) return GI_ERR_ARG;
+  int rc = check_ready(c);
+  if (rc) return rc;
+  auto t0 = std::chrono::steady_clock::now();
+  gi_params &P = c->P;
+  for (int m = 0; m < 2; m++) { c->hmap[m] = HostMap(); c->map_valid[m] = false; }
+  int nl = (int)c->scene.lights.size();
+  int64_t gem = 0, cem = 0;
+  if (st) memset(st, 0, sizeof *st);
+  if (nl <= 0) return GI_OK;
+  std::vector<double> powers(nl, 0.0);
+  double total = 0;
+  for (int i = 0; i < nl; i++) {
+    if (!c->scene.lights[i].active) continue;
+    powers[i] = light_power(c->scene, c->scene.lights[i]);
+    total += powers[i];
+  }
+  if (total <= 0) return GI_OK;
+  std::vector<gi_photon> gph, cph;
+  if (P.indirect_illum || P.direct_photon_illum) {
+    rc = trace_map(c, 0, P.global_photon_count, powers, total, gph, gem);
+    if (rc) return rc;
+  }
+  if (P.caustic_illum) {
+    rc = trace_map(c, 1, P.caustic_photon_count, powers, total, cph, cem);
+    if (rc) return rc;
+  }
+  auto t1 = std::chrono::steady_clock::now();
+  // power rescale (Q9), photonmap.cpp:339-361
+  auto rescale = [&](std::vector<gi_photon> &v, int64_t emitted) {
+    double pp = total / (double)emitted;
+    for (auto &p : v) {
+      double col[3];
+      rgbe_dec(p.rgbe, col);
+      for (int i = 0; i < 3; i++) col[i] *= pp;
+      rgbe_enc(col, p.rgbe);
+    }
+  };
+  if ((P.indirect_illum || P.direct_photon_illum) && !gph.empty()) {
+    P.global_photon_count = (int)gph.size();
+    rescale(gph, gem);
+  } else if (P.indirect_illum || P.direct_photon_illum) {
+    P.indirect_illum = 0;
+    P.direct_photon_illum = 0;
+  }
+  if (P.caustic_illum && !cph.empty()) {
+    P.caustic_photon_count = (int)cph.size();
+    rescale(cph, cem);
+  } else if (P.caustic_illum) {
+    P.caustic_illum = 0;
+  }
+  rc = set_map(c, GI_MAP_GLOBAL, gph.data(), (int64_t)gph.size());
+  if (rc) return rc;
+  rc = set_map(c, GI_MAP_CAUSTIC, cph.data(), (int64_t)cph.size());
+  if (rc) return rc;
+  auto t2 = std::chrono::steady_clock::now();
+  // irradiance cache, photonmap.cpp:381-413: irradiance = own power + EstimateIrradiance
+  if (P.irradiance_cache && (P.indirect_illum || P.direct_photon_illum) && !gph.empty()) {
+    HostMap &H = c->hmap[GI_MAP_GLOBAL];
+    int64_t n = (int64_t)H.storage.size();
+    std::vector<float> q(4 * n);
+    for (int64_t i = 0; i < n; i++) {
+      q[4 * i] = H.storage[i].pos[0];
+      q[4 * i + 1] = H.storage[i].pos[1];
+      q[4 * i + 2] = H.storage[i].pos[2];
+      q[4 * i + 3] = 0;
+    }
+    DBuf dq, dout;
+    HIPCHK(c, upload(dq, q.data(), q.size() * 4, c->stream));
+    HIPCHK(c, dout.ensure((size_t)n * 24));
+    KnnArgs k = knn_args(c, GI_MAP_GLOBAL);
+    k.mode = KNN_MODE_IRRADIANCE;
+    k.qpos = dq.as<float4>();
+    k.out = dout.as<double>();
+    k.stats = nullptr;
+    rc = run_knn(c, k, n, nullptr);
+    if (rc) return rc;
+    std::vector<double> irr(3 * n);
+    HIPCHK(c, hipMemcpyAsync(irr.data(), dout.p, (size_t)n * 24, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    dq.release();
+    dout.release();
+    std::vector<gi_photon> cached = H.storage;
+    for (int64_t i = 0; i < n; i++) {
+      double col[3];
+      rgbe_dec(cached[i].rgbe, col);
+      for (int j = 0; j < 3; j++) col[j] += irr[3 * i + j];
+      rgbe_enc(col, cached[i].rgbe);
+    }
+    rc = set_map(c, GI_MAP_GLOBAL, cached.data(), n);
+    if (rc) return rc;
+  }
+  auto t3 = std::chrono::steady_clock::now();
+  if (st) {
+    st->global_stored = (int64_t)c->hmap[0].storage.size();
+    st->caustic_stored = (int64_t)c->hmap[1].storage.size();
+    st->global_emitted = gem;
+    st->caustic_emitted = cem;
+    st->trace_s = std::chrono::duration<double>(t1 - t0).count();
+    st->kd_s = std::chrono::duration<double>(t2 - t1).count();
+    st->irradiance_s = std::chrono::duration<double>(t3 - t2).count();
+    st->total_s = std::chrono::duration<double>(t3 - t0).count();
+  }
+  return GI_OK;
+}
+
+int gi_set_photon_map(gi_ctx *c, int map, const gi_photon *ph, int64_t n) {
+  if (!c || map < 0 || map > 1 || (n > 0 && !ph)) return GI_ERR_ARG;
+  return set_map(c, map, ph, n);
+}
+
+int gi_get_photon_map(gi_ctx *c, int map, gi_photon *out, int64_t cap, int64_t *n) {
+  if (!c || map < 0 || map > 1) return GI_ERR_ARG;
+  const auto &v = c->hmap[map].storage;
+  if (n) *n = (int64_t)v.size();
+  if (out) {
+    if ((int64_t)v.size() > cap) return fail(c, GI_ERR_ARG, "capacity too small");
+    memcpy(out, v.data(), v.size() * sizeof(gi_photon));
+  }
+  return GI_OK;
+}
+
+static int render_common(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &pix,
+                         uint8_t *rgb8, float *rgbf, gi_render_stats *st, bool keep_rgbf) {
+  int rc = check_ready(c);
+  if (rc) return rc;
+  if (aa < 0 || w <= 0 || h <= 0) return fail(c, GI_ERR_ARG, "bad image size");
+  auto t0 = std::chrono::steady_clock::now();
+  size_t npx = (size_t)w * h * 3;
+  HIPCHK(c, c->rgbf.ensure(npx * 4));
+  HIPCHK(c, c->rgb8.ensure(npx));
+  if (keep_rgbf && rgbf) {
+    HIPCHK(c, hipMemcpyAsync(c->rgbf.p, rgbf, npx * 4, hipMemcpyHostToDevice, c->stream));
+  } else {
+    HIPCHK(c, hipMemsetAsync(c->rgbf.p, 0, npx * 4, c->stream));
+  }
+  HIPCHK(c, hipMemsetAsync(c->rgb8.p, 0, npx, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_stats.p, 0, ST_COUNT * 8, c->stream));
+  gi_render_stats local;
+  memset(&local, 0, sizeof local);
+  rc = render_pixels(c, aa, w, h, pix, &local);
+  if (rc) return rc;
+  if (rgbf) HIPCHK(c, hipMemcpyAsync(rgbf, c->rgbf.p, npx * 4, hipMemcpyDeviceToHost, c->stream));
+  if (rgb8) HIPCHK(c, hipMemcpyAsync(rgb8, c->rgb8.p, npx, hipMemcpyDeviceToHost, c->stream));
+  unsigned long long s[ST_COUNT];
+  HIPCHK(c, hipMemcpyAsync(s, c->d_stats.p, sizeof s, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (st) {
+    st->screen_rays = s[ST_RAY];
+    st->shadow_rays = s[ST_SHADOW];
+    st->monte_carlo_rays = s[ST_MONTE];
+    st->transmissive_samples = s[ST_TRANS];
+    st->specular_samples = s[ST_SPEC];
+    st->indirect_samples = s[ST_INDIRECT];
+    st->caustic_samples = s[ST_CAUSTIC];
+    st->knn_queries = s[ST_KNN];
+    st->knn_photons = s[ST_KNN_PHOTONS];
+    st->knn_kernel_ms = local.knn_kernel_ms;
+    st->knn_kernel_launches = local.knn_kernel_launches;
+    st->render_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return GI_OK;
+}
+
+// RenderImage, render.cpp:155-259
+int gi_render_image(gi_ctx *c, int aa, int w, int h, uint8_t *rgb8, float *rgbf,
+                    gi_render_stats *st) {
+  if (!c) return GI_ERR_ARG;
+  std::vector<int32_t> pix((size_t)w * h * 2);
+  for (int y = 0; y < h; y++)
+    for (int x = 0; x < w; x++) {
+      pix[2 * ((size_t)y * w + x)] = x;
+      pix[2 * ((size_t)y * w + x) + 1] = y;
+    }
+  return render_common(c, aa, w, h, pix, rgb8, rgbf, st, false);
+}
+
+int gi_render_tiles(gi_ctx *c, int aa, int w, int h, int tile, int shard, int nshards,
+                    float *rgbf, gi_render_stats *st) {
+  if (!c || tile <= 0 || nshards <= 0 || shard < 0 || shard >= nshards || !rgbf) return GI_ERR_ARG;
+  int tx = (w + tile - 1) / tile, ty = (h + tile - 1) / tile;
+  std::vector<int32_t> pix;
+  for (int t = 0; t < tx * ty; t++) {
+    if (t % nshards != shard) continue;
+    int x0 = (t % tx) * tile, y0 = (t / tx) * tile;
+    for (int y = y0; y < std::min(h, y0 + tile); y++)
+      for (int x = x0; x < std::min(w, x0 + tile); x++) {
+        pix.push_back(x);
+        pix.push_back(y);
+      }
+  }
+  return render_common(c, aa, w, h, pix, nullptr, rgbf, st, true);
+}
+
+int gi_quantize(int w, int h, const float *rgbf, uint8_t *rgb8) {
+  if (!rgbf || !rgb8) return GI_ERR_ARG;
+  for (size_t i = 0; i < (size_t)w * h * 3; i++) rgb8[i] = (uint8_t)(255 * (double)rgbf[i]);
+  return GI_OK;
+}
+
+int gi_estimate_radiance_batch(gi_ctx *c, int map, int64_t n, const gi_radiance_query *q,
+                               double *rgb_out, int32_t *nfound, float *maxd2) {
+  if (!c || map < 0 || map > 1 || (n > 0 && (!q || !rgb_out))) return GI_ERR_ARG;
+  if (n == 0) return GI_OK;
+  for (int64_t i = 1; i < n; i++)
+    if (q[i].k != q[0].k || q[i].max_dist != q[0].max_dist || q[i].filter != q[0].filter)
+      return fail(c, GI_ERR_ARG, "estimate_size / estimate_dist / filter must be uniform");
+  // one material per query carries its brdf terms
+  std::vector<DMaterial> mats(n);
+  std::vector<float> qp(4 * n);
+  std::vector<QShade> qs(n);
+  for (int64_t i = 0; i < n; i++) {
+    DMaterial &m = mats[i];
+    memset(&m, 0, sizeof m);
+    for (int j = 0; j < 3; j++) { m.kd[j] = q[i].kd[j]; m.ks[j] = q[i].ks[j]; }
+    m.n = q[i].shininess;
+    bool spec = !(m.ks[0] == 0.0 && m.ks[1] == 0.0 && m.ks[2] == 0.0);
+    m.flags = spec ? MF_SPECULAR : 0;
+    double ct = q[i].cos_theta;
+    uint32_t sign = (ct > 0) ? 1u : ((ct < 0) ? 2u : 0u);
+    uint32_t meta = sign | ((uint32_t)i << 2);
+    qp[4 * i] = (float)q[i].point[0];
+    qp[4 * i + 1] = (float)q[i].point[1];
+    qp[4 * i + 2] = (float)q[i].point[2];
+    memcpy(&qp[4 * i + 3], &meta, 4);
+    for (int j = 0; j < 3; j++) {
+      qs[i].n[j] = q[i].normal[j];
+      qs[i].ex[j] = q[i].exact_bounce[j];
+      qs[i].w[j] = 1.0;
+    }
+  }
+  DBuf dm, dq, ds, dout, dn, dmd;
+  HIPCHK(c, upload(dm, mats.data(), mats.size() * sizeof(DMaterial), c->stream));
+  HIPCHK(c, upload(dq, qp.data(), qp.size() * 4, c->stream));
+  HIPCHK(c, upload(ds, qs.data(), qs.size() * sizeof(QShade), c->stream));
+  HIPCHK(c, dout.ensure((size_t)n * 24));
+  HIPCHK(c, dn.ensure((size_t)n * 4));
+  HIPCHK(c, dmd.ensure((size_t)n * 4));
+  KnnArgs k = knn_args(c, map);
+  k.mats = dm.as<DMaterial>();
+  k.K = q[0].k;
+  k.filter = q[0].filter;
+  k.r2f = (float)(q[0].max_dist * q[0].max_dist);
+  k.rmax = q[0].max_dist;
+  k.qpos = dq.as<float4>();
+  k.qshade = ds.as<QShade>();
+  k.out = dout.as<double>();
+  k.out_n = dn.as<int32_t>();
+  k.out_maxd2 = dmd.as<float>();
+  k.stats = nullptr;
+  int rc = run_knn(c, k, n, nullptr);
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpyAsync(rgb_out, dout.p, (size_t)n * 24, hipMemcpyDeviceToHost, c->stream));
+  if (nfound) HIPCHK(c, hipMemcpyAsync(nfound, dn.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+  if (maxd2) HIPCHK(c, hipMemcpyAsync(maxd2, dmd.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  DBuf *bs[] = {&dm, &dq, &ds, &dout, &dn, &dmd};
+  for (DBuf *b : bs) b->release();
+  return GI_OK;
+}
+
+int gi_knn_batch(gi_ctx *c, int map, int64_t n, const double *pts, int K, double max_dist,
+                 int32_t *idx_out, float *d2_out, int32_t *nfound) {
+  if (!c || map < 0 || map > 1 || K <= 0 || (n > 0 && (!pts || !idx_out || !d2_out || !nfound)))
+    return GI_ERR_ARG;
+  if (n == 0) return GI_OK;
+  std::vector<float> qp(4 * n, 0.0f);
+  for (int64_t i = 0; i < n; i++)
+    for (int j = 0; j < 3; j++) qp[4 * i + j] = (float)pts[3 * i + j];
+  DBuf dq, di, dd, dn;
+  HIPCHK(c, upload(dq, qp.data(), qp.size() * 4, c->stream));
+  HIPCHK(c, di.ensure((size_t)n * K * 4));
+  HIPCHK(c, dd.ensure((size_t)n * K * 4));
+  HIPCHK(c, dn.ensure((size_t)n * 4));
+  KnnArgs k = knn_args(c, map);
+  k.mode = KNN_MODE_LIST;
+  k.K = K;
+  k.r2f = (float)(max_dist * max_dist);
+  k.rmax = max_dist;
+  k.qpos = dq.as<float4>();
+  k.out_idx = di.as<int32_t>();
+  k.out_d2 = dd.as<float>();
+  k.out_n = dn.as<int32_t>();
+  k.stats = nullptr;
+  int rc = run_knn(c, k, n, nullptr);
+  if (rc) return rc;
+  std::vector<int32_t> idx((size_t)n * K);
+  HIPCHK(c, hipMemcpyAsync(idx.data(), di.p, idx.size() * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d2_out, dd.p, (size_t)n * K * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(nfound, dn.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  // kd order -> storage (emission) order indices
+  const auto &perm = c->hmap[map].perm;
+  for (size_t i = 0; i < idx.size(); i++) idx_out[i] = idx[i] >= 0 ? perm[idx[i]] : -1;
+  dq.release(); di.release(); dd.release(); dn.release();
+  return GI_OK;
+}
+
+int gi_intersect_batch(gi_ctx *c, int64_t n, const double *org, const double *dir, int32_t *hit,
+                       double *t, double *point, double *normal, int32_t *material) {
+  if (!c) return GI_ERR_ARG;
+  if (!c->have_scene) return fail(c, GI_ERR_STATE, "no scene loaded");
+  if (n == 0) return GI_OK;
+  DBuf dorg, ddir, dhit, dt, dp, dn, dm;
+  HIPCHK(c, upload(dorg, org, (size_t)n * 24, c->stream));
+  HIPCHK(c, upload(ddir, dir, (size_t)n * 24, c->stream));
+  HIPCHK(c, dhit.ensure((size_t)n * 4));
+  HIPCHK(c, dt.ensure((size_t)n * 8));
+  HIPCHK(c, dp.ensure((size_t)n * 24));
+  HIPCHK(c, dn.ensure((size_t)n * 24));
+  HIPCHK(c, dm.ensure((size_t)n * 4));
+  launch_intersect(make_view(c), n, dorg.as<double>(), ddir.as<double>(), dhit.as<int32_t>(),
+                   dt.as<double>(), dp.as<double>(), dn.as<double>(), dm.as<int32_t>(), c->stream);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(hit, dhit.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(t, dt.p, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(point, dp.p, (size_t)n * 24, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(normal, dn.p, (size_t)n * 24, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(material, dm.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  DBuf *bs[] = {&dorg, &ddir, &dhit, &dt, &dp, &dn, &dm};
+  for (DBuf *b : bs) b->release();
+  return GI_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,123 @@
+// gi_kernels.h -- kernel argument blocks and host-callable launchers (gi_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "gi_device.h"
+
+namespace gi {
+
+// device-written photon record; byte-identical to gi_photon (gi.h) on little-endian
+struct gi_photon_dev {
+  float pos[3];
+  uint32_t rgbe;   // r | g<<8 | b<<16 | e<<24
+  uint16_t dir;
+  uint16_t flags;
+};
+static_assert(sizeof(gi_photon_dev) == 20, "photon record is 20 bytes");
+
+// per primary sample: the RayTrace state the sample paths need (raytracer.cpp:174-233)
+struct Spawn {
+  double p[3], n[3], v[3];
+  double ct, R;
+  double base[3];    // ambient + direct (+ background on a miss)
+  int32_t mat, hit;
+  int32_t n_t, n_s, n_i;  // transmissive / specular / indirect sample counts
+  int32_t q_glob, q_caus; // primary-hit photon-map queries (photon_viz / caustic)
+  int32_t pad;
+};
+
+// shading half of a photon-map query (search half is float4 {x, y, z, meta})
+struct QShade {
+  double n[3];   // surface normal
+  double ex[3];  // exact reflection direction (Phong lobe term)
+  double w[3];   // path weight multiplying the estimate
+};
+
+enum {
+  ST_RAY = 0, ST_SHADOW, ST_MONTE, ST_TRANS, ST_SPEC, ST_INDIRECT, ST_CAUSTIC,
+  ST_KNN, ST_KNN_PHOTONS, ST_KNN_VISITED, ST_COUNT = 16
+};
+
+struct RenderArgs {
+  SceneView S;
+  Flags F;
+  const int2 *pixels;   // output pixels of this batch
+  int32_t npix;
+  int32_t af;           // 2^aa
+  int32_t W, H;         // supersampled viewport (render.cpp:177-178)
+  int32_t dof_test;
+  int32_t out_w;
+  int64_t nprim;        // npix * af^2 * dof_test
+  int64_t total_paths;
+  Spawn *spawn;
+  uint32_t *npaths;     // [nprim]
+  const uint32_t *path_off;  // [nprim + 1]
+  uint32_t *cnt_g, *cnt_c;   // [total_paths]
+  const uint32_t *goff, *coff;  // [total_paths + 1]
+  float4 *gpos, *cpos;
+  QShade *gshade, *cshade;
+  double *base;         // [total_paths * 3]
+  const double *gout, *cout;   // k-NN contributions
+  float *rgbf;
+  uint8_t *rgb8;
+  unsigned long long *stats;
+};
+
+enum { KNN_MODE_RADIANCE = 0, KNN_MODE_IRRADIANCE = 1, KNN_MODE_LIST = 2 };
+
+struct KnnArgs {
+  KdView map;
+  const float4 *qpos;
+  const QShade *qshade;
+  const uint32_t *perm;    // optional query order (spatial sort)
+  const DMaterial *mats;
+  const double *lut;       // 65536 x 3 direction table
+  int64_t nq;
+  int32_t K;
+  int32_t filter;
+  int32_t mode;
+  int32_t pad;
+  float r2f;               // (float)(r*r) accept radius
+  double rmax;
+  double fa, fb, fk;       // FILTER_CONST_A/B/K
+  double *out;             // [nq*3]
+  int32_t *out_n;          // optional
+  float *out_maxd2;        // optional
+  int32_t *out_idx;        // KNN_MODE_LIST
+  float *out_d2;
+  float *gheap_d2;         // global heap scratch (K > 64)
+  int32_t *gheap_idx;
+  unsigned long long *stats;
+};
+
+struct PhotonArgs {
+  SceneView S;
+  Flags F;
+  int32_t light;
+  int32_t caustic;
+  int64_t e0;     // first emission index
+  int64_t n;      // photons in this launch
+  uint32_t *counts;
+  const uint32_t *offsets;
+  gi_photon_dev *out;
+};
+
+struct ScanTemp {
+  uint32_t *level[8];
+  uint32_t *level_out[8];
+  int depth;
+};
+
+hipError_t launch_scan(const uint32_t *in, uint32_t *out, int64_t n, ScanTemp &tmp,
+                       hipStream_t st);
+void launch_primary(const RenderArgs &a, hipStream_t st);
+void launch_path(const RenderArgs &a, bool emit, hipStream_t st);
+void launch_reduce(const RenderArgs &a, hipStream_t st);
+void launch_knn(const KnnArgs &a, bool lds_heap, hipStream_t st);
+void launch_cached(const KnnArgs &a, hipStream_t st);
+void launch_photons(const PhotonArgs &a, bool emit, hipStream_t st);
+void launch_intersect(const SceneView &S, int64_t n, const double *org, const double *dir,
+                      int32_t *hit, double *t, double *point, double *normal, int32_t *mat,
+                      hipStream_t st);
+
+}  // namespace gi

@@ -1,0 +1,1061 @@
+// gi_kernels.hip -- HIP kernels of the MI355X photon-mapping renderer (gfx950).
+//
+// Render pipeline for one batch of output pixels (all their 4^aa * DOF_TEST primary samples):
+//   primary_kernel   camera ray + RayTrace prologue (ambient, direct) and the sample fan-out
+//                    counts of raytracer.cpp:47-135 (transmissive / specular / indirect)
+//   path_kernel<0>   count k-NN queries each sample path will issue   (Monte Carlo loops,
+//   path_kernel<1>   emit them + the path's non-photon colour          montecarlo.cpp:16-305)
+//   knn_kernel       k nearest photons + EstimateRadiance (photon_utils.cpp:72-162) per query,
+//                    multiplied by the query's path weight
+//   reduce_kernel    per pixel: sum paths and queries per primary sample, DOF average, clamp,
+//                    box filter, 8-bit truncation (render.cpp:205-221)
+// The decomposition is exact: every k-NN estimate enters the pixel linearly (colour += w*est),
+// so deferring the estimates into a query list changes only the fp summation order.
+#include <hip/hip_runtime.h>
+#include "gi_device.h"
+#include "gi_kernels.h"
+
+namespace gi {
+
+// ---------------------------------------------------------------------------------------
+// wave-level counter reduction (one atomic per wave)
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void wave_add(unsigned long long *dst, uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, (unsigned long long)v);
+}
+
+// ---------------------------------------------------------------------------------------
+// exclusive scan of uint32 -> uint32 (n+1 outputs, last = total)
+// ---------------------------------------------------------------------------------------
+constexpr int SCAN_BLOCK = 256, SCAN_ITEMS = 4, SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
+
+__global__ __launch_bounds__(SCAN_BLOCK) void scan_tile_kernel(const uint32_t *in, uint32_t *out,
+                                                                uint32_t *block_sums, int64_t n) {
+  __shared__ uint32_t s[SCAN_BLOCK];
+  int64_t base = (int64_t)blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
+  uint32_t v[SCAN_ITEMS];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_ITEMS; i++) {
+    int64_t k = base + i;
+    v[i] = (k < n) ? in[k] : 0u;
+    sum += v[i];
+  }
+  s[threadIdx.x] = sum;
+  __syncthreads();
+  for (int off = 1; off < SCAN_BLOCK; off <<= 1) {
+    uint32_t t = (threadIdx.x >= (unsigned)off) ? s[threadIdx.x - off] : 0u;
+    __syncthreads();
+    s[threadIdx.x] += t;
+    __syncthreads();
+  }
+  uint32_t run = s[threadIdx.x] - sum;
+#pragma unroll
+  for (int i = 0; i < SCAN_ITEMS; i++) {
+    int64_t k = base + i;
+    if (k < n) out[k] = run;
+    run += v[i];
+  }
+  if (threadIdx.x == SCAN_BLOCK - 1) block_sums[blockIdx.x] = s[SCAN_BLOCK - 1];
+}
+
+__global__ void scan_add_kernel(uint32_t *out, const uint32_t *block_off, int64_t n) {
+  int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) out[k] += block_off[k / SCAN_TILE];
+}
+
+// ---------------------------------------------------------------------------------------
+// Render: primary samples
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void decode_primary(const RenderArgs &a, int64_t b, int &pix, int &i,
+                                               int &j, int &k, uint64_t &psample) {
+  int af2 = a.af * a.af;
+  k = (int)(b % a.dof_test);
+  int64_t r = b / a.dof_test;
+  int sub = (int)(r % af2);
+  pix = (int)(r / af2);
+  int2 pc = a.pixels[pix];
+  i = pc.x * a.af + (sub % a.af);
+  j = pc.y * a.af + (sub / a.af);
+  psample = ((uint64_t)j * (uint64_t)a.W + (uint64_t)i) * (uint64_t)a.dof_test + (uint64_t)k;
+}
+
+// Threadable_RayTracer body (render.cpp:96-132) + RayTrace (raytracer.cpp:174-233) up to the
+// sample fan-outs. Writes the spawn record the path kernels expand.
+__global__ __launch_bounds__(256) void primary_kernel(RenderArgs a) {
+  int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t c_ray = 0, c_shadow = 0, c_ind = 0;
+  if (b < a.nprim) {
+    const SceneView &S = a.S;
+    const Flags &F = a.F;
+    int pix, i, j, k;
+    uint64_t psample;
+    decode_primary(a, b, pix, i, j, k, psample);
+    Rng rng;
+    rng.init(F.seed, KIND_PRIMARY, psample, 0);
+    double dx = (double)(2 * (i - a.W / 2)) / (double)a.W;
+    double dy = (double)(2 * (j - a.H / 2)) / (double)a.H;
+    V far_point = ld3(S.cam.far_org) + (ld3(S.cam.far_right) * dx) + (ld3(S.cam.far_up) * dy);
+    V eye = ld3(S.cam.eye);
+    V org = eye;
+    if (F.dof) {
+      double r1, r2;
+      do {
+        r1 = (rng.next() * 2.0) - 1.0;
+        r2 = (rng.next() * 2.0) - 1.0;
+      } while (r1 * r1 + r2 * r2 > 1.0);
+      org = eye + r1 * ld3(S.cam.dof_u) + r2 * ld3(S.cam.dof_v);
+    }
+    V dir = normalize(far_point - org);
+    Spawn sp;
+    sp.hit = 0;
+    sp.n_t = sp.n_s = sp.n_i = 0;
+    sp.q_glob = sp.q_caus = 0;
+    Hit h;
+    Counts cnt = {0, 0, 0, 0, 0, 0};
+    if (!scene_intersect(S, org, dir, h)) {
+      C3 bg = ldc(S.background);
+      sp.base[0] = bg.r; sp.base[1] = bg.g; sp.base[2] = bg.b;
+    } else {
+      c_ray = 1;
+      const DMaterial &m = S.mats[h.mat];
+      C3 color = rgb(0, 0, 0);
+      if (F.ambient) color += ldc(S.ambient);
+      V view = normalize(h.p - eye);
+      double ct = dot(h.n, -view);
+      double R = 0;
+      if (F.ambient && (m.flags & MF_AMBIENT)) color += ldc(m.ka);
+      if (F.direct && (m.flags & (MF_DIFFUSE | MF_SPECULAR)))
+        direct_illumination(S, F, h.p, h.n, eye, color, m, ct, false, rng, cnt);
+      if (F.transmissive && (m.flags & MF_TRANSPARENT)) {
+        if (F.specular && F.fresnel) R = reflection_coeff(F.ir_air, ct, m.ir);
+        if (R < 1.0) {
+          C3 tw = (1.0 - R) * ldc(m.kt);
+          sp.n_t = (int)ceil((F.trans_test * maxch(tw) + F.trans_test) / 2.0);
+        }
+      }
+      if (F.specular && ((m.flags & MF_SPECULAR) || R > 0)) {
+        C3 tw = ldc(m.kt) * R + ldc(m.ks);
+        sp.n_s = (int)ceil((F.spec_test * maxch(tw) + F.spec_test) / 2.0);
+      }
+      if (F.indirect && (m.flags & MF_DIFFUSE))
+        sp.n_i = (int)ceil((F.indirect_test * m.max_kd + F.indirect_test) / 2.0);
+      if (F.caustic && (m.flags & MF_DIFFUSE)) sp.q_caus = 1;
+      if (F.photon_viz && (m.flags & MF_DIFFUSE)) {
+        sp.q_glob = 1;
+        if (!F.cache) c_ind = 1;
+      }
+      sp.hit = 1;
+      sp.p[0] = h.p.x; sp.p[1] = h.p.y; sp.p[2] = h.p.z;
+      sp.n[0] = h.n.x; sp.n[1] = h.n.y; sp.n[2] = h.n.z;
+      sp.v[0] = view.x; sp.v[1] = view.y; sp.v[2] = view.z;
+      sp.ct = ct;
+      sp.R = R;
+      sp.mat = h.mat;
+      sp.base[0] = color.r; sp.base[1] = color.g; sp.base[2] = color.b;
+    }
+    a.spawn[b] = sp;
+    a.npaths[b] = 1u + (uint32_t)(sp.n_t + sp.n_s + sp.n_i);
+    c_shadow = cnt.shadow;
+  }
+  wave_add(&a.stats[ST_RAY], c_ray);
+  wave_add(&a.stats[ST_SHADOW], c_shadow);
+  wave_add(&a.stats[ST_INDIRECT], c_ind);
+}
+
+// query sink: count mode only counts; emit mode writes (point f32, meta) + shading record
+struct QSink {
+  float4 *pos;
+  QShade *shade;
+  uint32_t off;
+};
+
+__device__ __forceinline__ void put_query(bool emit, QSink &s, uint32_t &count, V p, V n, V ex,
+                                          double ct, int mat, C3 w) {
+  if (emit) {
+    uint32_t sign = (ct > 0) ? 1u : ((ct < 0) ? 2u : 0u);
+    uint32_t meta = sign | ((uint32_t)mat << 2);
+    s.pos[s.off] = make_float4((float)p.x, (float)p.y, (float)p.z, __uint_as_float(meta));
+    QShade q;
+    q.n[0] = n.x; q.n[1] = n.y; q.n[2] = n.z;
+    q.ex[0] = ex.x; q.ex[1] = ex.y; q.ex[2] = ex.z;
+    q.w[0] = w.r; q.w[1] = w.g; q.w[2] = w.b;
+    s.shade[s.off] = q;
+    s.off++;
+  }
+  count++;
+}
+
+struct PathCtx {
+  const SceneView *S;
+  const Flags *F;
+  bool emit;
+  QSink g, c;
+  uint32_t ng, nc;
+  C3 base;
+  Counts cnt;
+};
+
+// global-map lookup at a diffuse hit: EstimateRadiance or (with -cache) the cached radiance
+__device__ __forceinline__ void global_query(PathCtx &P, V p, V n, V ex, double ct, int mat, C3 w) {
+  put_query(P.emit, P.g, P.ng, p, n, ex, ct, mat, w);
+}
+
+// MonteCarlo_IndirectSample, montecarlo.cpp:177-305 (W = outer weight of this path)
+__device__ __noinline__ void mc_indirect(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
+  const SceneView &S = *P.S;
+  const Flags &F = *P.F;
+  C3 tw = rgb(1, 1, 1);
+  V ray_start = org;
+  for (int iter = 0; iter < F.max_monte_depth; iter++) {
+    Hit h;
+    if (!scene_intersect(S, org, dir, h)) {
+      P.base += W * (tw * ldc(S.background));
+      break;
+    }
+    P.cnt.monte++;
+    const DMaterial &m = S.mats[h.mat];
+    V view = normalize(h.p - ray_start);
+    double ct = dot(h.n, -view);
+    double R = 0;
+    if (F.fresnel && (m.flags & MF_TRANSPARENT)) R = reflection_coeff(F.ir_air, ct, m.ir);
+    double pd = m.max_kd, pt = m.max_kt;
+    double ps = m.max_ks + R * pt;
+    pt *= (1.0 - R);
+    double pterm = m.max_e + F.prob_absorb;
+    double ptot = pd + pt + ps + pterm;
+    double rnd = rng.next();
+    if (ptot > 1.0) rnd *= ptot;
+    V sb;
+    if (rnd < pd) {
+      V ex = reflective_bounce(h.n, view, ct);
+      global_query(P, h.p, h.n, ex, ct, h.mat, W * (ldc(m.kd) * tw / pd));
+      break;
+    } else if (rnd < pd + pt) {
+      V ex = transmissive_bounce(F.ir_air, h.n, view, ct, m.ir);
+      sb = F.distrib_trans ? specular_sample(ex, m.n, ct, rng) : ex;
+      P.cnt.trans++;
+      tw *= (1.0 - R) * ldc(m.kt) / pt;
+    } else if (rnd < pd + pt + ps) {
+      V ex = reflective_bounce(h.n, view, ct);
+      sb = F.distrib_spec ? specular_sample(ex, m.n, ct, rng) : ex;
+      P.cnt.spec++;
+      tw *= (ldc(m.ks) + R * ldc(m.kt)) / ps;
+    } else {
+      break;
+    }
+    ray_start = h.p + sb * kEps;
+    org = ray_start;
+    dir = sb;
+  }
+}
+
+// MonteCarlo_PathTrace, montecarlo.cpp:16-171
+__device__ __noinline__ void mc_path(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
+  const SceneView &S = *P.S;
+  const Flags &F = *P.F;
+  if (!F.monte_carlo) return;
+  C3 tw = rgb(1, 1, 1);
+  V ray_start = org;
+  for (int iter = 0; iter < F.max_monte_depth; iter++) {
+    Hit h;
+    if (!scene_intersect(S, org, dir, h)) {
+      P.base += W * (tw * ldc(S.background));
+      break;
+    }
+    P.cnt.monte++;
+    const DMaterial &m = S.mats[h.mat];
+    C3 cb = rgb(0, 0, 0);
+    if (F.ambient) cb += ldc(S.ambient);
+    V view = normalize(h.p - ray_start);
+    double ct = dot(h.n, -view);
+    if (m.flags & (MF_DIFFUSE | MF_SPECULAR))
+      direct_illumination(S, F, h.p, h.n, ray_start, cb, m, ct, true, rng, P.cnt);
+    if (F.caustic && (m.flags & MF_DIFFUSE)) {
+      V ex = reflective_bounce(h.n, view, ct);
+      put_query(P.emit, P.c, P.nc, h.p, h.n, ex, ct, h.mat, W * tw);
+      P.cnt.caustic++;
+    }
+    P.base += W * (cb * tw);
+    double R = 0;
+    if (F.specular && F.transmissive && F.fresnel && (m.flags & MF_TRANSPARENT))
+      R = reflection_coeff(F.ir_air, ct, m.ir);
+    double pd = m.max_kd, pt = m.max_kt;
+    double ps = m.max_ks + R * pt;
+    pt *= (1.0 - R);
+    double pterm = m.max_e + F.prob_absorb;
+    double ptot = pd + pt + ps + pterm;
+    double rnd = rng.next();
+    if (ptot > 1.0) rnd *= ptot;
+    V sb;
+    if (rnd < pd) {
+      C3 kd = ldc(m.kd);
+      if (F.indirect) {
+        // IndirectIllumination(inMC): one sample continuing this path's stream
+        V s2 = diffuse_sample(h.n, ct, rng);
+        mc_indirect(P, h.p + s2 * kEps, s2, rng, W * ((kd * kd * tw) / pd));
+        P.cnt.indirect++;
+      } else if (F.fast_global) {
+        V ex = reflective_bounce(h.n, view, ct);
+        global_query(P, h.p, h.n, ex, ct, h.mat, W * (kd * tw / pd));
+        if (!F.cache) P.cnt.indirect++;
+      }
+      break;
+    } else if (rnd < pd + pt) {
+      if (!F.transmissive) break;
+      V ex = transmissive_bounce(F.ir_air, h.n, view, ct, m.ir);
+      sb = F.distrib_trans ? specular_sample(ex, m.n, ct, rng) : ex;
+      P.cnt.trans++;
+      tw *= (1.0 - R) * ldc(m.kt) / pt;
+    } else if (rnd < pd + pt + ps) {
+      if (!F.specular) break;
+      V ex = reflective_bounce(h.n, view, ct);
+      sb = F.distrib_spec ? specular_sample(ex, m.n, ct, rng) : ex;
+      P.cnt.spec++;
+      tw *= (ldc(m.ks) + R * ldc(m.kt)) / ps;
+    } else {
+      break;
+    }
+    ray_start = h.p + sb * kEps;
+    org = ray_start;
+    dir = sb;
+  }
+}
+
+// Expand path slot g of the batch: slot 0 of a primary sample = its own photon-map queries
+// (CausticIllumination / EstimateGlobalIllumination at the primary hit) and base colour;
+// slots 1.. = transmissive, specular and indirect sample paths (raytracer.cpp:47-135).
+template <bool EMIT>
+__global__ __launch_bounds__(128) void path_kernel(RenderArgs a) {
+  int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  Counts cnt = {0, 0, 0, 0, 0, 0};
+  if (g < a.total_paths) {
+    // primary sample owning this slot: last p with path_off[p] <= g
+    int64_t lo = 0, hi = a.nprim;
+    while (hi - lo > 1) {
+      int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)a.path_off[mid] <= g) lo = mid; else hi = mid;
+    }
+    int64_t pb = lo;
+    int slot = (int)(g - a.path_off[pb]);
+    const Spawn &sp = a.spawn[pb];
+    PathCtx P;
+    P.S = &a.S;
+    P.F = &a.F;
+    P.emit = EMIT;
+    P.ng = P.nc = 0;
+    P.base = rgb(0, 0, 0);
+    P.cnt = cnt;
+    if (EMIT) {
+      P.g.pos = a.gpos; P.g.shade = a.gshade; P.g.off = a.goff[g];
+      P.c.pos = a.cpos; P.c.shade = a.cshade; P.c.off = a.coff[g];
+    }
+    if (slot == 0) {
+      P.base = ldc(sp.base);
+      if (sp.hit) {
+        V p = ld3(sp.p), n = ld3(sp.n), view = ld3(sp.v);
+        V ex = reflective_bounce(n, view, sp.ct);
+        if (sp.q_caus) {
+          put_query(EMIT, P.c, P.nc, p, n, ex, sp.ct, sp.mat, rgb(1, 1, 1));
+          P.cnt.caustic++;
+        }
+        if (sp.q_glob) put_query(EMIT, P.g, P.ng, p, n, ex, sp.ct, sp.mat, rgb(1, 1, 1));
+      }
+    } else {
+      int pix, i, j, k;
+      uint64_t psample;
+      decode_primary(a, pb, pix, i, j, k, psample);
+      const SceneView &S = a.S;
+      const Flags &F = a.F;
+      const DMaterial &m = S.mats[sp.mat];
+      V p = ld3(sp.p), n = ld3(sp.n), view = ld3(sp.v);
+      double ct = sp.ct, R = sp.R;
+      int s = slot - 1;
+      Rng rng;
+      if (s < sp.n_t) {
+        // TransmissiveIllumination sample s (raytracer.cpp:47-77)
+        rng.init(F.seed, KIND_TRANS, psample, (uint64_t)s);
+        V ex = transmissive_bounce(F.ir_air, n, view, ct, m.ir);
+        C3 tw = (1.0 - R) * ldc(m.kt);
+        V sb = F.distrib_trans ? specular_sample(ex, m.n, ct, rng) : ex;
+        mc_path(P, p + sb * kEps, sb, rng, tw / (double)sp.n_t);
+        P.cnt.trans++;
+      } else if (s < sp.n_t + sp.n_s) {
+        // SpecularIllumination sample (raytracer.cpp:80-109)
+        s -= sp.n_t;
+        rng.init(F.seed, KIND_SPEC, psample, (uint64_t)s);
+        V ex = reflective_bounce(n, view, ct);
+        C3 tw = ldc(m.kt) * R + ldc(m.ks);
+        V sb = F.distrib_spec ? specular_sample(ex, m.n, ct, rng) : ex;
+        mc_path(P, p + sb * kEps, sb, rng, tw / (double)sp.n_s);
+        P.cnt.spec++;
+      } else {
+        // IndirectIllumination sample (raytracer.cpp:112-135)
+        s -= sp.n_t + sp.n_s;
+        rng.init(F.seed, KIND_IND, psample, (uint64_t)s);
+        V sb = diffuse_sample(n, ct, rng);
+        mc_indirect(P, p + sb * kEps, sb, rng, ldc(m.kd) / (double)sp.n_i);
+        P.cnt.indirect++;
+      }
+    }
+    if (EMIT) {
+      a.base[3 * g] = P.base.r;
+      a.base[3 * g + 1] = P.base.g;
+      a.base[3 * g + 2] = P.base.b;
+    } else {
+      a.cnt_g[g] = P.ng;
+      a.cnt_c[g] = P.nc;
+    }
+    cnt = P.cnt;
+  }
+  if (EMIT) {
+    wave_add(&a.stats[ST_SHADOW], cnt.shadow);
+    wave_add(&a.stats[ST_MONTE], cnt.monte);
+    wave_add(&a.stats[ST_TRANS], cnt.trans);
+    wave_add(&a.stats[ST_SPEC], cnt.spec);
+    wave_add(&a.stats[ST_INDIRECT], cnt.indirect);
+    wave_add(&a.stats[ST_CAUSTIC], cnt.caustic);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// k-NN radiance estimate (R3Kdtree::FindClosestQuick R3Kdtree.cpp:688-784 + EstimateRadiance
+// photon_utils.cpp:72-162). One query per lane; stackless nearest-first traversal of the
+// implicit complete kd-tree (parent = node>>1, sibling = node^1); per-lane max-heap of the K
+// best (d2, index) pairs in LDS laid out [slot][lane] (conflict-free b32 accesses) or, for
+// K > 64, in a global scratch laid out the same way.
+// ---------------------------------------------------------------------------------------
+struct HeapRef {
+  float *d2;
+  int32_t *idx;
+  int stride;  // elements between consecutive slots of one lane
+};
+
+__device__ __forceinline__ bool heap_less(float da, int ia, float db, int ib) {
+  return da < db || (da == db && ia < ib);
+}
+
+// 0-based binary max-heap on (d2, idx)
+__device__ __forceinline__ void heap_push(HeapRef h, int &size, float d, int id) {
+  int c = size++;
+  while (c > 0) {
+    int p = (c - 1) >> 1;
+    float pd = h.d2[p * h.stride];
+    int pi = h.idx[p * h.stride];
+    if (!heap_less(pd, pi, d, id)) break;
+    h.d2[c * h.stride] = pd;
+    h.idx[c * h.stride] = pi;
+    c = p;
+  }
+  h.d2[c * h.stride] = d;
+  h.idx[c * h.stride] = id;
+}
+__device__ __forceinline__ void heap_replace_top(HeapRef h, int size, float d, int id) {
+  int c = 0;
+  while (true) {
+    int l = 2 * c + 1;
+    if (l >= size) break;
+    float ld = h.d2[l * h.stride];
+    int li = h.idx[l * h.stride];
+    int r = l + 1;
+    if (r < size) {
+      float rd = h.d2[r * h.stride];
+      int ri = h.idx[r * h.stride];
+      if (heap_less(ld, li, rd, ri)) { l = r; ld = rd; li = ri; }
+    }
+    if (!heap_less(d, id, ld, li)) break;
+    h.d2[c * h.stride] = ld;
+    h.idx[c * h.stride] = li;
+    c = l;
+  }
+  h.d2[c * h.stride] = d;
+  h.idx[c * h.stride] = id;
+}
+
+__device__ __forceinline__ float metric_d2(float qx, float qy, float qz, float4 p) {
+  float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
+  return __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
+}
+
+// Find the K best photons of query (qx,qy,qz) within r2; returns heap size.
+__device__ __forceinline__ int knn_search(const KdView &M, float qx, float qy, float qz, float r2,
+                                          int K, HeapRef h, uint32_t &visited) {
+  int size = 0;
+  float maxd2 = r2;
+  float topd = 0.f;
+  int topi = 0;
+  if (M.n == 0) return 0;
+  const float2 *nodes = reinterpret_cast<const float2 *>(M.nodes);
+  const float4 *pos = reinterpret_cast<const float4 *>(M.pos4);
+  const int L = M.nleaves;
+  int node = 1;
+  bool done = false;
+  while (!done) {
+    // descend to the near leaf
+    while (node < L) {
+      float2 nd = nodes[node];
+      int axis = __float_as_int(nd.y);
+      float q = (axis == 0) ? qx : ((axis == 1) ? qy : qz);
+      node = 2 * node + ((q - nd.x >= 0.0f) ? 1 : 0);
+    }
+    int leaf = node - L;
+    int64_t s0 = ((int64_t)leaf * M.n) / L, s1 = ((int64_t)(leaf + 1) * M.n) / L;
+    for (int64_t ii = s0; ii < s1; ii++) {
+      float4 p = pos[ii];
+      float d2 = metric_d2(qx, qy, qz, p);
+      if (d2 <= maxd2) {
+        int id = (int)ii;
+        if (size < K) {
+          heap_push(h, size, d2, id);
+          if (size == K) {
+            topd = h.d2[0];
+            topi = h.idx[0];
+            maxd2 = topd;
+          }
+        } else if (heap_less(d2, id, topd, topi)) {
+          heap_replace_top(h, size, d2, id);
+          topd = h.d2[0];
+          topi = h.idx[0];
+          maxd2 = topd;
+        }
+      }
+    }
+    visited += (uint32_t)(s1 - s0);
+    // backtrack to the nearest unvisited far child that may hold candidates
+    while (true) {
+      if (node == 1) { done = true; break; }
+      int parent = node >> 1;
+      float2 nd = nodes[parent];
+      int axis = __float_as_int(nd.y);
+      float q = (axis == 0) ? qx : ((axis == 1) ? qy : qz);
+      float diff = q - nd.x;
+      int near_is_right = (diff >= 0.0f) ? 1 : 0;
+      if ((node & 1) == near_is_right && __fmul_rn(diff, diff) <= maxd2) {
+        node ^= 1;  // far sibling
+        break;
+      }
+      node = parent;
+    }
+  }
+  return size;
+}
+
+template <bool LDS_HEAP>
+__global__ __launch_bounds__(64) void knn_kernel(KnnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int lane = threadIdx.x;
+  int64_t q = (int64_t)blockIdx.x * 64 + lane;
+  uint64_t nfound_total = 0, visited_total = 0, nq_done = 0;
+  if (q < a.nq) {
+    HeapRef h;
+    if (LDS_HEAP) {
+      h.d2 = reinterpret_cast<float *>(smem) + lane;
+      h.idx = reinterpret_cast<int32_t *>(smem + (size_t)a.K * 64 * sizeof(float)) + lane;
+      h.stride = 64;
+    } else {
+      int64_t slot_stride = (int64_t)gridDim.x * 64;
+      h.d2 = a.gheap_d2 + q;
+      h.idx = a.gheap_idx + q;
+      h.stride = (int)slot_stride;
+    }
+    int64_t qi = a.perm ? (int64_t)a.perm[q] : q;
+    float4 qp = a.qpos[qi];
+    uint32_t visited = 0;
+    int num = knn_search(a.map, qp.x, qp.y, qp.z, a.r2f, a.K, h, visited);
+    nfound_total = num;
+    visited_total = visited;
+    nq_done = 1;
+    if (a.mode == KNN_MODE_LIST) {
+      for (int s = 0; s < a.K; s++) {
+        a.out_idx[qi * a.K + s] = (s < num) ? h.idx[s * h.stride] : -1;
+        a.out_d2[qi * a.K + s] = (s < num) ? h.d2[s * h.stride] : -1.0f;
+      }
+      a.out_n[qi] = num;
+    } else {
+      double o0 = 0, o1 = 0, o2 = 0;
+      double maxd2 = kEps;
+      if (num > 0) {
+        if (num < a.K) {
+          maxd2 = a.rmax * a.rmax;
+        } else {
+          for (int s = 0; s < num; s++) {
+            double d = (double)h.d2[s * h.stride];
+            if (d > maxd2) maxd2 = d;
+          }
+        }
+        if (a.mode == KNN_MODE_IRRADIANCE) {
+          // EstimateIrradiance, photon_utils.cpp:209-246
+          for (int s = 0; s < num; s++) {
+            uint32_t e = a.map.rgbe[h.idx[s * h.stride]];
+            uint32_t ex = e >> 24;
+            if (ex) {
+              double inv = ldexp(1.0, (int)ex - 128 - 8);
+              o0 += (double)(e & 255u) * inv;
+              o1 += (double)((e >> 8) & 255u) * inv;
+              o2 += (double)((e >> 16) & 255u) * inv;
+            }
+          }
+          double den = kPi * maxd2;
+          o0 /= den; o1 /= den; o2 /= den;
+        } else {
+          const QShade &sh = a.qshade[qi];
+          uint32_t meta = __float_as_uint(qp.w);
+          uint32_t sign = meta & 3u;
+          const DMaterial &m = a.mats[meta >> 2];
+          double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
+          double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
+          bool spec = (m.flags & MF_SPECULAR) || (m.n < 0);
+          double c1 = 1.0, c2 = 1.0, tot_w = 0;
+          if (a.filter == 1) c1 = 1.0 / (a.fk * sqrt(maxd2));
+          else if (a.filter == 2) {
+            c1 = pow(2.7182818284590452354, -a.fb);
+            c2 = 1.0 / (2.0 * maxd2);
+          }
+          for (int s = 0; s < num; s++) {
+            int id = h.idx[s * h.stride];
+            uint32_t dcode = __float_as_uint(a.map.pos4[4 * (int64_t)id + 3]) & 0xffffu;
+            double ix = a.lut[3 * dcode], iy = a.lut[3 * dcode + 1], iz = a.lut[3 * dcode + 2];
+            double perp = N0 * ix + N1 * iy + N2 * iz;
+            if ((sign == 2u && perp < 0) || (sign == 1u && perp > 0)) continue;
+            uint32_t e = a.map.rgbe[id];
+            uint32_t ee = e >> 24;
+            double inv = ee ? ldexp(1.0, (int)ee - 128 - 8) : 0.0;
+            double p0 = ee ? (double)(e & 255u) * inv : 0.0;
+            double p1 = ee ? (double)((e >> 8) & 255u) * inv : 0.0;
+            double p2 = ee ? (double)((e >> 16) & 255u) * inv : 0.0;
+            double ca = E0 * -ix + E1 * -iy + E2 * -iz;
+            if (ca < 0) ca = 0;
+            double ap = fabs(perp);
+            double pw = spec ? pow(ca, m.n) : 0.0;
+            p0 *= ap * m.kd[0] + pw * m.ks[0];
+            p1 *= ap * m.kd[1] + pw * m.ks[1];
+            p2 *= ap * m.kd[2] + pw * m.ks[2];
+            if (a.filter == 1) {
+              double f = (1.0 - c1 * sqrt((double)h.d2[s * h.stride]));
+              p0 *= f; p1 *= f; p2 *= f;
+            } else if (a.filter == 2) {
+              double w = (1.0 - (1.0 - pow(c1, c2 * (double)h.d2[s * h.stride])) / (1.0 - c1));
+              p0 *= w; p1 *= w; p2 *= w;
+              tot_w += w;
+            }
+            o0 += p0; o1 += p1; o2 += p2;
+          }
+          // photon_utils.cpp:149-158 normalisation
+          bool ok = true;
+          if (a.filter == 0 && maxd2 > 0) {
+            double den = kPi * maxd2;
+            o0 /= den; o1 /= den; o2 /= den;
+          } else if (a.filter == 1 && maxd2 > 0) {
+            double den = (1.0 - 2.0 / 3.0 / a.fk) * kPi * maxd2;
+            o0 /= den; o1 /= den; o2 /= den;
+          } else if (a.filter == 2 && tot_w > 0 && maxd2 > 0) {
+            double sc = a.fa * (num / tot_w) / (kPi * maxd2);
+            o0 *= sc; o1 *= sc; o2 *= sc;
+          } else {
+            ok = false;
+          }
+          if (ok) {
+            o0 *= sh.w[0]; o1 *= sh.w[1]; o2 *= sh.w[2];
+          } else {
+            o0 = o1 = o2 = 0;
+          }
+        }
+      }
+      a.out[3 * qi] = o0;
+      a.out[3 * qi + 1] = o1;
+      a.out[3 * qi + 2] = o2;
+      if (a.out_n) a.out_n[qi] = num;
+      if (a.out_maxd2) a.out_maxd2[qi] = (num > 0) ? (float)maxd2 : 0.0f;
+    }
+  }
+  if (a.stats) {
+    wave_add(&a.stats[ST_KNN], nq_done);
+    wave_add(&a.stats[ST_KNN_PHOTONS], nfound_total);
+    wave_add(&a.stats[ST_KNN_VISITED], visited_total);
+  }
+}
+
+// EstimateCachedRadiance (photon_utils.cpp:165-205) with FindClosest (R3Kdtree.cpp:317-445):
+// nearest photon at distance >= previous + 1e-6 until one passes the side test (Q8 guarded).
+__global__ __launch_bounds__(64) void cached_kernel(KnnArgs a) {
+  int64_t q = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  uint64_t nq_done = 0;
+  if (q < a.nq) {
+    nq_done = 1;
+    float4 qp = a.qpos[q];
+    const QShade &sh = a.qshade[q];
+    uint32_t meta = __float_as_uint(qp.w);
+    uint32_t sign = meta & 3u;
+    const DMaterial &m = a.mats[meta >> 2];
+    double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
+    double out0 = 0, out1 = 0, out2 = 0;
+    double closest = 0;
+    const float2 *nodes = reinterpret_cast<const float2 *>(a.map.nodes);
+    const float4 *pos = reinterpret_cast<const float4 *>(a.map.pos4);
+    const int L = a.map.nleaves;
+    for (int guard = 0; guard < 1 << 20 && a.map.n > 0; guard++) {
+      double mn = closest + kEps;
+      float min2 = (float)(mn * mn);
+      float best2 = a.r2f;
+      int best = -1;
+      int node = 1;
+      bool done = false;
+      while (!done) {
+        while (node < L) {
+          float2 nd = nodes[node];
+          int axis = __float_as_int(nd.y);
+          float qq = (axis == 0) ? qp.x : ((axis == 1) ? qp.y : qp.z);
+          node = 2 * node + ((qq - nd.x >= 0.0f) ? 1 : 0);
+        }
+        int leaf = node - L;
+        int64_t s0 = ((int64_t)leaf * a.map.n) / L, s1 = ((int64_t)(leaf + 1) * a.map.n) / L;
+        for (int64_t ii = s0; ii < s1; ii++) {
+          float d2 = metric_d2(qp.x, qp.y, qp.z, pos[ii]);
+          if (d2 >= min2 && d2 <= best2 && (d2 < best2 || best < 0 || (int)ii < best)) {
+            best2 = d2;
+            best = (int)ii;
+          }
+        }
+        while (true) {
+          if (node == 1) { done = true; break; }
+          int parent = node >> 1;
+          float2 nd = nodes[parent];
+          int axis = __float_as_int(nd.y);
+          float qq = (axis == 0) ? qp.x : ((axis == 1) ? qp.y : qp.z);
+          float diff = qq - nd.x;
+          int near_is_right = (diff >= 0.0f) ? 1 : 0;
+          if ((node & 1) == near_is_right && __fmul_rn(diff, diff) <= best2) {
+            node ^= 1;
+            break;
+          }
+          node = parent;
+        }
+      }
+      closest = sqrt((double)best2);
+      if (best < 0) break;
+      uint32_t dcode = __float_as_uint(a.map.pos4[4 * (int64_t)best + 3]) & 0xffffu;
+      double ix = a.lut[3 * dcode], iy = a.lut[3 * dcode + 1], iz = a.lut[3 * dcode + 2];
+      double perp = N0 * ix + N1 * iy + N2 * iz;
+      if ((sign == 2u && perp < 0) || (sign == 1u && perp > 0)) continue;
+      uint32_t e = a.map.rgbe[best];
+      uint32_t ee = e >> 24;
+      double inv = ee ? ldexp(1.0, (int)ee - 128 - 8) : 0.0;
+      double p0 = ee ? (double)(e & 255u) * inv : 0.0;
+      double p1 = ee ? (double)((e >> 8) & 255u) * inv : 0.0;
+      double p2 = ee ? (double)((e >> 16) & 255u) * inv : 0.0;
+      double ca = sh.ex[0] * -ix + sh.ex[1] * -iy + sh.ex[2] * -iz;
+      if (ca < 0) ca = 0;
+      double ap = fabs(perp);
+      double pw = pow(ca, m.n);
+      p0 *= ap * m.kd[0] + pw * m.ks[0];
+      p1 *= ap * m.kd[1] + pw * m.ks[1];
+      p2 *= ap * m.kd[2] + pw * m.ks[2];
+      out0 = p0 * sh.w[0];
+      out1 = p1 * sh.w[1];
+      out2 = p2 * sh.w[2];
+      break;
+    }
+    a.out[3 * q] = out0;
+    a.out[3 * q + 1] = out1;
+    a.out[3 * q + 2] = out2;
+  }
+  if (a.stats) wave_add(&a.stats[ST_KNN], nq_done);
+}
+
+// ---------------------------------------------------------------------------------------
+// Per-pixel reduction: RenderImage's DOF average + ClampColor + box filter + SetPixelRGB
+// (render.cpp:130-135, 205-221; R2Image.cpp:205-208)
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void reduce_kernel(RenderArgs a) {
+  int pix = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= a.npix) return;
+  int af2 = a.af * a.af;
+  double acc0 = 0, acc1 = 0, acc2 = 0;
+  // row-major subsample order inside the pixel block (render.cpp:207-214 sums j-outer)
+  for (int sub = 0; sub < af2; sub++) {
+    double s0 = 0, s1 = 0, s2 = 0;
+    for (int k = 0; k < a.dof_test; k++) {
+      int64_t b = ((int64_t)pix * af2 + sub) * a.dof_test + k;
+      uint32_t p0 = a.path_off[b], p1 = a.path_off[b + 1];
+      double c0 = 0, c1 = 0, c2 = 0;
+      for (uint32_t g = p0; g < p1; g++) {
+        c0 += a.base[3 * (int64_t)g];
+        c1 += a.base[3 * (int64_t)g + 1];
+        c2 += a.base[3 * (int64_t)g + 2];
+      }
+      for (uint32_t q = a.goff[p0]; q < a.goff[p1]; q++) {
+        c0 += a.gout[3 * (int64_t)q];
+        c1 += a.gout[3 * (int64_t)q + 1];
+        c2 += a.gout[3 * (int64_t)q + 2];
+      }
+      for (uint32_t q = a.coff[p0]; q < a.coff[p1]; q++) {
+        c0 += a.cout[3 * (int64_t)q];
+        c1 += a.cout[3 * (int64_t)q + 1];
+        c2 += a.cout[3 * (int64_t)q + 2];
+      }
+      s0 += c0; s1 += c1; s2 += c2;
+    }
+    s0 /= a.dof_test; s1 /= a.dof_test; s2 /= a.dof_test;
+    s0 = s0 < 0 ? 0 : (s0 > 1.0 ? 1.0 : s0);
+    s1 = s1 < 0 ? 0 : (s1 > 1.0 ? 1.0 : s1);
+    s2 = s2 < 0 ? 0 : (s2 > 1.0 ? 1.0 : s2);
+    acc0 += s0; acc1 += s1; acc2 += s2;
+  }
+  double bw = 1.0 / a.af / a.af;
+  double r = bw * acc0, g = bw * acc1, b = bw * acc2;
+  int2 pc = a.pixels[pix];
+  int64_t o = ((int64_t)pc.y * a.out_w + pc.x) * 3;
+  if (a.rgbf) {
+    a.rgbf[o] = (float)r;
+    a.rgbf[o + 1] = (float)g;
+    a.rgbf[o + 2] = (float)b;
+  }
+  if (a.rgb8) {
+    a.rgb8[o] = (uint8_t)(255 * r);
+    a.rgb8[o + 1] = (uint8_t)(255 * g);
+    a.rgb8[o + 2] = (uint8_t)(255 * b);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Photon tracing (photontracer.cpp:28-373)
+// ---------------------------------------------------------------------------------------
+// RNRgb_to_RGBE, graphics_utils.cpp:50-61
+__device__ __forceinline__ uint32_t rgbe_encode(C3 c) {
+  double mx = maxch(c);
+  if (!(mx > 0)) return 0u;
+  int e;
+  double m = frexp(mx, &e);
+  uint32_t r = (uint8_t)(256.0 * c.r / mx * m);
+  uint32_t g = (uint8_t)(256.0 * c.g / mx * m);
+  uint32_t b = (uint8_t)(256.0 * c.b / mx * m);
+  uint32_t x = (uint8_t)(e + 128);
+  return r | (g << 8) | (b << 16) | (x << 24);
+}
+
+struct PhotonOut {
+  gi_photon_dev *out;
+  uint32_t off;
+  uint32_t count;
+};
+
+// StorePhoton, photon_utils.cpp:40-65
+__device__ __forceinline__ void store_photon(bool emit, PhotonOut &o, C3 power, V inc, V p) {
+  if (emit) {
+    gi_photon_dev ph;
+    ph.pos[0] = (float)p.x;
+    ph.pos[1] = (float)p.y;
+    ph.pos[2] = (float)p.z;
+    ph.rgbe = rgbe_encode(power);
+    int phi = (uint8_t)(255.0 * (atan2(inc.y, inc.x) + kPi) / (2.0 * kPi));
+    double z = inc.z < -1.0 ? -1.0 : (inc.z > 1.0 ? 1.0 : inc.z);
+    int theta = (uint8_t)(255.0 * acos(z) / kPi);
+    ph.dir = (uint16_t)(phi * 256 + theta);
+    ph.flags = 0;
+    o.out[o.off + o.count] = ph;
+  }
+  o.count++;
+}
+
+// PhotonTrace, photontracer.cpp:28-176
+__device__ __noinline__ void photon_trace(const SceneView &S, const Flags &F, V org, V dir,
+                                          C3 photon, bool caustic, Rng &rng, bool emit,
+                                          PhotonOut &o) {
+  bool store = (!caustic && !F.fast_global);
+  V ray_start = org;
+  for (int iter = 0; iter < F.max_photon_depth; iter++) {
+    Hit h;
+    if (!scene_intersect(S, org, dir, h)) break;
+    const DMaterial &m = S.mats[h.mat];
+    V view = normalize(h.p - ray_start);
+    double ct = dot(h.n, -view);
+    if ((m.flags & MF_DIFFUSE) && store) store_photon(emit, o, photon, view, h.p);
+    double R = 0;
+    if (F.fresnel && (m.flags & MF_TRANSPARENT)) R = reflection_coeff(F.ir_air, ct, m.ir);
+    double mc = maxch(photon);
+    double pd = maxch(ldc(m.kd) * photon) / mc;
+    double pt = maxch(ldc(m.kt) * photon) / mc;
+    double ps = (maxch(ldc(m.ks) * photon) / mc) + R * pt;
+    pt *= (1.0 - R);
+    double ptot = pd + pt + ps + F.prob_absorb;
+    double rnd = rng.next();
+    if (ptot > 1.0) rnd *= ptot;
+    V sb;
+    if (rnd < pd) {
+      if (caustic) break;
+      store = true;
+      sb = diffuse_sample(h.n, ct, rng);
+      photon *= ldc(m.kd) / pd;
+    } else if (rnd < pd + pt) {
+      if (caustic) store = true;
+      V ex = transmissive_bounce(F.ir_air, h.n, view, ct, m.ir);
+      sb = F.distrib_trans ? specular_sample(ex, m.n, ct, rng) : ex;
+      photon *= (1.0 - R) * ldc(m.kt) / pt;
+    } else if (rnd < pd + pt + ps) {
+      if (caustic) store = true;
+      V ex = reflective_bounce(h.n, view, ct);
+      sb = F.distrib_spec ? specular_sample(ex, m.n, ct, rng) : ex;
+      photon *= (ldc(m.ks) + R * ldc(m.kt)) / ps;
+    } else {
+      break;
+    }
+    ray_start = h.p + sb * kEps;
+    org = ray_start;
+    dir = sb;
+  }
+}
+
+// EmitPhotons, photontracer.cpp:182-373, one photon per lane (emission index e0 + lane)
+template <bool EMIT>
+__global__ __launch_bounds__(128) void photon_kernel(PhotonArgs a) {
+  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= a.n) return;
+  const SceneView &S = a.S;
+  const Flags &F = a.F;
+  const DLight &L = S.lights[a.light];
+  Rng rng;
+  rng.init(F.seed, a.caustic ? KIND_PHOTON_CAUSTIC : KIND_PHOTON_GLOBAL, (uint64_t)(a.e0 + j), 0);
+  C3 photon = ldc(L.color);
+  double tot = photon.r + photon.g + photon.b;  // NormalizeColor, graphics_utils.cpp:25-36
+  if (tot > 0) photon = photon / tot;
+  V org, dir;
+  if (L.kind == LK_DIR) {
+    V ln = ld3(L.dir);
+    V center = ld3(S.centroid) - ln * S.radius * 3.0;
+    double r1, r2;
+    do {
+      r1 = rng.next() * 2.0 - 1.0;
+      r2 = rng.next() * 2.0 - 1.0;
+    } while (r1 * r1 + r2 * r2 > 1.0);
+    org = ((r1 * ld3(L.su) + r2 * ld3(L.sv)) + center) + ln * kEps;
+    dir = ln;
+  } else if (L.kind == LK_POINT) {
+    double x, y, z;
+    do {
+      x = rng.next() * 2.0 - 1.0;
+      y = rng.next() * 2.0 - 1.0;
+      z = rng.next() * 2.0 - 1.0;
+    } while (x * x + y * y + z * z > 1.0);
+    org = ld3(L.pos);
+    dir = normalize(mk(x, y, z));
+  } else if (L.kind == LK_SPOT) {
+    V ln = ld3(L.dir);
+    double cutoff = fabs(cos(L.cutoff));
+    int attempts_left = 20;
+    V sd;
+    do {
+      sd = specular_sample(ln, L.dropoff, 1.0, rng);
+    } while (dot(sd, ln) < cutoff && attempts_left-- > 0);
+    if (attempts_left == 0) sd = specular_sample(ln, L.dropoff, cutoff, rng);
+    org = ld3(L.pos);
+    dir = sd;
+  } else if (L.kind == LK_AREA) {
+    V ln = ld3(L.dir);
+    double r1, r2;
+    do {
+      r1 = rng.next() * 2.0 - 1.0;
+      r2 = rng.next() * 2.0 - 1.0;
+    } while (r1 * r1 + r2 * r2 > 1.0);
+    org = ((r1 * ld3(L.su) + r2 * ld3(L.sv)) + ld3(L.pos)) + ln * kEps;
+    dir = diffuse_sample(ln, 1.0, rng);
+  } else {
+    V ln = ld3(L.dir);
+    double r1 = rng.next() - 0.5;
+    double r2 = rng.next() - 0.5;
+    org = ((r1 * ld3(L.su) + r2 * ld3(L.sv)) + ld3(L.pos)) + ln * kEps;
+    dir = diffuse_sample(ln, 1.0, rng);
+  }
+  PhotonOut o;
+  o.out = a.out;
+  o.off = EMIT ? a.offsets[j] : 0u;
+  o.count = 0;
+  photon_trace(S, F, org, dir, photon, a.caustic != 0, rng, EMIT, o);
+  if (!EMIT) a.counts[j] = o.count;
+}
+
+// directional-light disk basis needs the scene radius: computed on host (gi_host.cpp)
+
+// ---------------------------------------------------------------------------------------
+// R3Scene::Intersects test seam
+// ---------------------------------------------------------------------------------------
+__global__ void intersect_kernel(SceneView S, int64_t n, const double *org, const double *dir,
+                                 int32_t *hit, double *t, double *point, double *normal,
+                                 int32_t *mat) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Hit h;
+  bool ok = scene_intersect(S, ld3(org + 3 * i), ld3(dir + 3 * i), h);
+  hit[i] = ok;
+  t[i] = ok ? h.t : 0.0;
+  point[3 * i] = ok ? h.p.x : 0; point[3 * i + 1] = ok ? h.p.y : 0; point[3 * i + 2] = ok ? h.p.z : 0;
+  normal[3 * i] = ok ? h.n.x : 0; normal[3 * i + 1] = ok ? h.n.y : 0; normal[3 * i + 2] = ok ? h.n.z : 0;
+  mat[i] = ok ? h.mat : -2;
+}
+
+// ---------------------------------------------------------------------------------------
+// host-callable launchers
+// ---------------------------------------------------------------------------------------
+static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+
+hipError_t launch_scan(const uint32_t *in, uint32_t *out, int64_t n, ScanTemp &tmp,
+                       hipStream_t st) {
+  // out has n+1 entries; out[n] = total
+  if (n <= 0) {
+    return hipMemsetAsync(out, 0, sizeof(uint32_t), st);
+  }
+  int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+  uint32_t *sums = tmp.level[tmp.depth];
+  uint32_t *soff = tmp.level_out[tmp.depth];
+  // write total via an extra padded element: scan n+1 with in[n] treated as 0
+  scan_tile_kernel<<<nblk(n, SCAN_TILE), SCAN_BLOCK, 0, st>>>(in, out, sums, n);
+  if (nb > 1) {
+    tmp.depth++;
+    hipError_t e = launch_scan(sums, soff, nb, tmp, st);
+    tmp.depth--;
+    if (e != hipSuccess) return e;
+    scan_add_kernel<<<nblk(n, 256), 256, 0, st>>>(out, soff, n);
+    // total = soff[nb]
+    return hipMemcpyAsync(out + n, soff + nb, sizeof(uint32_t), hipMemcpyDeviceToDevice, st);
+  }
+  return hipMemcpyAsync(out + n, sums, sizeof(uint32_t), hipMemcpyDeviceToDevice, st);
+}
+
+void launch_primary(const RenderArgs &a, hipStream_t st) {
+  primary_kernel<<<nblk(a.nprim, 256), 256, 0, st>>>(a);
+}
+void launch_path(const RenderArgs &a, bool emit, hipStream_t st) {
+  if (a.total_paths == 0) return;
+  if (emit) path_kernel<true><<<nblk(a.total_paths, 128), 128, 0, st>>>(a);
+  else path_kernel<false><<<nblk(a.total_paths, 128), 128, 0, st>>>(a);
+}
+void launch_reduce(const RenderArgs &a, hipStream_t st) {
+  reduce_kernel<<<nblk(a.npix, 64), 64, 0, st>>>(a);
+}
+void launch_knn(const KnnArgs &a, bool lds_heap, hipStream_t st) {
+  if (a.nq == 0) return;
+  if (lds_heap) {
+    size_t sm = (size_t)a.K * 64 * (sizeof(float) + sizeof(int32_t));
+    knn_kernel<true><<<nblk(a.nq, 64), 64, sm, st>>>(a);
+  } else {
+    knn_kernel<false><<<nblk(a.nq, 64), 64, 0, st>>>(a);
+  }
+}
+void launch_cached(const KnnArgs &a, hipStream_t st) {
+  if (a.nq == 0) return;
+  cached_kernel<<<nblk(a.nq, 64), 64, 0, st>>>(a);
+}
+void launch_photons(const PhotonArgs &a, bool emit, hipStream_t st) {
+  if (a.n == 0) return;
+  if (emit) photon_kernel<true><<<nblk(a.n, 128), 128, 0, st>>>(a);
+  else photon_kernel<false><<<nblk(a.n, 128), 128, 0, st>>>(a);
+}
+void launch_intersect(const SceneView &S, int64_t n, const double *org, const double *dir,
+                      int32_t *hit, double *t, double *point, double *normal, int32_t *mat,
+                      hipStream_t st) {
+  if (n == 0) return;
+  intersect_kernel<<<nblk(n, 128), 128, 0, st>>>(S, n, org, dir, hit, t, point, normal, mat);
+}
+
+}  // namespace gi

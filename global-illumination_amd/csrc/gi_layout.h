@@ -1,0 +1,107 @@
+// gi_layout.h -- POD layout of the flattened, device-resident scene and photon maps.
+//
+// The reference walks a pointer-based scene graph (R3SceneNode -> R3SceneElement -> R3Shape,
+// R3SceneNode.cpp:420-510, R3SceneElement.cpp:209-243). On the device the graph is flattened
+// into arrays in the same depth-first order (so "first element wins ties" semantics are kept):
+//   DNode[]    nodes in pre-order; root = 0; world->local transform chain via parent links
+//   DElement[] elements in (node pre-order, element order); material + shape range + bbox
+//   DShape[]   shapes in element order; triangles / meshes index into DTri[]
+//   DTri[]     triangles with precomputed plane and edge planes (R3Cont.cpp:491-512)
+// Everything geometric is fp64 (RNScalar is double; the 1e-6 tolerances of RNScalar.h:225-316
+// need it). Photon maps are fp32 (see DESIGN.md "Data layout").
+#pragma once
+#include <stdint.h>
+
+namespace gi {
+
+enum ShapeKind { SK_TRI = 0, SK_MESH = 1, SK_SPHERE = 2, SK_BOX = 3, SK_CIRCLE = 4,
+                 SK_CYLINDER = 5, SK_CONE = 6 };
+enum LightKind { LK_DIR = 0, LK_POINT = 1, LK_SPOT = 2, LK_AREA = 3, LK_RECT = 4 };
+enum MatFlags { MF_AMBIENT = 1, MF_DIFFUSE = 2, MF_SPECULAR = 4, MF_TRANSPARENT = 8,
+                MF_EMISSIVE = 16 };
+
+struct DTri {
+  double p0[3];
+  double n[3];       // plane normal
+  double d;          // plane offset
+  double ev[3][3];   // edge-plane normals  normalize(n x e_i)
+  double ed[3];      // edge-plane offsets
+  double bmin[3], bmax[3];
+};
+
+struct DShape {
+  int32_t kind;
+  int32_t tri_first;   // SK_TRI: triangle index; SK_MESH: first triangle
+  int32_t tri_count;   // SK_MESH: number of triangles
+  int32_t pad;
+  double c[3];         // sphere / circle centre
+  double n[3];         // circle normal
+  double r;            // radius
+  double bmin[3], bmax[3];  // shape bbox (box shape = the box itself)
+};
+
+struct DElement {
+  int32_t material;    // index into DMaterial[] (defaults are materialised by the loader)
+  int32_t node;        // owning node
+  int32_t shape_first, shape_count;
+  double bmin[3], bmax[3];  // element bbox in node-local coordinates
+};
+
+struct DNode {
+  double Tinv[12];     // world(parent)->local rows 0..2 of R4Matrix inverse
+  double T[12];        // local->parent
+  int32_t parent;      // -1 for root
+  int32_t identity;    // transform is exactly the identity
+  int32_t elem_first, elem_count;
+};
+
+struct DMaterial {
+  double ka[3], kd[3], ks[3], kt[3], e[3];
+  double n, ir;
+  int32_t flags;       // MatFlags (R3Brdf::UpdateFlags, R3Brdf.cpp:338-348)
+  int32_t pad;
+  // derived per-material constants used by the Monte Carlo loops (montecarlo.cpp:94-99)
+  double max_kd, max_kt, max_ks, max_e;
+};
+
+struct DLight {
+  int32_t kind;
+  int32_t active;
+  double color[3];
+  double intensity;
+  double pos[3];
+  double dir[3];       // directional dir / spot dir / area normal / rect normal
+  double ca, la, qa;
+  double dropoff, cutoff;   // spot
+  double radius;            // area
+  double a1[3], a2[3];      // rect axes (unit)
+  double len1, len2;
+  // precomputed sampling frames (illumination_utils.cpp:109-119, 281-283)
+  double su[3], sv[3];      // area: disk basis scaled by radius; rect: a1*len1, a2*len2
+  double area;              // pi r^2 or |a1 x a2|
+  double nr_ax1[3], nr_ax2[3];  // no-shadow area sampling axes (R3AreaLight.cpp:145-153)
+};
+
+struct DCamera {
+  double eye[3];
+  double far_org[3], far_right[3], far_up[3];  // render.cpp:67-69
+  double dof_u[3], dof_v[3];                   // render.cpp:72-77
+};
+
+// Device photon map: SoA in kd-leaf order.
+//   pos4[i]   = (x, y, z, bitcast(dir | flags << 16))
+//   rgbe[i]   = packed RGBE bytes (r | g<<8 | b<<16 | e<<24)
+//   nodes[j]  = (split, bitcast(axis)) for internal node j in [1, nleaves) of the implicit
+//               complete tree; leaf l in [nleaves, 2*nleaves) holds photons
+//               [start(l - nleaves), start(l - nleaves + 1)), start(j) = j * n / nleaves.
+struct KdView {
+  const float *pos4;       // float4
+  const uint32_t *rgbe;
+  const float *nodes;      // float2 per node (index 0 unused)
+  int64_t n;
+  int32_t nleaves;
+  int32_t levels;
+  float bmin[3], bmax[3];
+};
+
+}  // namespace gi

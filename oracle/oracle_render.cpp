@@ -1,0 +1,1666 @@
+// oracle_render.cpp -- TEST INFRASTRUCTURE ONLY (checker; never linked into the product).
+//
+// CPU restatement of the reference hot path: RenderImage / RayTrace / Monte Carlo loops /
+// photon tracing / kd-tree k-NN radiance estimate. Each function cites the reference
+// file:line it follows. Deviations (documented in DESIGN.md "Oracle"):
+//   - RNG: keyed counter streams instead of the unseeded per-thread mt19937
+//     (RNScalar.cpp:99-131): stream per primary sample, per spawned sample path, per photon;
+//   - photon positions fp32 + fp32 k-NN metric (oracle_core.h);
+//   - photon emission runs as ONE emitter (the reference splits quotas per CPU thread,
+//     photonmap.cpp:294-329); photons are stored in emission order;
+//   - kd-tree pivots are deterministic (reference: random quickselect R3Kdtree.cpp:1563);
+//   - Q8 (EstimateCachedRadiance null dereference) is guarded: no photon -> no contribution.
+#include "oracle_scene.h"
+#include "../include/gi.h"
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <cstdlib>
+#include <string>
+#include <thread>
+#include <vector>
+#include <zlib.h>
+
+namespace oracle {
+
+// ---------------------------------------------------------------------------------------
+// Per-thread counters (render.cpp:26-41)
+// ---------------------------------------------------------------------------------------
+struct Counters {
+  uint64_t ray = 0, shadow = 0, monte = 0, trans = 0, spec = 0, indirect = 0, caustic = 0;
+  uint64_t knn = 0, knn_photons = 0;
+  void add(const Counters &o) {
+    ray += o.ray; shadow += o.shadow; monte += o.monte; trans += o.trans; spec += o.spec;
+    indirect += o.indirect; caustic += o.caustic; knn += o.knn; knn_photons += o.knn_photons;
+  }
+};
+
+// ---------------------------------------------------------------------------------------
+// kd-tree over photons (R3Kdtree<Photon*>, R3Kdtree.cpp)
+// ---------------------------------------------------------------------------------------
+struct KdNode {
+  int child[2] = {-1, -1};
+  int dim = 0;
+  double split = 0;
+  int start = 0, count = 0;  // leaf range into KdTree::idx
+};
+struct KdTree {
+  std::vector<Photon> ph;   // storage (emission) order
+  std::vector<int> idx;     // leaf-ordered photon indices
+  std::vector<KdNode> nodes;
+  Box bbox;
+  bool empty() const { return ph.empty(); }
+};
+
+static int longest_axis(const Box &b) {
+  V3 d = b.mx - b.mn;
+  if (d.x > d.y && d.x > d.z) return 0;
+  if (d.y > d.z) return 1;
+  return 2;
+}
+
+// InsertPoints, R3Kdtree.cpp:1624-1671 (leaf if n < 32; split the node box's longest axis at
+// the median). Pivot selection deterministic (nth_element) instead of random quickselect.
+static int kd_insert(KdTree &t, const Box &box, int lo, int n) {
+  int id = (int)t.nodes.size();
+  t.nodes.push_back(KdNode());
+  if (n < 32) {
+    t.nodes[id].start = lo;
+    t.nodes[id].count = n;
+    return id;
+  }
+  int dim = longest_axis(box);
+  int mid = n / 2;
+  std::nth_element(t.idx.begin() + lo, t.idx.begin() + lo + mid, t.idx.begin() + lo + n,
+                   [&](int a, int b) { return t.ph[a].pos[dim] < t.ph[b].pos[dim]; });
+  double split = t.ph[t.idx[lo + mid]].pos[dim];
+  Box b0 = box, b1 = box;
+  b0.mx[dim] = split;
+  b1.mn[dim] = split;
+  t.nodes[id].dim = dim;
+  t.nodes[id].split = split;
+  int c0 = kd_insert(t, b0, lo, mid);
+  int c1 = kd_insert(t, b1, lo + mid, n - mid);
+  t.nodes[id].child[0] = c0;
+  t.nodes[id].child[1] = c1;
+  return id;
+}
+
+static void kd_build(KdTree &t) {
+  t.nodes.clear();
+  t.idx.resize(t.ph.size());
+  for (size_t i = 0; i < t.ph.size(); i++) t.idx[i] = (int)i;
+  t.bbox = Box();
+  for (auto &p : t.ph) t.bbox.add(V3(p.pos[0], p.pos[1], p.pos[2]));
+  if (!t.ph.empty()) kd_insert(t, t.bbox, 0, (int)t.ph.size());
+}
+
+struct Near {
+  float d2;
+  int i;
+  bool operator<(const Near &o) const { return d2 < o.d2; }  // PointAndDistanceSqd ordering
+};
+
+// slack for box pruning against the fp32 metric (pruning stays conservative)
+static inline bool box_far(double box_d2, double maxd2) { return box_d2 > maxd2 * (1.0 + 1e-6); }
+
+static double box_dist2(const float qf[3], const Box &b) {
+  double s = 0;
+  for (int i = 0; i < 3; i++) {
+    double q = qf[i], d = 0;
+    if (q > b.mx[i]) d = q - b.mx[i];
+    else if (q < b.mn[i]) d = b.mn[i] - q;
+    s += d * d;
+  }
+  return s;
+}
+
+// FindClosestQuick (recursive), R3Kdtree.cpp:688-784: child 0 first; leaf points accepted
+// when min2 <= d2 <= max2; delayed make_heap at k; replace-max with pop_heap/push_heap.
+static void kd_quick(const KdTree &t, int ni, const Box &box, const float qf[3], float min2,
+                     float max2, int k, std::vector<Near> &res) {
+  if ((int)res.size() == k) max2 = res[0].d2;
+  const KdNode &n = t.nodes[ni];
+  if (n.child[0] >= 0) {
+    if (box_far(box_dist2(qf, box), max2)) return;
+    double side = (double)qf[n.dim] - n.split;
+    if ((side <= 0) || !box_far(side * side, max2)) {
+      Box cb = box;
+      cb.mx[n.dim] = n.split;
+      kd_quick(t, n.child[0], cb, qf, min2, max2, k, res);
+    }
+    if ((int)res.size() == k) max2 = res[0].d2;
+    if ((side >= 0) || !box_far(side * side, max2)) {
+      Box cb = box;
+      cb.mn[n.dim] = n.split;
+      kd_quick(t, n.child[1], cb, qf, min2, max2, k, res);
+    }
+  } else {
+    for (int j = 0; j < n.count; j++) {
+      int pi = t.idx[n.start + j];
+      float d2 = knn_d2(qf, t.ph[pi].pos);
+      if (d2 >= min2 && d2 <= max2) {
+        int size = (int)res.size();
+        Near nd{d2, pi};
+        if (size < k - 1) {
+          res.push_back(nd);
+        } else if (size == k - 1) {
+          res.push_back(nd);
+          std::make_heap(res.begin(), res.end());
+          max2 = res[0].d2;
+        } else {
+          std::pop_heap(res.begin(), res.end());
+          res[k - 1] = nd;
+          std::push_heap(res.begin(), res.end());
+          max2 = res[0].d2;
+        }
+      }
+    }
+  }
+}
+
+static void kd_find_quick(const KdTree &t, V3 q, double max_dist, int k, std::vector<Near> &res) {
+  res.clear();
+  if (t.empty()) return;
+  float qf[3] = {(float)q.x, (float)q.y, (float)q.z};
+  float max2 = (float)(max_dist * max_dist);
+  kd_quick(t, 0, t.bbox, qf, 0.0f, max2, k, res);
+}
+
+// FindClosest (single nearest with min distance), R3Kdtree.cpp:317-445
+static void kd_closest(const KdTree &t, int ni, const Box &box, const float qf[3], float min2,
+                       int &best, float &best2) {
+  const KdNode &n = t.nodes[ni];
+  if (n.child[0] >= 0) {
+    if (box_far(box_dist2(qf, box), best2)) return;
+    double side = (double)qf[n.dim] - n.split;
+    Box b0 = box, b1 = box;
+    b0.mx[n.dim] = n.split;
+    b1.mn[n.dim] = n.split;
+    if (side <= 0) {
+      kd_closest(t, n.child[0], b0, qf, min2, best, best2);
+      if (!box_far(side * side, best2)) kd_closest(t, n.child[1], b1, qf, min2, best, best2);
+    } else {
+      kd_closest(t, n.child[1], b1, qf, min2, best, best2);
+      if (!box_far(side * side, best2)) kd_closest(t, n.child[0], b0, qf, min2, best, best2);
+    }
+  } else {
+    for (int j = 0; j < n.count; j++) {
+      int pi = t.idx[n.start + j];
+      float d2 = knn_d2(qf, t.ph[pi].pos);
+      if (d2 >= min2 && d2 <= best2) {
+        best2 = d2;
+        best = pi;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Colour / geometry utilities (utils/graphics_utils.cpp)
+// ---------------------------------------------------------------------------------------
+static void clamp_color(Rgb &c) {  // :14-22
+  for (int i = 0; i < 3; i++) {
+    if (c[i] < 0) c[i] = 0;
+    if (c[i] > 1.0) c[i] = 1.0;
+  }
+}
+static void normalize_color(Rgb &c) {  // :25-36
+  double total = 0;
+  for (int i = 0; i < 3; i++) total += c[i];
+  if (total > 0) c = c / total;
+}
+static double max_channel(const Rgb &c) {  // :39-46
+  double m = 0;
+  for (int i = 0; i < 3; i++)
+    if (c[i] > m) m = c[i];
+  return m;
+}
+// RNRgb_to_RGBE, :50-61 (guard: max <= 0 encodes black)
+static void rgb_to_rgbe(const Rgb &c, uint8_t *out) {
+  double mx = max_channel(c);
+  if (!(mx > 0)) { out[0] = out[1] = out[2] = out[3] = 0; return; }
+  int e;
+  double m = frexp(mx, &e);
+  out[0] = (uint8_t)(256.0 * c[0] / mx * m);
+  out[1] = (uint8_t)(256.0 * c[1] / mx * m);
+  out[2] = (uint8_t)(256.0 * c[2] / mx * m);
+  out[3] = (uint8_t)(e + 128);
+}
+// RGBE_to_RNRgb, :64-77
+static Rgb rgbe_to_rgb(const uint8_t *in) {
+  if (!in[3]) return Rgb(0, 0, 0);
+  double inv = ldexp(1.0, ((int)in[3]) - 128 - 8);
+  return Rgb(in[0], in[1], in[2]) * inv;
+}
+
+struct Ctx;
+static bool intersect(const Ctx &c, V3 org, V3 dir, Hit &h);
+
+// Schlick, :95-101
+static double reflection_coeff(double ir_air, double cos_theta, double ir_mat) {
+  double r0 = pow((ir_air - ir_mat) / (ir_air + ir_mat), 2);
+  return (r0 + (1.0 - r0) * pow((1.0 - fabs(cos_theta)), 5));
+}
+// ReflectiveBounce, :104-117
+static V3 reflective_bounce(V3 normal, V3 view, double cos_theta) {
+  if (cos_theta < 0) { normal = -normal; cos_theta *= -1.0; }
+  V3 perp = normal * cos_theta;
+  V3 r = view + perp * 2.0;
+  return normalize(r);
+}
+// TransmissiveBounce, :121-154
+static V3 transmissive_bounce(double ir_air, V3 normal, V3 view, double cos_theta, double ir_mat) {
+  double eta;
+  if (cos_theta < 0) {
+    eta = ir_mat / ir_air;
+    normal = -normal;
+    cos_theta *= -1.0;
+  } else {
+    eta = ir_air / ir_mat;
+  }
+  double theta = acos(cos_theta);
+  double sin_phi = eta * sin(theta);
+  if (sin_phi < -1.0 || 1.0 < sin_phi) return reflective_bounce(normal, view, cos_theta);
+  double phi = asin(sin_phi);
+  V3 par = normalize(view + normal * cos_theta);
+  V3 refr = par * tan(phi) - normal;
+  return normalize(refr);
+}
+// R3Vector::Rotate (Goldstein), R3Vector.cpp:352-363
+static V3 rotate(V3 v, V3 axis, double theta) {
+  double ct = cos(theta);
+  double d = dot(v, axis);
+  V3 cr = cross(v, axis);
+  v = v * ct;
+  v = v + axis * d * (1.0 - ct);
+  v = v - cr * sin(theta);
+  return v;
+}
+// Diffuse_ImportanceSample, :162-185
+static V3 diffuse_sample(V3 normal, double cos_theta, Rng &rng) {
+  if (cos_theta < 0) normal = -normal;
+  double theta = acos(sqrt(rng.next()));
+  double phi = 2 * PI * rng.next();
+  V3 perp(normal.y, -normal.x, 0);
+  if (1.0 - fabs(normal.z) < 0.1) perp = V3(normal.z, 0, -normal.x);
+  perp = normalize(perp);
+  V3 r = perp * sin(theta) + normal * cos(theta);
+  r = rotate(r, normal, phi);
+  return normalize(r);
+}
+// Specular_ImportanceSample, :189-216
+static V3 specular_sample(V3 exact, double n, double cos_theta, Rng &rng) {
+  double angle_limit = (1.0 - acos(fabs(cos_theta)) * 2.0 / PI);
+  double alpha = acos(pow(rng.next(), 1.0 / (n + 1.0))) * angle_limit;
+  double phi = 2.0 * PI * rng.next();
+  V3 perp(exact.y, -exact.x, 0);
+  if (1.0 - fabs(exact.z) < 0.1) perp = V3(exact.z, 0, -exact.x);
+  perp = normalize(perp);
+  V3 r = perp * sin(alpha) + exact * cos(alpha);
+  r = rotate(r, exact, phi);
+  return normalize(r);
+}
+
+// ---------------------------------------------------------------------------------------
+// Context (the reference's globals, photonmap.cpp:40-138)
+// ---------------------------------------------------------------------------------------
+struct Ctx {
+  gi_params P;
+  Scene scene;
+  double scene_radius = 0;
+  Rgb scene_ambient;
+  int nlights = 0;
+  KdTree gmap, cmap;
+  std::vector<double> lut;  // 65536 x 3
+  int64_t g_emitted = 0, c_emitted = 0;
+};
+
+static bool intersect(const Ctx &c, V3 org, V3 dir, Hit &h) {
+  return scene_intersect(c.scene, org, dir, h);
+}
+static const Brdf &brdf_of(const Ctx &c, int m) {
+  static Brdf def = [] {
+    Brdf d;
+    d.ka = Rgb(0.2, 0.2, 0.2); d.kd = Rgb(0.8, 0.8, 0.8); d.n = 0.2; d.ir = 1.0;
+    return d;
+  }();
+  return (m >= 0) ? c.scene.materials[m] : def;  // R3default_brdf via R3default_material
+}
+
+// IntersectionDist, graphics_utils.cpp:84-92
+static double intersection_dist(const Ctx &c, V3 org, V3 dir) {
+  Hit h;
+  if (intersect(c, org, dir, h)) return dist(org, h.point);
+  return RN_INF;
+}
+// RayIlluminationTest, illumination_utils.cpp:16-31 (Q13)
+static bool ray_illumination_test(const Ctx &c, V3 point_in_scene, V3 point_on_light,
+                                  Counters &cnt) {
+  double unoccluded = dist(point_on_light, point_in_scene);
+  V3 dir = normalize(point_in_scene - point_on_light);  // R3Ray(p_light, p_scene)
+  double len = intersection_dist(c, point_on_light, dir);
+  cnt.shadow++;
+  return fabs(len - unoccluded) < EPS;
+}
+// TestLightIntersection, illumination_utils.cpp:35-84
+static int test_light_intersection(V3 point, V3 eye, const Light &L) {
+  if (L.type == L_AREA) {
+    V3 v = point - L.pos;
+    double vlen = length(v);
+    v = normalize(v);
+    if (fabs(dot(v, L.dir)) < EPS && vlen <= L.radius) {
+      if (dot(L.dir, eye - point) <= 0) return -1;
+      return 1;
+    }
+  } else if (L.type == L_RECT) {
+    V3 v = point - L.pos;
+    double c1 = dot(v, L.a1), c2 = dot(v, L.a2);
+    v = normalize(v);
+    if (fabs(dot(v, L.dir)) < EPS && fabs(c1 * 2.0) <= L.len1 && fabs(c2 * 2.0) <= L.len2) {
+      if (dot(L.dir, eye - point) <= 0) return -1;
+      return 1;
+    }
+  }
+  return 0;
+}
+
+// disk basis used by area-light sampling, illumination_utils.cpp:109-119
+static void disk_basis(V3 n, double radius, V3 &u, V3 &v) {
+  u = V3(n.y, -n.x, 0);
+  if (1.0 - fabs(n.z) < 0.1) u = V3(n.z, 0, -n.x);
+  v = cross(u, n);
+  u = normalize(u) * radius;
+  v = normalize(v) * radius;
+}
+
+// ComputeAreaLightReflection (:91-262) and ComputeRectLightReflection (:265-417); both
+// multiply the whole accumulated colour by the shadow hit rate (Q1).
+static void soft_light(const Ctx &c, const Light &L, Rgb &color, const Brdf &brdf, V3 eye,
+                       V3 p, V3 normal, int nls, int nes, Rng &rng, Counters &cnt) {
+  if (!L.active) return;
+  bool area = (L.type == L_AREA);
+  V3 center = L.pos, ln = L.dir;
+  if (dot(ln, p - center) < 0) return;
+  V3 u, v, a1, a2;
+  double areasz;
+  if (area) {
+    disk_basis(ln, L.radius, u, v);
+    areasz = PI * pow(L.radius, 2.0);
+  } else {
+    a1 = L.a1 * L.len1;
+    a2 = L.a2 * L.len2;
+    areasz = length(cross(a1, a2));
+  }
+  auto sample_point = [&]() -> V3 {
+    double r1, r2;
+    if (area) {
+      do {
+        r1 = (rng.next() * 2.0) - 1.0;
+        r2 = (rng.next() * 2.0) - 1.0;
+      } while (r1 * r1 + r2 * r2 > 1.0);
+      return ((r1 * u + r2 * v) + center) + ln * EPS;
+    }
+    r1 = rng.next() - 0.5;
+    r2 = rng.next() - 0.5;
+    return ((r1 * a1 + r2 * a2) + center) + ln * EPS;
+  };
+  auto intensity_at = [&](V3 sp, V3 &Ldir) {
+    double I = L.intensity;
+    double d = dist(p, sp);
+    double denom = L.ca;
+    denom += d * L.la;
+    denom += d * d * L.qa;
+    if (isPos(denom)) I /= denom;
+    Ldir = normalize(sp - p);
+    I *= dot(ln, -Ldir) * 2.0;
+    return I;
+  };
+  int total_samples = 0, total_hits = 0;
+  if (brdf.isDiffuse()) {
+    double weight = 0;
+    int hits = 0;
+    for (int i = 0; i < nls; i++) {
+      V3 sp = sample_point();
+      if (ray_illumination_test(c, p, sp, cnt)) {
+        hits++;
+        V3 Ld;
+        double I = intensity_at(sp, Ld);
+        weight += I * fabs(dot(normal, Ld));
+      }
+    }
+    if (hits > 0) color += weight * brdf.kd * L.color * areasz / (double)hits;
+    total_hits += hits;
+    total_samples += nls;
+  }
+  if (brdf.isSpecular()) {
+    double weight = 0;
+    int hits = 0;
+    int n2 = nls * 2;
+    V3 V = normalize(eye - p);
+    for (int i = 0; i < n2; i++) {
+      V3 sp = sample_point();
+      if (ray_illumination_test(c, p, sp, cnt)) {
+        hits++;
+        V3 Ld;
+        double I = intensity_at(sp, Ld);
+        double NL = dot(normal, Ld);
+        V3 R = (2.0 * NL) * normal - Ld;
+        double VR = dot(V, R);
+        if (isNegOrZero(VR)) continue;
+        weight += (I * pow(VR, brdf.n));
+      }
+    }
+    if (hits > 0) color += weight * brdf.ks * L.color * areasz / (double)hits;
+    total_hits += hits;
+    total_samples += n2;
+  }
+  int hits = 0;
+  for (int i = 0; i < nes; i++) {
+    V3 sp = sample_point();
+    if (ray_illumination_test(c, p, sp, cnt)) hits++;
+  }
+  total_hits += hits;
+  total_samples += nes;
+  if (total_samples > 0) color *= ((double)total_hits) / total_samples;
+}
+
+// Light::Reflection for point / spot / directional (R3PointLight.cpp:213-244 with
+// IntensityAtPoint :111-121 and R3SpotLight.cpp:105-115; R3DirectionalLight.cpp:134-166)
+// and the area/rect Reflection used without shadows (R3AreaLight.cpp:122-330,
+// R3RectLight.cpp:150-340).
+static Rgb light_reflection(const Light &L, const Brdf &brdf, V3 eye, V3 p, V3 normal,
+                            int max_samples, Rng &rng) {
+  if (!L.active) return Rgb(0, 0, 0);
+  const Rgb &Dc = brdf.kd, &Sc = brdf.ks;
+  double s = brdf.n;
+  if (L.type == L_POINT || L.type == L_SPOT) {
+    double d = dist(p, L.pos);
+    double denom = L.ca;
+    denom += d * L.la;
+    denom += d * d * L.qa;
+    double I = isZero(denom) ? L.intensity : (L.intensity / denom);
+    if (L.type == L_SPOT) {
+      V3 ML = normalize(p - L.pos);
+      double ca = dot(ML, L.dir);
+      if (cos(L.cutoff) > ca) I = 0.0;
+      else I = I * pow(ca, L.dropoff);
+    }
+    V3 Ld = normalize(L.pos - p);
+    double NL = dot(normal, Ld);
+    V3 R = (2.0 * NL) * normal - Ld;
+    V3 V = normalize(eye - p);
+    double VR = dot(V, R);
+    Rgb rgb = I * Dc * L.color * fabs(NL);
+    if (isPos(VR)) rgb += (I * pow(VR, s)) * Sc * L.color;
+    return rgb;
+  }
+  if (L.type == L_DIR) {
+    double I = L.intensity;
+    V3 Ld = -L.dir;
+    double NL = dot(normal, Ld);
+    V3 R = (2.0 * NL) * normal - Ld;
+    V3 V = normalize(eye - p);
+    double VR = dot(V, R);
+    Rgb rgb = (I * fabs(NL)) * Dc * L.color;
+    if (isPos(VR)) rgb += (I * pow(VR, s) * Sc * L.color);
+    return rgb;
+  }
+  // area / rect without shadow tests
+  bool area = (L.type == L_AREA);
+  V3 dirn = L.dir, center = L.pos;
+  if (dot(dirn, p - center) < 0) return Rgb(0, 0, 0);
+  V3 ax1, ax2;
+  double areasz;
+  if (area) {
+    int dim = (fabs(dirn.x) <= fabs(dirn.y)) ? ((fabs(dirn.x) <= fabs(dirn.z)) ? 0 : 2)
+                                              : ((fabs(dirn.y) <= fabs(dirn.z)) ? 1 : 2);
+    V3 e(0, 0, 0);
+    e[dim] = 1.0;
+    ax1 = normalize(cross(dirn, e));
+    ax2 = normalize(cross(dirn, ax1));
+    ax1 = ax1 * L.radius;
+    ax2 = ax2 * L.radius;
+    areasz = PI * L.radius * L.radius;
+  } else {
+    ax1 = L.a1 * L.len1;
+    ax2 = L.a2 * L.len2;
+    areasz = length(cross(ax1, ax2));
+  }
+  auto contrib = [&](bool spec) {
+    int count = 0;
+    Rgb sum;
+    int target = spec ? 2 * max_samples : max_samples;
+    for (int i = 0; (spec ? i < target : count < target); i++) {
+      double r1, r2;
+      if (area) {
+        r1 = (rng.next() * 2.0) - 1.0;
+        r2 = (rng.next() * 2.0) - 1.0;
+        if (r1 * r1 + r2 * r2 > 1) continue;
+      } else {
+        r1 = rng.next() - 0.5;
+        r2 = rng.next() - 0.5;
+      }
+      V3 sp = center;
+      sp = sp + r1 * ax1;
+      sp = sp + r2 * ax2;
+      count++;
+      double I = L.intensity;
+      double d = dist(p, sp);
+      double denom = L.ca;
+      denom += d * L.la;
+      denom += d * d * L.qa;
+      if (isPos(denom)) I /= denom;
+      V3 Ld = normalize(sp - p);
+      I *= dot(dirn, -Ld) * 2.0;
+      double NL = dot(normal, Ld);
+      if (!spec) {
+        sum += (I * fabs(NL)) * Dc * L.color;
+      } else {
+        V3 R = (2.0 * NL) * normal - Ld;
+        V3 V = normalize(eye - p);
+        double VR = dot(V, R);
+        if (isNegOrZero(VR)) continue;
+        sum += (I * pow(VR, s) * Sc * L.color);
+      }
+    }
+    Rgb mean = sum;
+    if (count > 0) mean = mean / (double)count;
+    return areasz * mean;
+  };
+  Rgb diff = contrib(false);
+  Rgb spec = contrib(true);
+  return diff + spec;
+}
+
+// ComputeIllumination, illumination_utils.cpp:425-494
+static void compute_illumination(const Ctx &c, Rgb &color, const Light &L, const Brdf &brdf,
+                                 V3 eye, V3 p, V3 normal, double cos_theta, bool inMC, Rng &rng,
+                                 Counters &cnt) {
+  const gi_params &P = c.P;
+  bool compute_shadows = P.shadows && (!inMC || (P.recursive_shadows && inMC));
+  int nls = P.light_test, nes = P.shadow_test;
+  if (inMC) { nls = 2; nes = 0; }  // Q14
+  if (!compute_shadows) {
+    color += light_reflection(L, brdf, eye, p, normal, nls, rng);
+    return;
+  }
+  V3 pol;
+  if (L.type == L_DIR) {
+    pol = p - L.dir * c.scene_radius * 3.0;
+  } else if (L.type == L_POINT || L.type == L_SPOT) {
+    pol = L.pos;
+  } else {
+    if (!P.soft_shadows) {
+      pol = L.pos + EPS * L.dir;
+    } else {
+      soft_light(c, L, color, brdf, eye, p, normal, nls, nes, rng, cnt);
+      return;
+    }
+  }
+  double side = dot(normal, pol - p);
+  if ((side > 0 && cos_theta < 0) || (side < 0 && cos_theta > 0)) return;
+  if (ray_illumination_test(c, p, pol, cnt))
+    color += light_reflection(L, brdf, eye, p, normal, nls, rng);
+}
+
+// DirectIllumination, raytracer.cpp:18-44
+static void direct_illumination(const Ctx &c, V3 p, V3 normal, V3 eye, Rgb &color,
+                                const Brdf &brdf, double cos_theta, bool inMC, Rng &rng,
+                                Counters &cnt) {
+  bool should_emit = true;
+  for (int k = 0; k < c.nlights; k++) {
+    const Light &L = c.scene.lights[k];
+    int li = test_light_intersection(p, eye, L);
+    if (li != 0) {
+      if (li == -1) should_emit = false;
+      continue;
+    }
+    compute_illumination(c, color, L, brdf, eye, p, normal, cos_theta, inMC, rng, cnt);
+  }
+  if (should_emit) color += brdf.e;
+}
+
+// ---------------------------------------------------------------------------------------
+// Radiance estimates (utils/photon_utils.cpp)
+// ---------------------------------------------------------------------------------------
+// EstimateRadiance, :72-162
+static void estimate_radiance(const Ctx &c, V3 p, V3 normal, Rgb &color, const Brdf &brdf,
+                              V3 exact, double cos_theta, const KdTree &map, int k, double r,
+                              int filter, Counters *cnt, int *nfound_out = nullptr,
+                              float *maxd2_out = nullptr) {
+  std::vector<Near> near;
+  kd_find_quick(map, p, r, k, near);
+  int num = (int)near.size();
+  if (cnt) { cnt->knn++; cnt->knn_photons += num; }
+  if (nfound_out) *nfound_out = num;
+  if (maxd2_out) *maxd2_out = 0;
+  if (num == 0) return;
+  double maxd2 = EPS;
+  if (num < k) {
+    maxd2 = r * r;
+  } else {
+    for (int i = 0; i < num; i++)
+      if ((double)near[i].d2 > maxd2) maxd2 = near[i].d2;
+  }
+  if (maxd2_out) *maxd2_out = (float)maxd2;
+  const gi_params &P = c.P;
+  Rgb est;
+  double c1 = 1.0, c2 = 1.0, total_w = 0;
+  if (filter == GI_FILTER_CONE) c1 = 1.0 / (P.filter_const_k * sqrt(maxd2));
+  else if (filter == GI_FILTER_GAUSS) {
+    c1 = pow(2.7182818284590452354, -P.filter_const_b);
+    c2 = 1.0 / (2.0 * maxd2);
+  }
+  for (int i = 0; i < num; i++) {
+    const Photon &ph = map.ph[near[i].i];
+    int d = ph.dir;
+    V3 inc(c.lut[3 * d], c.lut[3 * d + 1], c.lut[3 * d + 2]);
+    double perp = dot(normal, inc);
+    if ((cos_theta < 0 && perp < 0) || (cos_theta > 0 && perp > 0)) continue;
+    Rgb pc = rgbe_to_rgb(ph.rgbe);
+    double ca = dot(exact, -inc);
+    if (ca < 0) ca = 0;
+    pc *= fabs(perp) * brdf.kd + pow(ca, brdf.n) * brdf.ks;
+    if (filter == GI_FILTER_CONE) {
+      pc *= (1.0 - c1 * sqrt((double)near[i].d2));
+    } else if (filter == GI_FILTER_GAUSS) {
+      double w = (1.0 - (1.0 - pow(c1, c2 * (double)near[i].d2)) / (1.0 - c1));
+      pc *= w;
+      total_w += w;
+    }
+    est += pc;
+  }
+  if (filter == GI_FILTER_DISK && maxd2 > 0) {
+    est = est / (PI * maxd2);
+  } else if (filter == GI_FILTER_CONE && maxd2 > 0) {
+    est = est / ((1.0 - 2.0 / 3.0 / P.filter_const_k) * PI * maxd2);
+  } else if (filter == GI_FILTER_GAUSS && total_w > 0 && maxd2 > 0) {
+    est *= P.filter_const_a * (num / total_w) / (PI * maxd2);
+  } else {
+    return;
+  }
+  color += est;
+}
+
+// EstimateCachedRadiance, :165-205 (Q8 guarded)
+static void estimate_cached(const Ctx &c, V3 p, V3 normal, Rgb &color, const Brdf &brdf,
+                            V3 exact, double cos_theta, const KdTree &map, double r) {
+  if (map.empty()) return;
+  float qf[3] = {(float)p.x, (float)p.y, (float)p.z};
+  double closest_dist = 0;
+  int best;
+  V3 inc;
+  double perp;
+  do {
+    double mn = closest_dist + EPS;
+    float min2 = (float)(mn * mn);
+    float best2 = (float)(r * r);
+    best = -1;
+    kd_closest(map, 0, map.bbox, qf, min2, best, best2);
+    closest_dist = sqrt((double)best2);
+    if (best < 0) return;
+    int d = map.ph[best].dir;
+    inc = V3(c.lut[3 * d], c.lut[3 * d + 1], c.lut[3 * d + 2]);
+    perp = dot(normal, inc);
+  } while ((cos_theta < 0 && perp < 0) || (cos_theta > 0 && perp > 0));
+  Rgb pc = rgbe_to_rgb(map.ph[best].rgbe);
+  double ca = dot(exact, -inc);
+  if (ca < 0) ca = 0;
+  pc *= fabs(perp) * brdf.kd + pow(ca, brdf.n) * brdf.ks;
+  color += pc;
+}
+
+// EstimateIrradiance, :209-246
+static void estimate_irradiance(V3 p, Rgb &color, const KdTree &map, int k, double r) {
+  std::vector<Near> near;
+  kd_find_quick(map, p, r, k, near);
+  int num = (int)near.size();
+  if (num == 0) return;
+  double maxd2 = EPS;
+  if (num < k) maxd2 = r * r;
+  else
+    for (int i = 0; i < num; i++)
+      if ((double)near[i].d2 > maxd2) maxd2 = near[i].d2;
+  Rgb est;
+  for (int i = 0; i < num; i++) est += rgbe_to_rgb(map.ph[near[i].i].rgbe);
+  est = est / (PI * maxd2);
+  color += est;
+}
+
+// BuildDirectionLookupTable, :253-272
+static void build_lut(std::vector<double> &lut) {
+  lut.assign(65536 * 3, 0.0);
+  for (int phi = 0; phi < 256; phi++)
+    for (int theta = 0; theta < 256; theta++) {
+      double tp = (phi * (2.0 * PI) / 255.0) - PI;
+      double tt = (theta * PI / 255.0);
+      V3 n = normalize(V3(sin(tt) * cos(tp), sin(tt) * sin(tp), cos(tt)));
+      int i = 256 * phi + theta;
+      lut[3 * i] = n.x; lut[3 * i + 1] = n.y; lut[3 * i + 2] = n.z;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Shading (raytracer.cpp) and Monte Carlo (montecarlo.cpp)
+// ---------------------------------------------------------------------------------------
+static void mc_indirect_sample(const Ctx &c, V3 org, V3 dir, Rgb &color, Rng &rng,
+                               Counters &cnt);
+
+// IndirectIllumination, raytracer.cpp:112-135 (samples get their own streams; in a Monte
+// Carlo path the single sample continues the path's stream)
+static void indirect_illumination(const Ctx &c, V3 p, V3 normal, Rgb &color, const Brdf &brdf,
+                                  double cos_theta, bool inMC, Rng *path_rng, uint64_t psample,
+                                  Counters &cnt) {
+  if (!brdf.isDiffuse()) return;
+  Rgb tw = brdf.kd;
+  double hw = max_channel(tw);
+  int n = (int)ceil((c.P.indirect_test * hw + c.P.indirect_test) / 2.0);
+  if (inMC) n = 1;
+  Rgb buf;
+  for (int i = 0; i < n; i++) {
+    Rng own;
+    Rng &rng = inMC ? *path_rng : (own = Rng(c.P.seed, KIND_IND, psample, i), own);
+    V3 sb = diffuse_sample(normal, cos_theta, rng);
+    mc_indirect_sample(c, p + sb * EPS, sb, buf, rng, cnt);
+    cnt.indirect++;
+  }
+  color += (buf / (double)n) * tw;
+}
+
+// CausticIllumination, raytracer.cpp:138-149
+static void caustic_illumination(const Ctx &c, V3 p, V3 normal, Rgb &color, const Brdf &brdf,
+                                 V3 view, double cos_theta, Counters &cnt) {
+  if (!brdf.isDiffuse()) return;
+  V3 exact = reflective_bounce(normal, view, cos_theta);
+  estimate_radiance(c, p, normal, color, brdf, exact, cos_theta, c.cmap,
+                    c.P.caustic_estimate_size, c.P.caustic_estimate_dist, c.P.caustic_filter,
+                    &cnt);
+  cnt.caustic++;
+}
+
+// EstimateGlobalIllumination, raytracer.cpp:151-167
+static void estimate_global_illumination(const Ctx &c, V3 p, V3 normal, Rgb &color,
+                                         const Brdf &brdf, V3 view, double cos_theta,
+                                         Counters &cnt) {
+  if (!brdf.isDiffuse()) return;
+  V3 exact = reflective_bounce(normal, view, cos_theta);
+  if (c.P.irradiance_cache) {
+    estimate_cached(c, p, normal, color, brdf, exact, cos_theta, c.gmap,
+                    c.P.global_estimate_dist);
+  } else {
+    estimate_radiance(c, p, normal, color, brdf, exact, cos_theta, c.gmap,
+                      c.P.global_estimate_size, c.P.global_estimate_dist, c.P.global_filter,
+                      &cnt);
+    cnt.indirect++;
+  }
+}
+
+// MonteCarlo_PathTrace, montecarlo.cpp:16-171
+static void mc_path_trace(const Ctx &c, V3 org, V3 dir, Rgb &color, Rng &rng, Counters &cnt) {
+  const gi_params &P = c.P;
+  if (!P.monte_carlo) return;
+  Rgb tw(1, 1, 1);
+  V3 ray_start = org;
+  for (int iter = 0; iter < P.max_monte_depth; iter++) {
+    Hit h;
+    if (intersect(c, org, dir, h)) {
+      cnt.monte++;
+      const Brdf &brdf = brdf_of(c, h.material);
+      Rgb cb;
+      if (P.ambient) cb += c.scene_ambient;
+      V3 view = normalize(h.point - ray_start);
+      double cos_theta = dot(h.normal, -view);
+      if (brdf.isDiffuse() || brdf.isSpecular())
+        direct_illumination(c, h.point, h.normal, ray_start, cb, brdf, cos_theta, true, rng, cnt);
+      if (P.caustic_illum && brdf.isDiffuse())
+        caustic_illumination(c, h.point, h.normal, cb, brdf, view, cos_theta, cnt);
+      color += cb * tw;
+      double R = 0;
+      if (P.specular_illum && P.transmissive_illum && P.fresnel && brdf.isTransparent())
+        R = reflection_coeff(P.ir_air, cos_theta, brdf.ir);
+      double pd = max_channel(brdf.kd);
+      double pt = max_channel(brdf.kt);
+      double ps = max_channel(brdf.ks) + R * pt;
+      pt *= (1.0 - R);
+      double pterm = max_channel(brdf.e) + P.prob_absorb;
+      double ptot = pd + pt + ps + pterm;
+      double rnd = rng.next();
+      if (ptot > 1.0) rnd *= ptot;
+      V3 sb;
+      if (rnd < pd) {
+        if (P.indirect_illum) {
+          cb = Rgb();
+          indirect_illumination(c, h.point, h.normal, cb, brdf, cos_theta, true, &rng, 0, cnt);
+          color += cb * brdf.kd * tw / pd;
+        } else if (P.fast_global) {
+          cb = Rgb();
+          estimate_global_illumination(c, h.point, h.normal, cb, brdf, view, cos_theta, cnt);
+          color += cb * brdf.kd * tw / pd;
+        }
+        break;
+      } else if (rnd < pd + pt) {
+        if (!P.transmissive_illum) break;
+        V3 ex = transmissive_bounce(P.ir_air, h.normal, view, cos_theta, brdf.ir);
+        sb = P.distrib_transmissive ? specular_sample(ex, brdf.n, cos_theta, rng) : ex;
+        cnt.trans++;
+        tw *= (1.0 - R) * brdf.kt / pt;
+      } else if (rnd < pd + pt + ps) {
+        if (!P.specular_illum) break;
+        V3 ex = reflective_bounce(h.normal, view, cos_theta);
+        sb = P.distrib_specular ? specular_sample(ex, brdf.n, cos_theta, rng) : ex;
+        cnt.spec++;
+        tw *= (brdf.ks + R * brdf.kt) / ps;
+      } else {
+        break;
+      }
+      ray_start = h.point + sb * EPS;
+      org = ray_start;
+      dir = sb;
+    } else {
+      color += tw * c.scene.background;
+      break;
+    }
+  }
+}
+
+// MonteCarlo_IndirectSample, montecarlo.cpp:177-305
+static void mc_indirect_sample(const Ctx &c, V3 org, V3 dir, Rgb &color, Rng &rng,
+                               Counters &cnt) {
+  const gi_params &P = c.P;
+  Rgb tw(1, 1, 1);
+  V3 ray_start = org;
+  for (int iter = 0; iter < P.max_monte_depth; iter++) {
+    Hit h;
+    if (intersect(c, org, dir, h)) {
+      cnt.monte++;
+      const Brdf &brdf = brdf_of(c, h.material);
+      V3 view = normalize(h.point - ray_start);
+      double cos_theta = dot(h.normal, -view);
+      double R = 0;
+      if (P.fresnel && brdf.isTransparent()) R = reflection_coeff(P.ir_air, cos_theta, brdf.ir);
+      double pd = max_channel(brdf.kd);
+      double pt = max_channel(brdf.kt);
+      double ps = max_channel(brdf.ks) + R * pt;
+      pt *= (1.0 - R);
+      double pterm = max_channel(brdf.e) + P.prob_absorb;
+      double ptot = pd + pt + ps + pterm;
+      double rnd = rng.next();
+      if (ptot > 1.0) rnd *= ptot;
+      V3 sb;
+      if (rnd < pd) {
+        Rgb cb;
+        V3 ex = reflective_bounce(h.normal, view, cos_theta);
+        if (P.irradiance_cache)
+          estimate_cached(c, h.point, h.normal, cb, brdf, ex, cos_theta, c.gmap,
+                          P.global_estimate_dist);
+        else
+          estimate_radiance(c, h.point, h.normal, cb, brdf, ex, cos_theta, c.gmap,
+                            P.global_estimate_size, P.global_estimate_dist, P.global_filter,
+                            &cnt);
+        color += cb * brdf.kd * tw / pd;
+        break;
+      } else if (rnd < pd + pt) {
+        V3 ex = transmissive_bounce(P.ir_air, h.normal, view, cos_theta, brdf.ir);
+        sb = P.distrib_transmissive ? specular_sample(ex, brdf.n, cos_theta, rng) : ex;
+        cnt.trans++;
+        tw *= (1.0 - R) * brdf.kt / pt;
+      } else if (rnd < pd + pt + ps) {
+        V3 ex = reflective_bounce(h.normal, view, cos_theta);
+        sb = P.distrib_specular ? specular_sample(ex, brdf.n, cos_theta, rng) : ex;
+        cnt.spec++;
+        tw *= (brdf.ks + R * brdf.kt) / ps;
+      } else {
+        break;
+      }
+      ray_start = h.point + sb * EPS;
+      org = ray_start;
+      dir = sb;
+    } else {
+      color += tw * c.scene.background;
+      break;
+    }
+  }
+}
+
+// TransmissiveIllumination (raytracer.cpp:47-77) / SpecularIllumination (:80-109)
+static void bounce_illumination(const Ctx &c, bool trans, V3 p, V3 normal, Rgb &color,
+                                const Brdf &brdf, V3 view, double cos_theta, double coeff,
+                                uint64_t psample, Counters &cnt) {
+  const gi_params &P = c.P;
+  V3 exact;
+  Rgb tw;
+  int test;
+  bool distrib;
+  if (trans) {
+    exact = transmissive_bounce(P.ir_air, normal, view, cos_theta, brdf.ir);
+    tw = coeff * brdf.kt;
+    test = P.transmissive_test;
+    distrib = P.distrib_transmissive;
+  } else {
+    exact = reflective_bounce(normal, view, cos_theta);
+    tw = brdf.kt * coeff + brdf.ks;
+    test = P.specular_test;
+    distrib = P.distrib_specular;
+  }
+  double hw = max_channel(tw);
+  int n = (int)ceil((test * hw + test) / 2.0);
+  Rgb buf;
+  for (int i = 0; i < n; i++) {
+    Rng rng(P.seed, trans ? KIND_TRANS : KIND_SPEC, psample, i);
+    V3 sb = distrib ? specular_sample(exact, brdf.n, cos_theta, rng) : exact;
+    mc_path_trace(c, p + sb * EPS, sb, buf, rng, cnt);
+    if (trans) cnt.trans++; else cnt.spec++;
+  }
+  color += (buf / (double)n) * tw;
+}
+
+// RayTrace, raytracer.cpp:174-233
+static void ray_trace(const Ctx &c, const Hit &h, V3 eye, Rgb &color, Rng &rng,
+                      uint64_t psample, Counters &cnt) {
+  const gi_params &P = c.P;
+  const Brdf &brdf = brdf_of(c, h.material);
+  if (P.ambient) color += c.scene_ambient;
+  V3 point = h.point, normal = h.normal;
+  V3 view = normalize(point - eye);
+  double cos_theta = dot(normal, -view);
+  double R = 0;
+  if (P.ambient && brdf.isAmbient()) color += brdf.ka;
+  if (P.direct_illum && (brdf.isDiffuse() || brdf.isSpecular()))
+    direct_illumination(c, point, normal, eye, color, brdf, cos_theta, false, rng, cnt);
+  if (P.transmissive_illum && brdf.isTransparent()) {
+    if (P.specular_illum && P.fresnel) R = reflection_coeff(P.ir_air, cos_theta, brdf.ir);
+    if (R < 1.0)
+      bounce_illumination(c, true, point, normal, color, brdf, view, cos_theta, 1.0 - R, psample,
+                          cnt);
+  }
+  if (P.specular_illum && (brdf.isSpecular() || R > 0))
+    bounce_illumination(c, false, point, normal, color, brdf, view, cos_theta, R, psample, cnt);
+  if (P.indirect_illum && brdf.isDiffuse())
+    indirect_illumination(c, point, normal, color, brdf, cos_theta, false, nullptr, psample, cnt);
+  if (P.caustic_illum && brdf.isDiffuse())
+    caustic_illumination(c, point, normal, color, brdf, view, cos_theta, cnt);
+  if (P.direct_photon_illum && brdf.isDiffuse())
+    estimate_global_illumination(c, point, normal, color, brdf, view, cos_theta, cnt);
+}
+
+// ---------------------------------------------------------------------------------------
+// Photon tracing (photontracer.cpp, photonmap.cpp, photon_utils.cpp StorePhoton)
+// ---------------------------------------------------------------------------------------
+// StorePhoton, photon_utils.cpp:40-65 (direction code clamped to the valid acos domain)
+static void store_photon(const Rgb &power, V3 inc, V3 p, std::vector<Photon> &out) {
+  Photon ph;
+  ph.pos[0] = (float)p.x; ph.pos[1] = (float)p.y; ph.pos[2] = (float)p.z;
+  rgb_to_rgbe(power, ph.rgbe);
+  int phi = (uint8_t)(255.0 * (atan2(inc.y, inc.x) + PI) / (2.0 * PI));
+  double z = inc.z < -1.0 ? -1.0 : (inc.z > 1.0 ? 1.0 : inc.z);
+  int theta = (uint8_t)(255.0 * acos(z) / PI);
+  ph.dir = (uint16_t)(phi * 256 + theta);
+  ph.flags = 0;
+  out.push_back(ph);
+}
+
+// PhotonTrace, photontracer.cpp:28-176
+static void photon_trace(const Ctx &c, V3 org, V3 dir, Rgb photon, bool caustic, Rng &rng,
+                         std::vector<Photon> &out) {
+  const gi_params &P = c.P;
+  bool store = (!caustic && !P.fast_global);
+  V3 ray_start = org;
+  for (int iter = 0; iter < P.max_photon_depth; iter++) {
+    Hit h;
+    if (!intersect(c, org, dir, h)) break;
+    const Brdf &brdf = brdf_of(c, h.material);
+    V3 view = normalize(h.point - ray_start);
+    double cos_theta = dot(h.normal, -view);
+    if (brdf.isDiffuse() && store) store_photon(photon, view, h.point, out);
+    double R = 0;
+    if (P.fresnel && brdf.isTransparent()) R = reflection_coeff(P.ir_air, cos_theta, brdf.ir);
+    double mc = max_channel(photon);
+    double pd = max_channel(brdf.kd * photon) / mc;
+    double pt = max_channel(brdf.kt * photon) / mc;
+    double ps = (max_channel(brdf.ks * photon) / mc) + R * pt;
+    pt *= (1.0 - R);
+    double ptot = pd + pt + ps + P.prob_absorb;
+    double rnd = rng.next();
+    if (ptot > 1.0) rnd *= ptot;
+    V3 sb;
+    if (rnd < pd) {
+      if (caustic) break;
+      store = true;
+      sb = diffuse_sample(h.normal, cos_theta, rng);
+      photon *= brdf.kd / pd;
+    } else if (rnd < pd + pt) {
+      if (caustic) store = true;
+      V3 ex = transmissive_bounce(P.ir_air, h.normal, view, cos_theta, brdf.ir);
+      sb = P.distrib_transmissive ? specular_sample(ex, brdf.n, cos_theta, rng) : ex;
+      photon *= (1.0 - R) * brdf.kt / pt;
+    } else if (rnd < pd + pt + ps) {
+      if (caustic) store = true;
+      V3 ex = reflective_bounce(h.normal, view, cos_theta);
+      sb = P.distrib_specular ? specular_sample(ex, brdf.n, cos_theta, rng) : ex;
+      photon *= (brdf.ks + R * brdf.kt) / ps;
+    } else {
+      break;
+    }
+    ray_start = h.point + sb * EPS;
+    org = ray_start;
+    dir = sb;
+  }
+}
+
+// EmitPhotons, photontracer.cpp:182-373 (one photon, stream rng)
+static void emit_one(const Ctx &c, const Light &L, bool caustic, Rng &rng,
+                     std::vector<Photon> &out) {
+  Rgb photon = L.color;
+  normalize_color(photon);
+  V3 org, dir;
+  if (L.type == L_DIR) {
+    V3 ln = L.dir;
+    V3 center = c.scene.centroid - ln * c.scene_radius * 3.0;
+    V3 u, v;
+    disk_basis(ln, c.scene_radius, u, v);
+    double r1, r2;
+    do {
+      r1 = rng.next() * 2.0 - 1.0;
+      r2 = rng.next() * 2.0 - 1.0;
+    } while (r1 * r1 + r2 * r2 > 1.0);
+    org = ((r1 * u + r2 * v) + center) + ln * EPS;
+    dir = ln;
+  } else if (L.type == L_POINT) {
+    double x, y, z;
+    do {
+      x = rng.next() * 2.0 - 1.0;
+      y = rng.next() * 2.0 - 1.0;
+      z = rng.next() * 2.0 - 1.0;
+    } while (x * x + y * y + z * z > 1.0);
+    org = L.pos;
+    dir = normalize(V3(x, y, z));
+  } else if (L.type == L_SPOT) {
+    V3 ln = L.dir;
+    double cutoff = fabs(cos(L.cutoff));
+    int attempts_left = 20;
+    V3 sd;
+    do {
+      sd = specular_sample(ln, L.dropoff, 1.0, rng);
+    } while (dot(sd, ln) < cutoff && attempts_left-- > 0);
+    if (attempts_left == 0) sd = specular_sample(ln, L.dropoff, cutoff, rng);
+    org = L.pos;
+    dir = sd;
+  } else if (L.type == L_AREA) {
+    V3 ln = L.dir;
+    V3 u, v;
+    disk_basis(ln, L.radius, u, v);
+    double r1, r2;
+    do {
+      r1 = rng.next() * 2.0 - 1.0;
+      r2 = rng.next() * 2.0 - 1.0;
+    } while (r1 * r1 + r2 * r2 > 1.0);
+    org = ((r1 * u + r2 * v) + L.pos) + ln * EPS;
+    dir = diffuse_sample(ln, 1.0, rng);
+  } else {
+    V3 ln = L.dir;
+    V3 a1 = L.a1 * L.len1, a2 = L.a2 * L.len2;
+    double r1 = rng.next() - 0.5;
+    double r2 = rng.next() - 0.5;
+    org = ((r1 * a1 + r2 * a2) + L.pos) + ln * EPS;
+    dir = diffuse_sample(ln, 1.0, rng);
+  }
+  photon_trace(c, org, dir, photon, caustic, rng, out);
+}
+
+// LightPower, graphics_utils.cpp:223-258
+static double light_power(const Ctx &c, const Light &L) {
+  double area = 1.0, flux = 4.0 * PI;
+  if (L.type == L_DIR) {
+    area = PI * pow(c.scene_radius, 2.0);
+    flux = 1.0;
+  } else if (L.type == L_AREA) {
+    area = PI * pow(L.radius, 2.0);
+    flux /= 2.0;
+  } else if (L.type == L_RECT) {
+    area = length(cross(L.a1 * L.len1, L.a2 * L.len2));
+    flux /= 2.0;
+  } else if (L.type == L_SPOT) {
+    double s = L.dropoff;
+    flux = (2.0 * PI) / (s + 1.0) * (1.0 - pow(cos(L.cutoff), s + 1.0));
+  }
+  return (L.color.r + L.color.g + L.color.b) * area * flux;
+}
+
+// trace photons [e0, e0+n) of one light in parallel, concatenated in emission order
+static void emit_range(const Ctx &c, const Light &L, bool caustic, int64_t e0, int64_t n,
+                       std::vector<Photon> &map) {
+  int T = std::max(1, c.P.threads);
+  std::vector<std::vector<Photon>> part(T);
+  auto work = [&](int tid) {
+    int64_t lo = n * tid / T, hi = n * (tid + 1) / T;
+    for (int64_t j = lo; j < hi; j++) {
+      Rng rng(c.P.seed, caustic ? KIND_PHOTON_CAUSTIC : KIND_PHOTON_GLOBAL, (uint64_t)(e0 + j), 0);
+      emit_one(c, L, caustic, rng, part[tid]);
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; t++) th.emplace_back(work, t);
+  work(0);
+  for (auto &t : th) t.join();
+  for (auto &p : part) map.insert(map.end(), p.begin(), p.end());
+}
+
+// Threadable_PhotonTracer adaptive rounds (photonmap.cpp:145-257) for one map, one emitter
+static int64_t trace_map(const Ctx &c, bool caustic, int64_t goal_count,
+                         const std::vector<double> &powers, double total_power,
+                         std::vector<Photon> &map) {
+  int64_t stored = 0, emitted = 0;
+  double rate = caustic ? (double)c.P.max_photon_depth : 4.0;
+  double slowdown = 1.0;
+  int attempts = 10;
+  while (stored < goal_count && attempts > 0) {
+    int emit_goal = (int)((double)(int)(goal_count - stored) / rate / slowdown + 1);
+    int64_t assigned = 0;
+    for (int i = 0; i < c.nlights; i++) {
+      int num = (int)ceil(emit_goal * (powers[i] / total_power));
+      const Light &L = c.scene.lights[i];
+      if (L.active && num) emit_range(c, L, caustic, emitted + assigned, num, map);
+      assigned += num;
+    }
+    emitted += assigned;
+    stored = (int64_t)map.size();
+    if (stored > 0 && emitted > 0) {
+      rate = (double)stored / emitted;
+      double frac = caustic ? (double)stored / goal_count : (double)stored / emitted;
+      slowdown = (frac < 0.75) ? 2.0 : 1.0;
+    } else {
+      rate /= 2.0;
+      attempts--;
+    }
+  }
+  return emitted;
+}
+
+// MapPhotons, photonmap.cpp:260-436
+static void map_photons(Ctx &c, gi_photon_stats *st) {
+  auto t0 = std::chrono::steady_clock::now();
+  c.gmap = KdTree();
+  c.cmap = KdTree();
+  if (c.nlights <= 0) return;
+  std::vector<double> powers(c.nlights, 0.0);
+  double total = 0;
+  for (int i = 0; i < c.nlights; i++) {
+    if (!c.scene.lights[i].active) continue;
+    powers[i] = light_power(c, c.scene.lights[i]);
+    total += powers[i];
+  }
+  if (total <= 0) return;
+  gi_params &P = c.P;
+  if (P.indirect_illum || P.direct_photon_illum)
+    c.g_emitted = trace_map(c, false, P.global_photon_count, powers, total, c.gmap.ph);
+  if (P.caustic_illum)
+    c.c_emitted = trace_map(c, true, P.caustic_photon_count, powers, total, c.cmap.ph);
+  auto t1 = std::chrono::steady_clock::now();
+  // power rescale (Q9), photonmap.cpp:339-361
+  if ((P.indirect_illum || P.direct_photon_illum) && !c.gmap.ph.empty()) {
+    P.global_photon_count = (int)c.gmap.ph.size();
+    double pp = total / (double)c.g_emitted;
+    for (auto &ph : c.gmap.ph) {
+      Rgb col = rgbe_to_rgb(ph.rgbe);
+      col *= pp;
+      rgb_to_rgbe(col, ph.rgbe);
+    }
+  } else if ((P.indirect_illum || P.direct_photon_illum) && c.gmap.ph.empty()) {
+    P.indirect_illum = 0;
+    P.direct_photon_illum = 0;
+  }
+  if (P.caustic_illum && !c.cmap.ph.empty()) {
+    P.caustic_photon_count = (int)c.cmap.ph.size();
+    double pp = total / (double)c.c_emitted;
+    for (auto &ph : c.cmap.ph) {
+      Rgb col = rgbe_to_rgb(ph.rgbe);
+      col *= pp;
+      rgb_to_rgbe(col, ph.rgbe);
+    }
+  } else if (P.caustic_illum && c.cmap.ph.empty()) {
+    P.caustic_illum = 0;
+  }
+  kd_build(c.gmap);
+  kd_build(c.cmap);
+  auto t2 = std::chrono::steady_clock::now();
+  // irradiance cache, photonmap.cpp:381-413
+  if (P.irradiance_cache && (P.indirect_illum || P.direct_photon_illum)) {
+    std::vector<Photon> cache = c.gmap.ph;
+    for (size_t i = 0; i < cache.size(); i++) {
+      Rgb irr = rgbe_to_rgb(cache[i].rgbe);
+      V3 q(cache[i].pos[0], cache[i].pos[1], cache[i].pos[2]);
+      estimate_irradiance(q, irr, c.gmap, P.global_estimate_size, P.global_estimate_dist);
+      rgb_to_rgbe(irr, cache[i].rgbe);
+    }
+    for (size_t i = 0; i < cache.size(); i++)
+      memcpy(c.gmap.ph[i].rgbe, cache[i].rgbe, 4);
+  }
+  auto t3 = std::chrono::steady_clock::now();
+  if (st) {
+    st->global_stored = (int64_t)c.gmap.ph.size();
+    st->caustic_stored = (int64_t)c.cmap.ph.size();
+    st->global_emitted = c.g_emitted;
+    st->caustic_emitted = c.c_emitted;
+    st->trace_s = std::chrono::duration<double>(t1 - t0).count();
+    st->kd_s = std::chrono::duration<double>(t2 - t1).count();
+    st->irradiance_s = std::chrono::duration<double>(t3 - t2).count();
+    st->total_s = std::chrono::duration<double>(t3 - t0).count();
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// RenderImage, render.cpp:48-259
+// ---------------------------------------------------------------------------------------
+struct Image {
+  int w = 0, h = 0;
+  std::vector<uint8_t> rgb;   // SetPixelRGB values, row y = image row y
+  std::vector<float> rgbf;    // box-filtered clamped colour
+};
+
+static void render_image(const Ctx &c, int aa, int width, int height, Image &img,
+                         Counters &total, double *render_s) {
+  auto t0 = std::chrono::steady_clock::now();
+  const gi_params &P = c.P;
+  int af = (int)pow(2.0, aa);
+  double axis_scale = 1.0 / af;
+  double box_weight = 1.0 / af / af;
+  int W = width * af, H = height * af;
+  std::vector<Rgb> buf((size_t)W * H);
+  const Camera &cam = c.scene.camera;
+  V3 far_org = cam.eye + cam.towards * P.focus_depth;
+  V3 far_right = cam.right * tan(cam.xfov) * P.focus_depth;
+  V3 far_up = cam.up * tan(cam.yfov) * P.focus_depth;
+  V3 u = normalize(cam.up) * P.aperture_radius;
+  V3 v = normalize(cam.right) * P.aperture_radius;
+  int xc = W / 2, yc = H / 2;
+  int T = std::max(1, P.threads);
+  std::vector<Counters> cnts(T);
+  auto work = [&](int id) {
+    Counters &cnt = cnts[id];
+    for (int i = 0; i < W; i++) {
+      if (i % T != id) continue;  // column interleave, render.cpp:90
+      for (int j = 0; j < H; j++) {
+        Rgb acc;
+        double dx = (double)(2 * (i - xc)) / (double)W;
+        double dy = (double)(2 * (j - yc)) / (double)H;
+        V3 far_point = far_org + (far_right * dx) + (far_up * dy);
+        for (int k = 0; k < P.dof_test; k++) {
+          uint64_t psample = ((uint64_t)j * W + i) * (uint64_t)P.dof_test + k;
+          Rng rng(P.seed, KIND_PRIMARY, psample, 0);
+          V3 org = cam.eye;
+          if (P.depth_of_field) {
+            double r1, r2;
+            do {
+              r1 = (rng.next() * 2.0) - 1.0;
+              r2 = (rng.next() * 2.0) - 1.0;
+            } while (r1 * r1 + r2 * r2 > 1.0);
+            org = cam.eye + r1 * u + r2 * v;
+          }
+          V3 dir = normalize(far_point - org);
+          Hit h;
+          if (intersect(c, org, dir, h)) {
+            Rgb color;
+            ray_trace(c, h, cam.eye, color, rng, psample, cnt);
+            acc += color;
+            cnt.ray++;
+          } else {
+            acc += c.scene.background;
+          }
+        }
+        buf[(size_t)j * W + i] = acc / (double)P.dof_test;
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; t++) th.emplace_back(work, t);
+  work(0);
+  for (auto &t : th) t.join();
+  for (auto &cc : cnts) total.add(cc);
+  // downsample, render.cpp:205-221
+  std::vector<Rgb> down((size_t)width * height);
+  for (int j = 0; j < H; j++)
+    for (int i = 0; i < W; i++) {
+      int uu = (int)(i * axis_scale), vv = (int)(j * axis_scale);
+      Rgb col = buf[(size_t)j * W + i];
+      clamp_color(col);
+      down[(size_t)vv * width + uu] += col;
+    }
+  img.w = width;
+  img.h = height;
+  img.rgb.resize((size_t)width * height * 3);
+  img.rgbf.resize((size_t)width * height * 3);
+  for (int j = 0; j < height; j++)
+    for (int i = 0; i < width; i++) {
+      Rgb col = box_weight * down[(size_t)j * width + i];
+      size_t o = ((size_t)j * width + i) * 3;
+      for (int ch = 0; ch < 3; ch++) {
+        img.rgb[o + ch] = (uint8_t)(255 * col[ch]);  // R2Image::SetPixelRGB, R2Image.cpp:205-208
+        img.rgbf[o + ch] = (float)col[ch];
+      }
+    }
+  if (render_s)
+    *render_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// ---------------------------------------------------------------------------------------
+// ParseArgs, io_utils.cpp:16-212 (+ extension: -seed S)
+// ---------------------------------------------------------------------------------------
+static void params_default(gi_params &P) {
+  memset(&P, 0, sizeof P);
+  P.verbose = 0; P.threads = 1; P.fresnel = 1; P.ir_air = 1.0;
+  P.ambient = 1; P.direct_illum = 1; P.transmissive_illum = 1; P.specular_illum = 1;
+  P.indirect_illum = 1; P.caustic_illum = 1;
+  P.direct_photon_illum = 0; P.fast_global = 0; P.irradiance_cache = 0;
+  P.shadows = 1; P.soft_shadows = 1; P.light_test = 128; P.shadow_test = 128;
+  P.monte_carlo = 1; P.max_monte_depth = 128; P.prob_absorb = 0.005; P.recursive_shadows = 1;
+  P.distrib_transmissive = 1; P.transmissive_test = 128; P.distrib_specular = 1;
+  P.specular_test = 128;
+  P.depth_of_field = 0; P.dof_test = 1; P.focus_depth = 100.0; P.aperture_radius = 0.025;
+  P.global_photon_count = 2176; P.caustic_photon_count = 10000000; P.max_photon_depth = 128;
+  P.indirect_test = 256; P.global_estimate_size = 50; P.global_estimate_dist = 2.5;
+  P.global_filter = GI_FILTER_DISK; P.caustic_estimate_size = 225;
+  P.caustic_estimate_dist = 0.225; P.caustic_filter = GI_FILTER_DISK;
+  P.filter_const_a = 0.918; P.filter_const_b = 1.953; P.filter_const_k = 1.0;
+  P.seed = 1;
+}
+
+static int parse_args(int argc, char **argv, gi_params &P, std::string &scene, std::string &out,
+                      int &w, int &h, int &aa, int &real, std::string &err) {
+  argc--; argv++;
+  const char *sc = nullptr, *op = nullptr;
+  auto need = [&](int n) { return argc > n; };
+  while (argc > 0) {
+    const char *a = *argv;
+    if (a[0] == '-') {
+      if (!strcmp(a, "-v")) P.verbose = 1;
+      else if (!strcmp(a, "-threads") && need(1)) { argc--; argv++; P.threads = (int)atof(*argv); if (P.threads <= 0) P.threads = 1; }
+      else if (!strcmp(a, "-aa") && need(1)) { argc--; argv++; aa = atoi(*argv); if (aa < 0) aa *= -1; }
+      else if (!strcmp(a, "-real")) real = 1;
+      else if (!strcmp(a, "-no_fresnel")) P.fresnel = 0;
+      else if (!strcmp(a, "-ir") && need(1)) { argc--; argv++; P.ir_air = atof(*argv); if (P.ir_air <= 0) P.ir_air = EPS; }
+      else if (!strcmp(a, "-no_ambient")) P.ambient = 0;
+      else if (!strcmp(a, "-no_direct")) P.direct_illum = 0;
+      else if (!strcmp(a, "-no_transmissive")) P.transmissive_illum = 0;
+      else if (!strcmp(a, "-no_specular")) P.specular_illum = 0;
+      else if (!strcmp(a, "-no_indirect")) P.indirect_illum = 0;
+      else if (!strcmp(a, "-no_caustic")) P.caustic_illum = 0;
+      else if (!strcmp(a, "-photon_viz")) P.direct_photon_illum = 1;
+      else if (!strcmp(a, "-fast_global")) { P.fast_global = 1; P.direct_photon_illum = 1; P.indirect_illum = 0; }
+      else if (!strcmp(a, "-cache")) P.irradiance_cache = 1;
+      else if (!strcmp(a, "-no_monte")) P.monte_carlo = 0;
+      else if (!strcmp(a, "-md") && need(1)) { argc--; argv++; P.max_monte_depth = atoi(*argv); if (P.max_monte_depth < 1) P.max_monte_depth = 1; }
+      else if (!strcmp(a, "-absorb") && need(1)) { argc--; argv++; P.prob_absorb = atof(*argv); if (P.prob_absorb < 0) P.prob_absorb = 0; }
+      else if (!strcmp(a, "-no_rs")) P.recursive_shadows = 0;
+      else if (!strcmp(a, "-no_dt")) P.distrib_transmissive = 0;
+      else if (!strcmp(a, "-tt") && need(1)) { argc--; argv++; P.transmissive_test = atoi(*argv); if (P.transmissive_test < 1) P.transmissive_test = 1; }
+      else if (!strcmp(a, "-no_ds")) P.distrib_specular = 0;
+      else if (!strcmp(a, "-st") && need(1)) { argc--; argv++; P.specular_test = atoi(*argv); if (P.specular_test < 1) P.specular_test = 1; }
+      else if (!strcmp(a, "-global") && need(1)) { argc--; argv++; P.global_photon_count = atoi(*argv); if (P.global_photon_count < 1) P.global_photon_count = 1; }
+      else if (!strcmp(a, "-caustic") && need(1)) { argc--; argv++; P.caustic_photon_count = atoi(*argv); if (P.caustic_photon_count < 1) P.caustic_photon_count = 1; }
+      else if (!strcmp(a, "-pd") && need(1)) { argc--; argv++; P.max_photon_depth = atoi(*argv); if (P.max_photon_depth < 1) P.max_photon_depth = 1; }
+      else if (!strcmp(a, "-it") && need(1)) { argc--; argv++; P.indirect_test = atoi(*argv); if (P.indirect_test < 1) P.indirect_test = 1; }
+      else if (!strcmp(a, "-gs") && need(1)) { argc--; argv++; P.global_estimate_size = atoi(*argv); if (P.global_estimate_size < 1) P.global_estimate_size = 1; }
+      else if (!strcmp(a, "-gd") && need(1)) { argc--; argv++; P.global_estimate_dist = atof(*argv); if (P.global_estimate_dist < 0.0) P.global_estimate_dist = EPS; }
+      else if (!strcmp(a, "-gf") && need(1)) {
+        argc--; argv++;
+        if (!strcmp(*argv, "cone") && need(1)) { P.global_filter = GI_FILTER_CONE; argc--; argv++; P.filter_const_k = atof(*argv); if (P.filter_const_k < 1) P.filter_const_k = 1; }
+        else if (!strcmp(*argv, "gauss")) P.global_filter = GI_FILTER_GAUSS;
+      }
+      else if (!strcmp(a, "-cs") && need(1)) { argc--; argv++; P.caustic_estimate_size = atoi(*argv); if (P.caustic_estimate_size < 1) P.caustic_estimate_size = 1; }
+      else if (!strcmp(a, "-cd") && need(1)) { argc--; argv++; P.caustic_estimate_dist = atof(*argv); if (P.caustic_estimate_dist < 0.0) P.caustic_estimate_dist = EPS; }
+      else if (!strcmp(a, "-cf") && need(1)) {
+        argc--; argv++;
+        if (!strcmp(*argv, "cone") && need(1)) { P.caustic_filter = GI_FILTER_CONE; argc--; argv++; P.filter_const_k = atof(*argv); if (P.filter_const_k < 1) P.filter_const_k = 1; }
+        else if (!strcmp(*argv, "gauss")) P.caustic_filter = GI_FILTER_GAUSS;
+      }
+      else if (!strcmp(a, "-no_shadow")) P.shadows = 0;
+      else if (!strcmp(a, "-no_ss")) P.soft_shadows = 0;
+      else if (!strcmp(a, "-lt") && need(1)) { argc--; argv++; P.light_test = atoi(*argv); if (P.light_test < 1) P.light_test = 1; }
+      else if (!strcmp(a, "-ss") && need(1)) { argc--; argv++; P.shadow_test = atoi(*argv); if (P.shadow_test < 0) P.shadow_test = 0; }
+      else if (!strcmp(a, "-dof") && need(3)) {
+        P.depth_of_field = 1;
+        argc--; argv++; P.dof_test = atoi(*argv);
+        argc--; argv++; P.focus_depth = atof(*argv);
+        argc--; argv++; P.aperture_radius = atof(*argv);
+        if (P.dof_test < 1) P.dof_test = 1;
+        if (P.focus_depth < EPS) P.focus_depth = EPS;
+        if (P.aperture_radius <= 0) P.aperture_radius = EPS;
+      }
+      else if (!strcmp(a, "-resolution") && need(2)) {
+        argc--; argv++; w = atoi(*argv);
+        argc--; argv++; h = atoi(*argv);
+        if (w < 0) w *= -1;
+        if (h < 0) h *= -1;
+      }
+      else if (!strcmp(a, "-seed") && need(1)) { argc--; argv++; P.seed = strtoull(*argv, nullptr, 10); }
+      else { err = std::string("Invalid program argument: ") + a; return 1; }
+      argv++; argc--;
+    } else {
+      if (!sc) sc = a;
+      else if (!op) op = a;
+      else { err = std::string("Invalid program argument: ") + a; return 1; }
+      argv++; argc--;
+    }
+  }
+  if (!sc || !op) { err = "Usage: photonmap inputscenefile outputimagefile [-FLAGS]"; return 2; }
+  scene = sc;
+  out = op;
+  return 0;
+}
+
+// minimal PNG writer (zlib), bottom-up rows like R2Image::WritePNG (R2Image.cpp:1430)
+static bool write_png(const std::string &path, const Image &img) {
+  FILE *fp = fopen(path.c_str(), "wb");
+  if (!fp) return false;
+  auto be32 = [](uint8_t *p, uint32_t v) { p[0] = v >> 24; p[1] = v >> 16; p[2] = v >> 8; p[3] = v; };
+  auto chunk = [&](const char *type, const std::vector<uint8_t> &data) {
+    uint8_t hdr[8];
+    be32(hdr, (uint32_t)data.size());
+    memcpy(hdr + 4, type, 4);
+    fwrite(hdr, 1, 8, fp);
+    if (!data.empty()) fwrite(data.data(), 1, data.size(), fp);
+    uLong crc = crc32(0, (const Bytef *)type, 4);
+    if (!data.empty()) crc = crc32(crc, data.data(), (uInt)data.size());
+    uint8_t cb[4];
+    be32(cb, (uint32_t)crc);
+    fwrite(cb, 1, 4, fp);
+  };
+  const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+  fwrite(sig, 1, 8, fp);
+  std::vector<uint8_t> ihdr(13, 0);
+  be32(&ihdr[0], img.w);
+  be32(&ihdr[4], img.h);
+  ihdr[8] = 8; ihdr[9] = 2;
+  chunk("IHDR", ihdr);
+  std::vector<uint8_t> raw;
+  for (int r = 0; r < img.h; r++) {
+    raw.push_back(0);
+    const uint8_t *row = &img.rgb[(size_t)(img.h - 1 - r) * img.w * 3];
+    raw.insert(raw.end(), row, row + (size_t)img.w * 3);
+  }
+  uLongf zl = compressBound(raw.size());
+  std::vector<uint8_t> z(zl);
+  compress2(z.data(), &zl, raw.data(), raw.size(), 6);
+  z.resize(zl);
+  chunk("IDAT", z);
+  chunk("IEND", {});
+  fclose(fp);
+  return true;
+}
+
+static bool setup(Ctx &c, int argc, char **argv, std::string &out, int &w, int &h, int &aa,
+                  std::string &err) {
+  params_default(c.P);
+  std::string scene;
+  int real = 0;
+  w = 1024; h = 1024; aa = 2;
+  int rc = parse_args(argc, argv, c.P, scene, out, w, h, aa, real, err);
+  if (rc) return false;
+  if (!read_scene(scene, real != 0, c.scene, err)) return false;
+  c.scene_radius = c.scene.radius;
+  c.scene_ambient = c.scene.ambient;
+  c.nlights = (int)c.scene.lights.size();
+  build_lut(c.lut);
+  return true;
+}
+
+}  // namespace oracle
+
+// =======================================================================================
+// C API for tests / bench (ctypes). All functions are checker-side only.
+// =======================================================================================
+using namespace oracle;
+
+extern "C" {
+
+// Full pipeline like photonmap main (photonmap.cpp:442-499) without writing the file unless
+// write != 0. rgb (w*h*3, row y = image row y) and stats[16] are optional outputs:
+// stats = {trace_s, kd_s, render_s, global_stored, caustic_stored, screen, shadow, monte,
+//          trans, spec, indirect, caustic, knn, knn_photons, w, h}
+int oracle_run(int argc, char **argv, uint8_t *rgb, int64_t cap, double *stats, int write) {
+  Ctx *c = new Ctx();
+  std::string out, err;
+  int w, h, aa;
+  if (!setup(*c, argc, argv, out, w, h, aa, err)) {
+    fprintf(stderr, "%s\n", err.c_str());
+    delete c;
+    return 1;
+  }
+  gi_photon_stats pst{};
+  if (c->P.indirect_illum || c->P.caustic_illum || c->P.direct_photon_illum) map_photons(*c, &pst);
+  Image img;
+  Counters cnt;
+  double rs = 0;
+  render_image(*c, aa, w, h, img, cnt, &rs);
+  if (rgb) {
+    if ((int64_t)img.rgb.size() > cap) { delete c; return 2; }
+    memcpy(rgb, img.rgb.data(), img.rgb.size());
+  }
+  if (stats) {
+    double s[16] = {pst.trace_s, pst.kd_s, rs, (double)pst.global_stored, (double)pst.caustic_stored,
+                    (double)cnt.ray, (double)cnt.shadow, (double)cnt.monte, (double)cnt.trans,
+                    (double)cnt.spec, (double)cnt.indirect, (double)cnt.caustic, (double)cnt.knn,
+                    (double)cnt.knn_photons, (double)w, (double)h};
+    memcpy(stats, s, sizeof s);
+  }
+  if (write && !write_png(out, img)) { delete c; return 3; }
+  delete c;
+  return 0;
+}
+
+// Photon maps only (MapPhotons), storage (emission) order, after power rescale.
+int oracle_map_photons(int argc, char **argv, gi_photon *gout, int64_t gcap, int64_t *gn,
+                       gi_photon *cout, int64_t ccap, int64_t *cn, int64_t *emitted2) {
+  Ctx c;
+  std::string out, err;
+  int w, h, aa;
+  if (!setup(c, argc, argv, out, w, h, aa, err)) { fprintf(stderr, "%s\n", err.c_str()); return 1; }
+  gi_photon_stats pst{};
+  map_photons(c, &pst);
+  *gn = (int64_t)c.gmap.ph.size();
+  *cn = (int64_t)c.cmap.ph.size();
+  if (emitted2) { emitted2[0] = c.g_emitted; emitted2[1] = c.c_emitted; }
+  if (*gn > gcap || *cn > ccap) return 2;
+  if (*gn) memcpy(gout, c.gmap.ph.data(), *gn * sizeof(gi_photon));
+  if (*cn) memcpy(cout, c.cmap.ph.data(), *cn * sizeof(gi_photon));
+  return 0;
+}
+
+// EstimateRadiance over an explicit photon map (kd built here).
+int oracle_estimate_radiance(const gi_photon *photons, int64_t n, const gi_radiance_query *q,
+                             int64_t nq, double filter_k, double *rgb_out, int32_t *nfound,
+                             float *maxd2) {
+  Ctx c;
+  params_default(c.P);
+  c.P.filter_const_k = filter_k;
+  build_lut(c.lut);
+  c.gmap.ph.assign((const Photon *)photons, (const Photon *)photons + n);
+  kd_build(c.gmap);
+  for (int64_t i = 0; i < nq; i++) {
+    const gi_radiance_query &Q = q[i];
+    Brdf b;
+    b.kd = Rgb(Q.kd[0], Q.kd[1], Q.kd[2]);
+    b.ks = Rgb(Q.ks[0], Q.ks[1], Q.ks[2]);
+    b.n = Q.shininess;
+    Rgb col;
+    int nf = 0;
+    float md = 0;
+    estimate_radiance(c, V3(Q.point[0], Q.point[1], Q.point[2]),
+                      V3(Q.normal[0], Q.normal[1], Q.normal[2]), col, b,
+                      V3(Q.exact_bounce[0], Q.exact_bounce[1], Q.exact_bounce[2]), Q.cos_theta,
+                      c.gmap, Q.k, Q.max_dist, Q.filter, nullptr, &nf, &md);
+    rgb_out[3 * i] = col.r; rgb_out[3 * i + 1] = col.g; rgb_out[3 * i + 2] = col.b;
+    if (nfound) nfound[i] = nf;
+    if (maxd2) maxd2[i] = md;
+  }
+  return 0;
+}
+
+// k nearest (FindClosestQuick), results sorted by (d2, index) for comparison
+int oracle_knn(const gi_photon *photons, int64_t n, const double *pts, int64_t nq, int k,
+               double max_dist, int32_t *idx_out, float *d2_out, int32_t *nfound) {
+  KdTree t;
+  t.ph.assign((const Photon *)photons, (const Photon *)photons + n);
+  kd_build(t);
+  std::vector<Near> res;
+  for (int64_t i = 0; i < nq; i++) {
+    kd_find_quick(t, V3(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]), max_dist, k, res);
+    std::sort(res.begin(), res.end(), [](const Near &a, const Near &b) {
+      return a.d2 < b.d2 || (a.d2 == b.d2 && a.i < b.i);
+    });
+    nfound[i] = (int32_t)res.size();
+    for (int j = 0; j < k; j++) {
+      idx_out[i * k + j] = j < (int)res.size() ? res[j].i : -1;
+      d2_out[i * k + j] = j < (int)res.size() ? res[j].d2 : -1.0f;
+    }
+  }
+  return 0;
+}
+
+// R3Scene::Intersects for a batch of rays
+int oracle_intersect(const char *scene_path, int64_t n, const double *org, const double *dir,
+                     int32_t *hit, double *t, double *point, double *normal, int32_t *material) {
+  Scene s;
+  std::string err;
+  if (!read_scene(scene_path, false, s, err)) { fprintf(stderr, "%s\n", err.c_str()); return 1; }
+  for (int64_t i = 0; i < n; i++) {
+    Hit h;
+    bool ok = scene_intersect(s, V3(org[3 * i], org[3 * i + 1], org[3 * i + 2]),
+                              V3(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]), h);
+    hit[i] = ok;
+    t[i] = ok ? h.t : 0;
+    for (int j = 0; j < 3; j++) {
+      point[3 * i + j] = ok ? h.point[j] : 0;
+      normal[3 * i + j] = ok ? h.normal[j] : 0;
+    }
+    material[i] = ok ? h.material : -2;
+  }
+  return 0;
+}
+
+// RGBE codec + direction LUT known-answer helpers
+void oracle_rgbe_encode(const double *rgb, uint8_t *out) { rgb_to_rgbe(Rgb(rgb[0], rgb[1], rgb[2]), out); }
+void oracle_rgbe_decode(const uint8_t *in, double *rgb) {
+  Rgb c = rgbe_to_rgb(in);
+  rgb[0] = c.r; rgb[1] = c.g; rgb[2] = c.b;
+}
+void oracle_direction_lut(double *out) {
+  std::vector<double> l;
+  build_lut(l);
+  memcpy(out, l.data(), l.size() * sizeof(double));
+}
+
+int oracle_main(int argc, char **argv) { return oracle_run(argc, argv, nullptr, 0, nullptr, 1); }
+
+// ParseArgs restatement (returns 0 ok, 1 bad flag, 2 usage) for flag-parity tests
+int oracle_parse_args(int argc, char **argv, gi_params *P, int *w, int *h, int *aa, int *real) {
+  params_default(*P);
+  std::string scene, out, err;
+  *w = 1024; *h = 1024; *aa = 2; *real = 0;
+  return parse_args(argc, argv, *P, scene, out, *w, *h, *aa, *real, err);
+}
+
+}  // extern "C"

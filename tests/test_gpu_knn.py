@@ -1,0 +1,62 @@
+"""k-NN search and EstimateRadiance on the device vs the oracle restatement
+(R3Kdtree::FindClosestQuick R3Kdtree.cpp:688-848; EstimateRadiance photon_utils.cpp:72-162).
+
+Tolerances: the photon metric is fp32 and identical on both sides, so the k-NN *sets* and
+their squared distances must match exactly (ties at the k-th distance may resolve to different
+photons; the sorted d2 lists must still be equal). Radiance sums are fp64 accumulated in a
+different order: relative tolerance 1e-10."""
+import numpy as np
+import pytest
+
+import oracle_lib
+import synth
+from gi_amd import CAUSTIC, GLOBAL, DISK, CONE, GAUSS
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n,k,r", [(20000, 50, 2.5), (50000, 225, 0.225), (3000, 50, 0.05),
+                                   (1, 50, 2.5), (100, 1, 0.3)])
+def test_knn_sets_match_oracle(renderer, n, k, r):
+    ph = synth.photon_map(n, seed=n)
+    q = synth.queries(512, seed=k)["point"]
+    renderer.set_photon_map(GLOBAL, ph)
+    gi, gd, gn = renderer.FindClosestQuick(GLOBAL, q, k, r)
+    oi, od, on = oracle_lib.knn(ph, q, k, r)
+    np.testing.assert_array_equal(gn, on)
+    for i in range(len(q)):
+        m = gn[i]
+        np.testing.assert_array_equal(np.sort(gd[i, :m]), od[i, :m])
+        order = np.lexsort((gi[i, :m], gd[i, :m]))
+        got = gi[i, :m][order]
+        d_sorted = gd[i, :m][order]
+        # identical sets except possibly photons tied at the k-th distance
+        mism = got != oi[i, :m]
+        assert np.all(d_sorted[mism] == od[i, m - 1]), (i, got[mism], oi[i, :m][mism])
+
+
+def test_knn_empty_map(renderer):
+    renderer.set_photon_map(CAUSTIC, synth.photon_map(0))
+    q = synth.queries(64)["point"]
+    _, _, n = renderer.FindClosestQuick(CAUSTIC, q, 10, 1.0)
+    assert np.all(n == 0)
+
+
+@pytest.mark.parametrize("filt,k,r,spec", [(DISK, 50, 2.5, False), (DISK, 225, 0.225, True),
+                                           (CONE, 50, 0.3, False), (GAUSS, 64, 0.3, True),
+                                           (DISK, 10, 0.02, True)])
+def test_estimate_radiance_matches_oracle(renderer, filt, k, r, spec):
+    ph = synth.photon_map(30000, seed=7)
+    q = synth.queries(1000, seed=3, k=k, r=r, filt=filt, spec=spec)
+    fk = 1.25 if filt == CONE else 1.0
+    p = renderer.params
+    p.filter_const_k = fk
+    renderer.set_params(p)
+    renderer.set_photon_map(GLOBAL, ph)
+    g, gn, gm = renderer.EstimateRadiance(GLOBAL, q)
+    o, on, om = oracle_lib.estimate_radiance(ph, q, filter_k=fk)
+    np.testing.assert_array_equal(gn, on)
+    np.testing.assert_allclose(gm, om, rtol=0, atol=0)
+    np.testing.assert_allclose(g, o, rtol=1e-10, atol=1e-300)
+    p.filter_const_k = 1.0
+    renderer.set_params(p)

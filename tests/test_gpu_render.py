@@ -1,0 +1,109 @@
+"""Device render / photon tracing / ray casting vs the oracle restatement on the same inputs
+and RNG streams. Images are compared on the 8-bit output (R2Image::SetPixelRGB truncation):
+direct-only renders must match exactly except for rare 1-LSB truncation flips (fp64
+reassociation), full-GI renders must agree per pixel within 1 LSB on >= 99% of pixels and in
+mean within 0.5 LSB (path divergence from last-ulp transcendental differences is allowed)."""
+import os
+
+import numpy as np
+import pytest
+
+import gi_amd
+import oracle_lib
+
+pytestmark = pytest.mark.gpu
+INP = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "scenes")
+
+
+def scene(name):
+    return os.path.join(INP, name)
+
+
+def run_gpu(renderer, args):
+    p, sc, _out, w, h, aa, real = gi_amd.ParseArgs(args)
+    renderer.set_params(p)
+    renderer.ReadScene(sc, real)
+    pst = None
+    if p.indirect_illum or p.caustic_illum or p.direct_photon_illum:
+        pst = renderer.MapPhotons()
+    rgb, st = renderer.RenderImage(aa, w, h)
+    return rgb, st, pst
+
+
+def compare(a, b, exact_frac, le1_frac, mean_tol):
+    d = np.abs(a.astype(int) - b.astype(int))
+    assert (d.max(-1) == 0).mean() >= exact_frac, (d.max(-1) == 0).mean()
+    assert (d.max(-1) <= 1).mean() >= le1_frac, (d.max(-1) <= 1).mean()
+    assert abs(a.astype(float).mean() - b.astype(float).mean()) <= mean_tol
+
+
+@pytest.mark.parametrize("name,extra", [
+    ("cornell.scn", []), ("jensen.scn", ["-lt", "8", "-ss", "8"]), ("stilllife.scn", []),
+    ("pointlight1.scn", []), ("spotlight1.scn", []), ("dirlight1.scn", [])])
+def test_direct_only_matches_oracle(renderer, name, extra):
+    args = [scene(name), "/tmp/x.png", "-resolution", "48", "48", "-aa", "0", "-no_indirect",
+            "-no_caustic", "-tt", "8", "-st", "8", "-seed", "3"] + extra
+    g, gst, _ = run_gpu(renderer, args)
+    o, ost = oracle_lib.render(args, 48, 48)
+    compare(g, o, 0.995, 0.999, 0.05)
+    assert gst["screen_rays"] == ost["screen_rays"]
+
+
+def test_full_gi_cornell_matches_oracle(renderer):
+    args = [scene("cornell.scn"), "/tmp/x.png", "-resolution", "24", "24", "-aa", "1",
+            "-global", "20000", "-caustic", "20000", "-it", "16", "-tt", "8", "-st", "8",
+            "-seed", "5"]
+    g, gst, gp = run_gpu(renderer, args)
+    o, ost = oracle_lib.render(args, 24, 24)
+    assert gp["global_stored"] == ost["global_stored"]
+    assert gp["caustic_stored"] == ost["caustic_stored"]
+    compare(g, o, 0.97, 0.99, 0.5)
+    assert abs(gst["knn_queries"] - ost["knn_queries"]) <= 0.01 * ost["knn_queries"]
+
+
+def test_photon_maps_match_oracle(renderer):
+    args = [scene("cornell.scn"), "/tmp/x.png", "-global", "30000", "-caustic", "30000",
+            "-seed", "11"]
+    p, sc, *_ = gi_amd.ParseArgs(args)
+    renderer.set_params(p)
+    renderer.ReadScene(sc)
+    renderer.MapPhotons()
+    gg = renderer.photon_map(gi_amd.GLOBAL)
+    gc = renderer.photon_map(gi_amd.CAUSTIC)
+    og, oc, em = oracle_lib.map_photons(args)
+    for a, b in ((gg, og), (gc, oc)):
+        assert len(a) == len(b)
+        np.testing.assert_allclose(a["pos"], b["pos"], atol=1e-5)
+        assert (a["rgbe"] == b["rgbe"]).all(axis=1).mean() > 0.999
+        assert (a["dir"] == b["dir"]).mean() > 0.999
+
+
+@pytest.mark.parametrize("name", ["cornell.scn", "stilllife.scn", "teapot.scn", "jensen.scn"])
+def test_intersections_match_oracle(renderer, name):
+    rng = np.random.default_rng(0)
+    info = renderer.ReadScene(scene(name))
+    n = 4000
+    org = rng.normal(size=(n, 3)) * info["radius"] * 0.5
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    gh, gt, gp, gn, gm = renderer.Intersects(org, d)
+    oh, ot, op, on, om = oracle_lib.intersect(scene(name), org, d)
+    assert (gh == oh).mean() > 0.999
+    both = (gh == 1) & (oh == 1)
+    np.testing.assert_allclose(gt[both], ot[both], rtol=1e-9, atol=1e-12)
+    assert (gm[both] == om[both]).mean() > 0.999
+    np.testing.assert_allclose(gn[both], on[both], atol=1e-9)
+
+
+def test_tiles_compose_full_image(renderer):
+    args = [scene("cornell.scn"), "/tmp/x.png", "-resolution", "40", "24", "-aa", "1",
+            "-no_indirect", "-no_caustic", "-tt", "4", "-st", "4"]
+    p, sc, _o, w, h, aa, _r = gi_amd.ParseArgs(args)
+    renderer.set_params(p)
+    renderer.ReadScene(sc)
+    full, ff, _ = renderer.RenderImage(aa, w, h, want_float=True)
+    acc = np.zeros((h, w, 3), dtype=np.float32)
+    for s in range(3):
+        part, _ = renderer.render_tiles(aa, w, h, 16, s, 3)
+        acc += part
+    np.testing.assert_array_equal(acc, ff)

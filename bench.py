@@ -118,7 +118,8 @@ def main():
         step()
     barrier()
     t0 = time.perf_counter()
-    agg = {"knn_photons": 0, "knn_queries": 0, "knn_kernel_ms": 0.0, "knn_kernel_launches": 0.0}
+    agg = {"knn_photons": 0, "knn_queries": 0, "knn_visited": 0, "knn_kernel_ms": 0.0,
+           "knn_kernel_launches": 0.0}
     for _ in range(a.steps):
         st = step()
         for k in agg:
@@ -152,6 +153,7 @@ def main():
                     "bytes_per_unit": "16 B per photon returned",
                     "photons_per_frame": agg["knn_photons"] / a.steps,
                     "queries_per_frame": agg["knn_queries"] / a.steps,
+                    "visited_per_query": agg["knn_visited"] / max(1, agg["knn_queries"]),
                     "knn_ms_per_frame": agg["knn_kernel_ms"] / a.steps / max(1, world)}
         cpu = None
         if not a.no_cpu_baseline and world == 1:

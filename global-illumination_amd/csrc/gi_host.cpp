@@ -18,6 +18,7 @@
 #include "../../include/gi.h"
 #include "gi_kernels.h"
 #include "gi_scene.h"
+#include "gi_sort.h"
 
 using namespace gi;
 
@@ -184,12 +185,18 @@ struct gi_ctx {
   bool map_valid[2] = {false, false};
   int leaf_size = 16;
   // render scratch
-  DBuf spawn, npaths, path_off, cnt_g, cnt_c, goff, coff, base, gpos, cpos, gshade, cshade, gout,
-      cout, pixels, rgbf, rgb8, gheap_d2, gheap_idx, perm;
+  DBuf spawn, npaths, path_off, base, pixels, rgbf, rgb8, gheap_d2, gheap_idx, qcount, stats_bak;
+  DBuf qpos[2], qshade[2], qkey[2], qout[2];
+  size_t qcap_hint[2] = {0, 0};
+  KeySortScratch keysort[2];
+  int knn_kernel_kind = 2;  // 2 = packet (wave-shared traversal), 1 = query per wave, 0 = per-lane
   DBuf scan_lvl[8], scan_out[8];
   // photon tracing scratch
   DBuf pcounts, poffs, pbuf;
   int64_t prim_per_batch = 1 << 17;
+  SortScratch sorter;
+  bool sort_queries = true;
+  float sbmin[3] = {0, 0, 0}, sbmax[3] = {1, 1, 1};
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
@@ -444,19 +451,32 @@ KnnArgs knn_args(gi_ctx *c, int mi) {
 
 // run a k-NN launch over nq queries (chunked when the heap lives in global scratch)
 int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
+  // packet traversal while the per-lane heaps fit LDS at >= 2 waves/CU, else one query/wave
+  int kind = c->knn_kernel_kind;
+  if (kind == 2 && (int64_t)k.K * 64 * 8 > 80 * 1024) kind = 1;
+  if ((kind == 1 && k.K + 64 <= 1024) || kind == 2) {
+    k.nq = nq;
+    k.q0 = 0;
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    if (kind == 2) launch_knn_packet(k, c->stream);
+    else launch_knn_wave(k, c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    if (ms) {
+      HIPCHK(c, hipEventSynchronize(c->ev1));
+      float t = 0;
+      HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+      *ms += t;
+    }
+    return GI_OK;
+  }
   bool lds = k.K <= 64;
   const int64_t CH = lds ? nq : (int64_t)(1 << 20);
   for (int64_t s = 0; s < nq; s += CH) {
     int64_t m = std::min(CH, nq - s);
     KnnArgs a = k;
     a.nq = m;
-    a.qpos = k.qpos + s;
-    a.qshade = k.qshade ? k.qshade + s : nullptr;
-    a.out = k.out ? k.out + 3 * s : nullptr;
-    a.out_n = k.out_n ? k.out_n + s : nullptr;
-    a.out_maxd2 = k.out_maxd2 ? k.out_maxd2 + s : nullptr;
-    a.out_idx = k.out_idx ? k.out_idx + (size_t)s * k.K : nullptr;
-    a.out_d2 = k.out_d2 ? k.out_d2 + (size_t)s * k.K : nullptr;
+    a.q0 = s;
     if (!lds) {
       size_t slots = (size_t)((m + 63) / 64) * 64 * (size_t)k.K;
       HIPCHK(c, c->gheap_d2.ensure(slots * 4));
@@ -478,6 +498,27 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
   return GI_OK;
 }
 
+// run the k-NN estimate of one query list into out[slot] (Morton-ordered launch)
+int knn_list(gi_ctx *c, int mi, const float4 *qpos, const QShade *qshade, int64_t nq,
+             double *out, double *ms) {
+  KnnArgs k = knn_args(c, mi);
+  k.qpos = qpos;
+  k.qshade = qshade;
+  k.out = out;
+  k.nq = nq;
+  if (c->sort_queries) {
+    uint32_t *perm = nullptr;
+    HIPCHK(c, morton_order(qpos, nq, c->sbmin, c->sbmax, c->sorter, &perm, c->stream));
+    k.perm = perm;
+  }
+  if (c->P.irradiance_cache && mi == GI_MAP_GLOBAL) {
+    launch_cached(k, c->stream);
+    HIPCHK(c, hipGetLastError());
+    return GI_OK;
+  }
+  return run_knn(c, k, nq, ms);
+}
+
 // render the given output pixels into the device image buffers
 int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &pix_xy,
                   gi_render_stats *rs) {
@@ -489,6 +530,8 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
   int64_t pix_batch = std::max<int64_t>(1, c->prim_per_batch / per_pix);
   double knn_ms = 0, launches = 0;
   HIPCHK(c, upload(c->pixels, pix_xy.data(), pix_xy.size() * 4, c->stream));
+  HIPCHK(c, c->qcount.ensure(16));
+  HIPCHK(c, c->stats_bak.ensure(ST_COUNT * 8));
   for (int64_t p0 = 0; p0 < npix_total; p0 += pix_batch) {
     int64_t npix = std::min(pix_batch, npix_total - p0);
     int64_t nprim = npix * per_pix;
@@ -520,75 +563,59 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
                              hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     a.total_paths = total_paths;
-    HIPCHK(c, c->cnt_g.ensure((size_t)total_paths * 4));
-    HIPCHK(c, c->cnt_c.ensure((size_t)total_paths * 4));
-    HIPCHK(c, c->goff.ensure((size_t)(total_paths + 1) * 4));
-    HIPCHK(c, c->coff.ensure((size_t)(total_paths + 1) * 4));
     HIPCHK(c, c->base.ensure((size_t)total_paths * 24));
-    a.cnt_g = c->cnt_g.as<uint32_t>();
-    a.cnt_c = c->cnt_c.as<uint32_t>();
-    a.goff = c->goff.as<uint32_t>();
-    a.coff = c->coff.as<uint32_t>();
     a.base = c->base.as<double>();
-    launch_path(a, false, c->stream);
-    HIPCHK(c, hipGetLastError());
-    t = scan_temp(c, total_paths);
-    HIPCHK(c, launch_scan(a.cnt_g, c->goff.as<uint32_t>(), total_paths, t, c->stream));
-    HIPCHK(c, launch_scan(a.cnt_c, c->coff.as<uint32_t>(), total_paths, t, c->stream));
-    uint32_t ng = 0, nc = 0;
-    HIPCHK(c, hipMemcpyAsync(&ng, c->goff.as<uint32_t>() + total_paths, 4, hipMemcpyDeviceToHost,
-                             c->stream));
-    HIPCHK(c, hipMemcpyAsync(&nc, c->coff.as<uint32_t>() + total_paths, 4, hipMemcpyDeviceToHost,
-                             c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    HIPCHK(c, c->gpos.ensure((size_t)ng * 16));
-    HIPCHK(c, c->gshade.ensure((size_t)ng * sizeof(QShade)));
-    HIPCHK(c, c->gout.ensure((size_t)ng * 24));
-    HIPCHK(c, c->cpos.ensure((size_t)nc * 16));
-    HIPCHK(c, c->cshade.ensure((size_t)nc * sizeof(QShade)));
-    HIPCHK(c, c->cout.ensure((size_t)nc * 24));
-    a.gpos = c->gpos.as<float4>();
-    a.gshade = c->gshade.as<QShade>();
-    a.cpos = c->cpos.as<float4>();
-    a.cshade = c->cshade.as<QShade>();
-    launch_path(a, true, c->stream);
-    HIPCHK(c, hipGetLastError());
-    // photon-map estimates
-    if (ng) {
-      if (!c->map_valid[GI_MAP_GLOBAL]) {
-        HIPCHK(c, hipMemsetAsync(c->gout.p, 0, (size_t)ng * 24, c->stream));
-      } else {
-        KnnArgs k = knn_args(c, GI_MAP_GLOBAL);
-        k.qpos = a.gpos;
-        k.qshade = a.gshade;
-        k.out = c->gout.as<double>();
-        k.nq = ng;
-        if (P.irradiance_cache) {
-          launch_cached(k, c->stream);
-          HIPCHK(c, hipGetLastError());
-        } else {
-          int rc = run_knn(c, k, ng, rs ? &knn_ms : nullptr);
-          if (rc) return rc;
-          launches++;
-        }
+    // single Monte Carlo pass; grow the query lists and re-run on overflow
+    uint32_t nq[2] = {0, 0};
+    HIPCHK(c, hipMemcpyAsync(c->stats_bak.p, c->d_stats.p, ST_COUNT * 8,
+                             hipMemcpyDeviceToDevice, c->stream));
+    for (int attempt = 0; attempt < 3; attempt++) {
+      for (int l = 0; l < 2; l++) {
+        size_t cap = std::max<size_t>(c->qcap_hint[l], 1024);
+        HIPCHK(c, c->qpos[l].ensure(cap * 16));
+        HIPCHK(c, c->qshade[l].ensure(cap * sizeof(QShade)));
+        HIPCHK(c, c->qkey[l].ensure(cap * 8));
+        a.qpos[l] = c->qpos[l].as<float4>();
+        a.qshade[l] = c->qshade[l].as<QShade>();
+        a.qkey[l] = c->qkey[l].as<uint64_t>();
+        a.qcap[l] = (uint32_t)std::min<size_t>(cap, 0xFFFFFFF0u);
       }
+      a.qcount = c->qcount.as<uint32_t>();
+      HIPCHK(c, hipMemsetAsync(c->qcount.p, 0, 8, c->stream));
+      launch_path(a, c->stream);
+      HIPCHK(c, hipGetLastError());
+      HIPCHK(c, hipMemcpyAsync(nq, c->qcount.p, 8, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      bool ok = nq[0] <= a.qcap[0] && nq[1] <= a.qcap[1];
+      for (int l = 0; l < 2; l++)
+        c->qcap_hint[l] = std::max<size_t>(c->qcap_hint[l], (size_t)(nq[l] * 1.25) + 1024);
+      if (ok) break;
+      if (attempt == 2) return fail(c, GI_ERR_ALLOC, "query list overflow");
+      HIPCHK(c, hipMemcpyAsync(c->d_stats.p, c->stats_bak.p, ST_COUNT * 8,
+                               hipMemcpyDeviceToDevice, c->stream));
     }
-    if (nc) {
-      if (!c->map_valid[GI_MAP_CAUSTIC]) {
-        HIPCHK(c, hipMemsetAsync(c->cout.p, 0, (size_t)nc * 24, c->stream));
+    // photon-map estimates, then a deterministic (key) order of each list for the reduction
+    for (int l = 0; l < 2; l++) {
+      a.nq[l] = nq[l];
+      if (!nq[l]) continue;
+      HIPCHK(c, c->qout[l].ensure((size_t)nq[l] * 24));
+      if (!c->map_valid[l]) {
+        HIPCHK(c, hipMemsetAsync(c->qout[l].p, 0, (size_t)nq[l] * 24, c->stream));
       } else {
-        KnnArgs k = knn_args(c, GI_MAP_CAUSTIC);
-        k.qpos = a.cpos;
-        k.qshade = a.cshade;
-        k.out = c->cout.as<double>();
-        k.nq = nc;
-        int rc = run_knn(c, k, nc, rs ? &knn_ms : nullptr);
+        int rc = knn_list(c, l, a.qpos[l], a.qshade[l], nq[l], c->qout[l].as<double>(),
+                          rs ? &knn_ms : nullptr);
         if (rc) return rc;
         launches++;
       }
+      uint64_t *sk = nullptr;
+      uint32_t *ss = nullptr;
+      int bits = 20;
+      while (bits < 64 && ((uint64_t)total_paths >> (bits - 20)) != 0) bits++;
+      HIPCHK(c, key_order(a.qkey[l], nq[l], bits, c->keysort[l], &sk, &ss, c->stream));
+      a.skey[l] = sk;
+      a.sslot[l] = ss;
+      a.qout[l] = c->qout[l].as<double>();
     }
-    a.gout = c->gout.as<double>();
-    a.cout = c->cout.as<double>();
     a.rgbf = c->rgbf.as<float>();
     a.rgb8 = c->rgb8.as<uint8_t>();
     launch_reduce(a, c->stream);
@@ -636,6 +663,9 @@ int gi_create(gi_ctx **out, int dev) {
   hipStreamSynchronize(c->stream);
   if (const char *s = getenv("GI_PRIM_PER_BATCH")) c->prim_per_batch = std::max(1LL, atoll(s));
   if (const char *s = getenv("GI_LEAF_SIZE")) c->leaf_size = std::max(1, atoi(s));
+  if (const char *s = getenv("GI_SORT_QUERIES")) c->sort_queries = atoi(s) != 0;
+  if (const char *s = getenv("GI_KNN_KERNEL")) c->knn_kernel_kind = atoi(s);
+  if (c->knn_kernel_kind >= 1 && !getenv("GI_LEAF_SIZE")) c->leaf_size = 64;
   *out = c;
   return GI_OK;
 }
@@ -644,17 +674,21 @@ void gi_destroy(gi_ctx *c) {
   if (!c) return;
   hipSetDevice(c->device);
   DBuf *bufs[] = {&c->d_nodes, &c->d_elems, &c->d_shapes, &c->d_tris, &c->d_mats, &c->d_lights,
-                  &c->d_lut, &c->d_stats, &c->spawn, &c->npaths, &c->path_off, &c->cnt_g,
-                  &c->cnt_c, &c->goff, &c->coff, &c->base, &c->gpos, &c->cpos, &c->gshade,
-                  &c->cshade, &c->gout, &c->cout, &c->pixels, &c->rgbf, &c->rgb8, &c->gheap_d2,
-                  &c->gheap_idx, &c->perm, &c->pcounts, &c->poffs, &c->pbuf};
+                  &c->d_lut, &c->d_stats, &c->spawn, &c->npaths, &c->path_off, &c->base,
+                  &c->pixels, &c->rgbf, &c->rgb8, &c->gheap_d2, &c->gheap_idx, &c->qcount,
+                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf};
   for (DBuf *b : bufs) b->release();
+  for (int l = 0; l < 2; l++) {
+    c->qpos[l].release(); c->qshade[l].release(); c->qkey[l].release(); c->qout[l].release();
+    sort_scratch_release(c->keysort[l]);
+  }
   for (int l = 0; l < 8; l++) { c->scan_lvl[l].release(); c->scan_out[l].release(); }
   for (int m = 0; m < 2; m++) {
     c->dmap[m].pos4.release();
     c->dmap[m].rgbe.release();
     c->dmap[m].nodes.release();
   }
+  sort_scratch_release(c->sorter);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
   if (c->stream) hipStreamDestroy(c->stream);
@@ -686,6 +720,10 @@ int gi_read_scene(gi_ctx *c, const char *path, int real) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->have_scene = true;
   c->map_valid[0] = c->map_valid[1] = false;
+  for (int i = 0; i < 3; i++) {
+    c->sbmin[i] = (float)H.bmin[i];
+    c->sbmax[i] = (float)H.bmax[i];
+  }
   return GI_OK;
 }
 
@@ -857,6 +895,7 @@ static int render_common(gi_ctx *c, int aa, int w, int h, const std::vector<int3
     st->caustic_samples = s[ST_CAUSTIC];
     st->knn_queries = s[ST_KNN];
     st->knn_photons = s[ST_KNN_PHOTONS];
+    st->knn_visited = s[ST_KNN_VISITED];
     st->knn_kernel_ms = local.knn_kernel_ms;
     st->knn_kernel_launches = local.knn_kernel_launches;
     st->render_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -995,6 +1034,70 @@ int gi_knn_batch(gi_ctx *c, int map, int64_t n, const double *pts, int K, double
   const auto &perm = c->hmap[map].perm;
   for (size_t i = 0; i < idx.size(); i++) idx_out[i] = idx[i] >= 0 ? perm[idx[i]] : -1;
   dq.release(); di.release(); dd.release(); dn.release();
+  return GI_OK;
+}
+
+int gi_knn_bench(gi_ctx *c, int map, int64_t n, const double *pts, const double *nrm,
+                 const int32_t *mat, int mode, int kernel, int iters, double *ms_out,
+                 double *found_out, double *visited_out) {
+  if (!c || map < 0 || map > 1 || n <= 0 || !pts || iters <= 0 || mode < 0 || mode > 2)
+    return GI_ERR_ARG;
+  if (mode == KNN_MODE_RADIANCE && (!nrm || !mat || !c->have_scene))
+    return fail(c, GI_ERR_STATE, "radiance mode needs normals, materials and a scene");
+  std::vector<float> qp(4 * n, 0.0f);
+  std::vector<QShade> qs(n);
+  for (int64_t i = 0; i < n; i++) {
+    for (int j = 0; j < 3; j++) qp[4 * i + j] = (float)pts[3 * i + j];
+    uint32_t meta = mat ? ((uint32_t)std::max(0, mat[i]) << 2) : 0u;
+    memcpy(&qp[4 * i + 3], &meta, 4);
+    for (int j = 0; j < 3; j++) {
+      qs[i].n[j] = nrm ? nrm[3 * i + j] : 0.0;
+      qs[i].ex[j] = nrm ? nrm[3 * i + j] : 0.0;
+      qs[i].w[j] = 1.0;
+    }
+  }
+  KnnArgs k = knn_args(c, map);
+  DBuf dq, ds, dout, di, dd, dn;
+  HIPCHK(c, upload(dq, qp.data(), qp.size() * 4, c->stream));
+  HIPCHK(c, upload(ds, qs.data(), qs.size() * sizeof(QShade), c->stream));
+  HIPCHK(c, dout.ensure((size_t)n * 24));
+  k.qpos = dq.as<float4>();
+  k.qshade = ds.as<QShade>();
+  k.out = dout.as<double>();
+  k.mode = mode;
+  if (mode == KNN_MODE_LIST) {
+    HIPCHK(c, di.ensure((size_t)n * k.K * 4));
+    HIPCHK(c, dd.ensure((size_t)n * k.K * 4));
+    HIPCHK(c, dn.ensure((size_t)n * 4));
+    k.out_idx = di.as<int32_t>();
+    k.out_d2 = dd.as<float>();
+    k.out_n = dn.as<int32_t>();
+  }
+  float bmin[3], bmax[3];
+  for (int j = 0; j < 3; j++) { bmin[j] = FLT_MAX; bmax[j] = -FLT_MAX; }
+  for (int64_t i = 0; i < n; i++)
+    for (int j = 0; j < 3; j++) {
+      bmin[j] = std::min(bmin[j], qp[4 * i + j]);
+      bmax[j] = std::max(bmax[j], qp[4 * i + j]);
+    }
+  uint32_t *perm = nullptr;
+  HIPCHK(c, morton_order(dq.as<float4>(), n, bmin, bmax, c->sorter, &perm, c->stream));
+  k.perm = perm;
+  int saved = c->knn_kernel_kind;
+  if (kernel >= 0) c->knn_kernel_kind = kernel;
+  HIPCHK(c, hipMemsetAsync(c->d_stats.p, 0, ST_COUNT * 8, c->stream));
+  double ms = 0;
+  int rc = GI_OK;
+  for (int it = 0; it < iters && rc == GI_OK; it++) rc = run_knn(c, k, n, &ms);
+  c->knn_kernel_kind = saved;
+  if (rc) return rc;
+  unsigned long long st[ST_COUNT];
+  HIPCHK(c, hipMemcpyAsync(st, c->d_stats.p, sizeof st, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (ms_out) *ms_out = ms / iters;
+  double nqd = (double)std::max<unsigned long long>(1, st[ST_KNN]);
+  if (found_out) *found_out = (double)st[ST_KNN_PHOTONS] / nqd;
+  if (visited_out) *visited_out = (double)st[ST_KNN_VISITED] / nqd;
   return GI_OK;
 }
 

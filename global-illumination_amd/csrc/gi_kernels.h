@@ -52,16 +52,30 @@ struct RenderArgs {
   Spawn *spawn;
   uint32_t *npaths;     // [nprim]
   const uint32_t *path_off;  // [nprim + 1]
-  uint32_t *cnt_g, *cnt_c;   // [total_paths]
-  const uint32_t *goff, *coff;  // [total_paths + 1]
-  float4 *gpos, *cpos;
-  QShade *gshade, *cshade;
+  // query lists (0 = global map, 1 = caustic map): appended with an atomic counter; each
+  // query carries key = path_slot << 20 | index-in-path so the per-pixel reduction can sum
+  // them in a deterministic order after a key sort
+  float4 *qpos[2];
+  QShade *qshade[2];
+  uint64_t *qkey[2];
+  uint32_t *qcount;     // [2] device counters
+  uint32_t qcap[2];
+  const uint64_t *skey[2];    // sorted keys
+  const uint32_t *sslot[2];   // slot of each sorted key
+  uint32_t nq[2];
   double *base;         // [total_paths * 3]
-  const double *gout, *cout;   // k-NN contributions
+  const double *qout[2];       // k-NN contributions per slot
   float *rgbf;
   uint8_t *rgb8;
   unsigned long long *stats;
 };
+
+// wave-level counter reduction (one atomic per wave)
+__device__ __forceinline__ void wave_add(unsigned long long *dst, uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, (unsigned long long)v);
+}
 
 enum { KNN_MODE_RADIANCE = 0, KNN_MODE_IRRADIANCE = 1, KNN_MODE_LIST = 2 };
 
@@ -72,7 +86,8 @@ struct KnnArgs {
   const uint32_t *perm;    // optional query order (spatial sort)
   const DMaterial *mats;
   const double *lut;       // 65536 x 3 direction table
-  int64_t nq;
+  int64_t nq;              // queries in this launch
+  int64_t q0;              // first (sorted) query position of this launch
   int32_t K;
   int32_t filter;
   int32_t mode;
@@ -111,9 +126,11 @@ struct ScanTemp {
 hipError_t launch_scan(const uint32_t *in, uint32_t *out, int64_t n, ScanTemp &tmp,
                        hipStream_t st);
 void launch_primary(const RenderArgs &a, hipStream_t st);
-void launch_path(const RenderArgs &a, bool emit, hipStream_t st);
+void launch_path(const RenderArgs &a, hipStream_t st);
 void launch_reduce(const RenderArgs &a, hipStream_t st);
 void launch_knn(const KnnArgs &a, bool lds_heap, hipStream_t st);
+bool launch_knn_wave(const KnnArgs &a, hipStream_t st);
+bool launch_knn_packet(const KnnArgs &a, hipStream_t st);
 void launch_cached(const KnnArgs &a, hipStream_t st);
 void launch_photons(const PhotonArgs &a, bool emit, hipStream_t st);
 void launch_intersect(const SceneView &S, int64_t n, const double *org, const double *dir,

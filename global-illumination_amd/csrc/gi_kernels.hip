@@ -18,15 +18,6 @@
 namespace gi {
 
 // ---------------------------------------------------------------------------------------
-// wave-level counter reduction (one atomic per wave)
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ void wave_add(unsigned long long *dst, uint64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, (unsigned long long)v);
-}
-
-// ---------------------------------------------------------------------------------------
 // exclusive scan of uint32 -> uint32 (n+1 outputs, last = total)
 // ---------------------------------------------------------------------------------------
 constexpr int SCAN_BLOCK = 256, SCAN_ITEMS = 4, SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
@@ -165,42 +156,47 @@ __global__ __launch_bounds__(256) void primary_kernel(RenderArgs a) {
   wave_add(&a.stats[ST_INDIRECT], c_ind);
 }
 
-// query sink: count mode only counts; emit mode writes (point f32, meta) + shading record
-struct QSink {
-  float4 *pos;
-  QShade *shade;
-  uint32_t off;
-};
-
-__device__ __forceinline__ void put_query(bool emit, QSink &s, uint32_t &count, V p, V n, V ex,
-                                          double ct, int mat, C3 w) {
-  if (emit) {
-    uint32_t sign = (ct > 0) ? 1u : ((ct < 0) ? 2u : 0u);
-    uint32_t meta = sign | ((uint32_t)mat << 2);
-    s.pos[s.off] = make_float4((float)p.x, (float)p.y, (float)p.z, __uint_as_float(meta));
-    QShade q;
-    q.n[0] = n.x; q.n[1] = n.y; q.n[2] = n.z;
-    q.ex[0] = ex.x; q.ex[1] = ex.y; q.ex[2] = ex.z;
-    q.w[0] = w.r; q.w[1] = w.g; q.w[2] = w.b;
-    s.shade[s.off] = q;
-    s.off++;
-  }
-  count++;
-}
-
 struct PathCtx {
   const SceneView *S;
   const Flags *F;
-  bool emit;
-  QSink g, c;
-  uint32_t ng, nc;
+  const RenderArgs *A;
+  uint64_t g;       // path slot
+  uint32_t j;       // queries issued so far by this path
   C3 base;
   Counts cnt;
 };
 
+// append one photon-map query (list 0 = global, 1 = caustic): search half (point as f32 +
+// meta) and shading half (normal, exact bounce, path weight)
+__device__ __forceinline__ void put_query(PathCtx &P, int list, V p, V n, V ex, double ct,
+                                          int mat, C3 w) {
+  const RenderArgs &a = *P.A;
+  // one atomic per wave for all lanes that emit here (a single counter word serialises
+  // ~10^8 atomics/s, MI355X_MICROARCH.md 'dequeue')
+  uint64_t act = __ballot(1);
+  int lane = (int)(threadIdx.x & 63);
+  int leader = __ffsll((long long)act) - 1;
+  uint32_t rank = (uint32_t)__popcll(act & ((1ull << lane) - 1ull));
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(&a.qcount[list], (uint32_t)__popcll(act));
+  base = (uint32_t)__shfl((int)base, leader, 64);
+  uint32_t slot = base + rank;
+  uint64_t key = (P.g << 20) | (uint64_t)(P.j++);
+  if (slot >= a.qcap[list]) return;  // overflow: the host grows the lists and re-runs
+  uint32_t sign = (ct > 0) ? 1u : ((ct < 0) ? 2u : 0u);
+  uint32_t meta = sign | ((uint32_t)mat << 2);
+  a.qpos[list][slot] = make_float4((float)p.x, (float)p.y, (float)p.z, __uint_as_float(meta));
+  QShade q;
+  q.n[0] = n.x; q.n[1] = n.y; q.n[2] = n.z;
+  q.ex[0] = ex.x; q.ex[1] = ex.y; q.ex[2] = ex.z;
+  q.w[0] = w.r; q.w[1] = w.g; q.w[2] = w.b;
+  a.qshade[list][slot] = q;
+  a.qkey[list][slot] = key;
+}
+
 // global-map lookup at a diffuse hit: EstimateRadiance or (with -cache) the cached radiance
 __device__ __forceinline__ void global_query(PathCtx &P, V p, V n, V ex, double ct, int mat, C3 w) {
-  put_query(P.emit, P.g, P.ng, p, n, ex, ct, mat, w);
+  put_query(P, 0, p, n, ex, ct, mat, w);
 }
 
 // MonteCarlo_IndirectSample, montecarlo.cpp:177-305 (W = outer weight of this path)
@@ -275,7 +271,7 @@ __device__ __noinline__ void mc_path(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
       direct_illumination(S, F, h.p, h.n, ray_start, cb, m, ct, true, rng, P.cnt);
     if (F.caustic && (m.flags & MF_DIFFUSE)) {
       V ex = reflective_bounce(h.n, view, ct);
-      put_query(P.emit, P.c, P.nc, h.p, h.n, ex, ct, h.mat, W * tw);
+      put_query(P, 1, h.p, h.n, ex, ct, h.mat, W * tw);
       P.cnt.caustic++;
     }
     P.base += W * (cb * tw);
@@ -327,7 +323,6 @@ __device__ __noinline__ void mc_path(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
 // Expand path slot g of the batch: slot 0 of a primary sample = its own photon-map queries
 // (CausticIllumination / EstimateGlobalIllumination at the primary hit) and base colour;
 // slots 1.. = transmissive, specular and indirect sample paths (raytracer.cpp:47-135).
-template <bool EMIT>
 __global__ __launch_bounds__(128) void path_kernel(RenderArgs a) {
   int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   Counts cnt = {0, 0, 0, 0, 0, 0};
@@ -344,24 +339,21 @@ __global__ __launch_bounds__(128) void path_kernel(RenderArgs a) {
     PathCtx P;
     P.S = &a.S;
     P.F = &a.F;
-    P.emit = EMIT;
-    P.ng = P.nc = 0;
+    P.A = &a;
+    P.g = (uint64_t)g;
+    P.j = 0;
     P.base = rgb(0, 0, 0);
     P.cnt = cnt;
-    if (EMIT) {
-      P.g.pos = a.gpos; P.g.shade = a.gshade; P.g.off = a.goff[g];
-      P.c.pos = a.cpos; P.c.shade = a.cshade; P.c.off = a.coff[g];
-    }
     if (slot == 0) {
       P.base = ldc(sp.base);
       if (sp.hit) {
         V p = ld3(sp.p), n = ld3(sp.n), view = ld3(sp.v);
         V ex = reflective_bounce(n, view, sp.ct);
         if (sp.q_caus) {
-          put_query(EMIT, P.c, P.nc, p, n, ex, sp.ct, sp.mat, rgb(1, 1, 1));
+          put_query(P, 1, p, n, ex, sp.ct, sp.mat, rgb(1, 1, 1));
           P.cnt.caustic++;
         }
-        if (sp.q_glob) put_query(EMIT, P.g, P.ng, p, n, ex, sp.ct, sp.mat, rgb(1, 1, 1));
+        if (sp.q_glob) put_query(P, 0, p, n, ex, sp.ct, sp.mat, rgb(1, 1, 1));
       }
     } else {
       int pix, i, j, k;
@@ -400,24 +392,17 @@ __global__ __launch_bounds__(128) void path_kernel(RenderArgs a) {
         P.cnt.indirect++;
       }
     }
-    if (EMIT) {
-      a.base[3 * g] = P.base.r;
-      a.base[3 * g + 1] = P.base.g;
-      a.base[3 * g + 2] = P.base.b;
-    } else {
-      a.cnt_g[g] = P.ng;
-      a.cnt_c[g] = P.nc;
-    }
+    a.base[3 * g] = P.base.r;
+    a.base[3 * g + 1] = P.base.g;
+    a.base[3 * g + 2] = P.base.b;
     cnt = P.cnt;
   }
-  if (EMIT) {
-    wave_add(&a.stats[ST_SHADOW], cnt.shadow);
-    wave_add(&a.stats[ST_MONTE], cnt.monte);
-    wave_add(&a.stats[ST_TRANS], cnt.trans);
-    wave_add(&a.stats[ST_SPEC], cnt.spec);
-    wave_add(&a.stats[ST_INDIRECT], cnt.indirect);
-    wave_add(&a.stats[ST_CAUSTIC], cnt.caustic);
-  }
+  wave_add(&a.stats[ST_SHADOW], cnt.shadow);
+  wave_add(&a.stats[ST_MONTE], cnt.monte);
+  wave_add(&a.stats[ST_TRANS], cnt.trans);
+  wave_add(&a.stats[ST_SPEC], cnt.spec);
+  wave_add(&a.stats[ST_INDIRECT], cnt.indirect);
+  wave_add(&a.stats[ST_CAUSTIC], cnt.caustic);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -560,7 +545,8 @@ __global__ __launch_bounds__(64) void knn_kernel(KnnArgs a) {
       h.idx = a.gheap_idx + q;
       h.stride = (int)slot_stride;
     }
-    int64_t qi = a.perm ? (int64_t)a.perm[q] : q;
+    int64_t qg = a.q0 + q;
+    int64_t qi = a.perm ? (int64_t)a.perm[qg] : qg;
     float4 qp = a.qpos[qi];
     uint32_t visited = 0;
     int num = knn_search(a.map, qp.x, qp.y, qp.z, a.r2f, a.K, h, visited);
@@ -785,15 +771,21 @@ __global__ __launch_bounds__(64) void reduce_kernel(RenderArgs a) {
         c1 += a.base[3 * (int64_t)g + 1];
         c2 += a.base[3 * (int64_t)g + 2];
       }
-      for (uint32_t q = a.goff[p0]; q < a.goff[p1]; q++) {
-        c0 += a.gout[3 * (int64_t)q];
-        c1 += a.gout[3 * (int64_t)q + 1];
-        c2 += a.gout[3 * (int64_t)q + 2];
-      }
-      for (uint32_t q = a.coff[p0]; q < a.coff[p1]; q++) {
-        c0 += a.cout[3 * (int64_t)q];
-        c1 += a.cout[3 * (int64_t)q + 1];
-        c2 += a.cout[3 * (int64_t)q + 2];
+      for (int l = 0; l < 2; l++) {
+        const uint64_t *K = a.skey[l];
+        uint32_t n = a.nq[l];
+        uint64_t k0 = (uint64_t)p0 << 20, k1 = (uint64_t)p1 << 20;
+        uint32_t lo = 0, hi = n;
+        while (lo < hi) {
+          uint32_t mid = (lo + hi) >> 1;
+          if (K[mid] < k0) lo = mid + 1; else hi = mid;
+        }
+        for (uint32_t q = lo; q < n && K[q] < k1; q++) {
+          uint32_t sl = a.sslot[l][q];
+          c0 += a.qout[l][3 * (int64_t)sl];
+          c1 += a.qout[l][3 * (int64_t)sl + 1];
+          c2 += a.qout[l][3 * (int64_t)sl + 2];
+        }
       }
       s0 += c0; s1 += c1; s2 += c2;
     }
@@ -1025,10 +1017,9 @@ hipError_t launch_scan(const uint32_t *in, uint32_t *out, int64_t n, ScanTemp &t
 void launch_primary(const RenderArgs &a, hipStream_t st) {
   primary_kernel<<<nblk(a.nprim, 256), 256, 0, st>>>(a);
 }
-void launch_path(const RenderArgs &a, bool emit, hipStream_t st) {
+void launch_path(const RenderArgs &a, hipStream_t st) {
   if (a.total_paths == 0) return;
-  if (emit) path_kernel<true><<<nblk(a.total_paths, 128), 128, 0, st>>>(a);
-  else path_kernel<false><<<nblk(a.total_paths, 128), 128, 0, st>>>(a);
+  path_kernel<<<nblk(a.total_paths, 128), 128, 0, st>>>(a);
 }
 void launch_reduce(const RenderArgs &a, hipStream_t st) {
   reduce_kernel<<<nblk(a.npix, 64), 64, 0, st>>>(a);

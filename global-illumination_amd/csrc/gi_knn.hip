@@ -1,0 +1,550 @@
+// gi_knn.hip -- wave-cooperative k-nearest-photon radiance estimate (the dominant kernel).
+//
+// Re-expresses R3Kdtree<Photon*>::FindClosestQuick (R3Kdtree.cpp:688-784) + EstimateRadiance
+// (photon_utils.cpp:72-162) for CDNA4: ONE QUERY PER WAVE.
+//   * traversal of the implicit kd-tree is wave-uniform: node ids, split planes and leaf
+//     ranges live in SGPRs (scalar loads), nearest-first, stackless (parent = node>>1);
+//   * leaves hold <= 64 photons: one photon per lane, one coalesced 16-B load per lane;
+//   * candidates with key = (d2 bits << 32 | photon index) below the current threshold are
+//     appended to an LDS buffer by ballot/mbcnt compaction; when the buffer cannot take the
+//     next leaf, a bitonic sort of the buffer keeps the K best and tightens the threshold
+//     (the reference's delayed make_heap + replace-max, R3Kdtree.cpp:753-782, as a batched
+//     selection). Result set: the K smallest (d2, index) pairs with d2 <= r2 -- identical
+//     to the reference's set up to ties at the K-th distance.
+//   * the estimate sums the K photons across lanes and reduces in registers.
+// LDS per wave: CAP * 8 bytes (1 KiB for K <= 64, 4 KiB for K <= 448), so occupancy is set
+// by registers, not by a per-lane heap.
+#include <hip/hip_runtime.h>
+#include "gi_device.h"
+#include "gi_kernels.h"
+
+namespace gi {
+
+__device__ __forceinline__ uint32_t ufirst(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+__device__ __forceinline__ float ffirst(float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// bitonic sort of buf[0, CAP) ascending (CAP power of two, 64 lanes)
+template <int CAP>
+__device__ __forceinline__ void bitonic_sort(uint64_t *buf, int lane) {
+#pragma unroll 1
+  for (int k = 2; k <= CAP; k <<= 1) {
+#pragma unroll 1
+    for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+      for (int p = lane; p < CAP / 2; p += 64) {
+        int i = 2 * p - (p & (j - 1));
+        int ixj = i + j;
+        uint64_t x = buf[i], y = buf[ixj];
+        bool up = (i & k) == 0;
+        if ((x > y) == up) {
+          buf[i] = y;
+          buf[ixj] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+template <int CAP>
+__device__ __forceinline__ void select_k(uint64_t *buf, int lane, uint32_t &count, int K,
+                                         uint64_t &thr) {
+  for (int s = lane; s < CAP; s += 64)
+    if ((uint32_t)s >= count) buf[s] = ~0ull;
+  __syncthreads();
+  bitonic_sort<CAP>(buf, lane);
+  if (count > (uint32_t)K) count = (uint32_t)K;
+  if (count == (uint32_t)K) thr = buf[K - 1];  // candidates must beat the K-th
+}
+
+template <int CAP>
+__global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
+  __shared__ uint64_t buf[CAP];
+  const int lane = threadIdx.x;
+  const float2 *nodes = reinterpret_cast<const float2 *>(a.map.nodes);
+  const float4 *pos = reinterpret_cast<const float4 *>(a.map.pos4);
+  const int L = a.map.nleaves;
+  const int64_t N = a.map.n;
+  const int K = a.K;
+  uint64_t st_q = 0, st_found = 0, st_vis = 0;
+  for (int64_t qq = blockIdx.x; qq < a.nq; qq += gridDim.x) {
+    int64_t qg = a.q0 + qq;
+    int64_t qi = a.perm ? (int64_t)a.perm[qg] : qg;
+    float4 qp = a.qpos[qi];
+    float qx = ffirst(qp.x), qy = ffirst(qp.y), qz = ffirst(qp.z);
+    uint32_t count = 0;
+    // keys accepted while key < thr; start: every d2 <= r2
+    uint64_t thr = ((uint64_t)__float_as_uint(a.r2f) << 32) + 0x100000000ull;
+    uint32_t visited = 0;
+    if (N > 0) {
+      int node = 1;
+      bool done = false;
+      while (!done) {
+        while (node < L) {
+          float2 nd = nodes[node];
+          int axis = __float_as_int(nd.y);
+          float q = (axis == 0) ? qx : ((axis == 1) ? qy : qz);
+          node = 2 * node + ((q - nd.x >= 0.0f) ? 1 : 0);
+        }
+        int leaf = node - L;
+        int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
+        visited += (uint32_t)(s1 - s0);
+        for (int64_t base = s0; base < s1; base += 64) {
+          int64_t ii = base + lane;
+          uint64_t key = ~0ull;
+          if (ii < s1) {
+            float4 p = pos[ii];
+            float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
+            float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
+            key = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)(uint32_t)ii;
+          }
+          bool pass = key < thr;
+          uint64_t m = __ballot(pass);
+          uint32_t nnew = (uint32_t)__popcll(m);
+          if (nnew == 0) continue;
+          if (count + nnew > (uint32_t)CAP) {
+            select_k<CAP>(buf, lane, count, K, thr);
+            pass = key < thr;
+            m = __ballot(pass);
+            nnew = (uint32_t)__popcll(m);
+            if (nnew == 0) continue;
+          }
+          if (pass) {
+            uint32_t off = count + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            buf[off] = key;
+          }
+          count += nnew;
+          __syncthreads();
+        }
+        // prune with the current threshold's distance (a bound on the K-th distance)
+        float pr = __uint_as_float((uint32_t)((thr - 1ull) >> 32));
+        while (true) {
+          if (node == 1) { done = true; break; }
+          int parent = node >> 1;
+          float2 nd = nodes[parent];
+          int axis = __float_as_int(nd.y);
+          float q = (axis == 0) ? qx : ((axis == 1) ? qy : qz);
+          float diff = q - nd.x;
+          int near_is_right = (diff >= 0.0f) ? 1 : 0;
+          if ((node & 1) == near_is_right && __fmul_rn(diff, diff) <= pr) {
+            node ^= 1;
+            break;
+          }
+          node = parent;
+        }
+      }
+    }
+    // exact K best
+    if (count > (uint32_t)K) select_k<CAP>(buf, lane, count, K, thr);
+    int num = (int)count;
+    st_q += 1;
+    st_found += (uint64_t)num;
+    st_vis += visited;
+    if (a.mode == KNN_MODE_LIST) {
+      if (count > 0 && a.K > 0) {
+        // sort for a deterministic listing
+        select_k<CAP>(buf, lane, count, K, thr);
+      }
+      for (int s = lane; s < K; s += 64) {
+        bool v = s < num;
+        a.out_idx[qi * K + s] = v ? (int32_t)(uint32_t)buf[s] : -1;
+        a.out_d2[qi * K + s] = v ? __uint_as_float((uint32_t)(buf[s] >> 32)) : -1.0f;
+      }
+      if (lane == 0) a.out_n[qi] = num;
+      __syncthreads();
+      continue;
+    }
+    double maxd2 = kEps;
+    double o0 = 0, o1 = 0, o2 = 0;
+    if (num > 0) {
+      if (num < K) {
+        maxd2 = a.rmax * a.rmax;
+      } else {
+        double lm = 0.0;
+        for (int s = lane; s < num; s += 64) {
+          double d = (double)__uint_as_float((uint32_t)(buf[s] >> 32));
+          lm = d > lm ? d : lm;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          double t = __shfl_xor(lm, o, 64);
+          lm = t > lm ? t : lm;
+        }
+        if (lm > maxd2) maxd2 = lm;
+      }
+      if (a.mode == KNN_MODE_IRRADIANCE) {
+        for (int s = lane; s < num; s += 64) {
+          uint32_t e = a.map.rgbe[(uint32_t)buf[s]];
+          uint32_t ee = e >> 24;
+          if (ee) {
+            double inv = ldexp(1.0, (int)ee - 128 - 8);
+            o0 += (double)(e & 255u) * inv;
+            o1 += (double)((e >> 8) & 255u) * inv;
+            o2 += (double)((e >> 16) & 255u) * inv;
+          }
+        }
+        o0 = wave_sum(o0); o1 = wave_sum(o1); o2 = wave_sum(o2);
+        double den = kPi * maxd2;
+        o0 /= den; o1 /= den; o2 /= den;
+      } else {
+        const QShade &sh = a.qshade[qi];
+        uint32_t meta = __float_as_uint(qp.w);
+        uint32_t sign = meta & 3u;
+        const DMaterial &m = a.mats[meta >> 2];
+        double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
+        double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
+        bool spec = (m.flags & MF_SPECULAR) || (m.n < 0);
+        double c1 = 1.0, c2 = 1.0, tw = 0;
+        if (a.filter == 1) c1 = 1.0 / (a.fk * sqrt(maxd2));
+        else if (a.filter == 2) {
+          c1 = pow(2.7182818284590452354, -a.fb);
+          c2 = 1.0 / (2.0 * maxd2);
+        }
+        for (int s = lane; s < num; s += 64) {
+          uint32_t id = (uint32_t)buf[s];
+          double d2 = (double)__uint_as_float((uint32_t)(buf[s] >> 32));
+          uint32_t dcode = __float_as_uint(a.map.pos4[4 * (int64_t)id + 3]) & 0xffffu;
+          double ix = a.lut[3 * dcode], iy = a.lut[3 * dcode + 1], iz = a.lut[3 * dcode + 2];
+          double perp = N0 * ix + N1 * iy + N2 * iz;
+          if ((sign == 2u && perp < 0) || (sign == 1u && perp > 0)) continue;
+          uint32_t e = a.map.rgbe[id];
+          uint32_t ee = e >> 24;
+          double inv = ee ? ldexp(1.0, (int)ee - 128 - 8) : 0.0;
+          double p0 = ee ? (double)(e & 255u) * inv : 0.0;
+          double p1 = ee ? (double)((e >> 8) & 255u) * inv : 0.0;
+          double p2 = ee ? (double)((e >> 16) & 255u) * inv : 0.0;
+          double ca = E0 * -ix + E1 * -iy + E2 * -iz;
+          if (ca < 0) ca = 0;
+          double ap = fabs(perp);
+          double pw = spec ? pow(ca, m.n) : 0.0;
+          p0 *= ap * m.kd[0] + pw * m.ks[0];
+          p1 *= ap * m.kd[1] + pw * m.ks[1];
+          p2 *= ap * m.kd[2] + pw * m.ks[2];
+          if (a.filter == 1) {
+            double f = (1.0 - c1 * sqrt(d2));
+            p0 *= f; p1 *= f; p2 *= f;
+          } else if (a.filter == 2) {
+            double w = (1.0 - (1.0 - pow(c1, c2 * d2)) / (1.0 - c1));
+            p0 *= w; p1 *= w; p2 *= w;
+            tw += w;
+          }
+          o0 += p0; o1 += p1; o2 += p2;
+        }
+        o0 = wave_sum(o0); o1 = wave_sum(o1); o2 = wave_sum(o2);
+        if (a.filter == 2) tw = wave_sum(tw);
+        bool ok = true;
+        if (a.filter == 0 && maxd2 > 0) {
+          double den = kPi * maxd2;
+          o0 /= den; o1 /= den; o2 /= den;
+        } else if (a.filter == 1 && maxd2 > 0) {
+          double den = (1.0 - 2.0 / 3.0 / a.fk) * kPi * maxd2;
+          o0 /= den; o1 /= den; o2 /= den;
+        } else if (a.filter == 2 && tw > 0 && maxd2 > 0) {
+          double sc = a.fa * (num / tw) / (kPi * maxd2);
+          o0 *= sc; o1 *= sc; o2 *= sc;
+        } else {
+          ok = false;
+        }
+        if (ok) {
+          o0 *= sh.w[0]; o1 *= sh.w[1]; o2 *= sh.w[2];
+        } else {
+          o0 = o1 = o2 = 0;
+        }
+      }
+    }
+    if (lane == 0) {
+      a.out[3 * qi] = o0;
+      a.out[3 * qi + 1] = o1;
+      a.out[3 * qi + 2] = o2;
+      if (a.out_n) a.out_n[qi] = num;
+      if (a.out_maxd2) a.out_maxd2[qi] = (num > 0) ? (float)maxd2 : 0.0f;
+    }
+    __syncthreads();
+  }
+  if (a.stats && lane == 0) {
+    if (st_q) atomicAdd(&a.stats[ST_KNN], (unsigned long long)st_q);
+    if (st_found) atomicAdd(&a.stats[ST_KNN_PHOTONS], (unsigned long long)st_found);
+    if (st_vis) atomicAdd(&a.stats[ST_KNN_VISITED], (unsigned long long)st_vis);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Packet k-NN: 64 spatially adjacent queries (Morton order) per wave share ONE wave-uniform
+// traversal of the kd-tree, so each node and leaf fetch serves 64 queries. Every lane keeps
+// its own exact max-heap of the K best keys (d2 bits << 32 | photon index) in LDS laid out
+// [slot][lane] (8-B stride across lanes: conflict-free ds_read/write_b64).
+//
+// Exactness: a subtree is skipped only if, for EVERY lane, the query lies on the visited side
+// of the split and diff^2 > that lane's current bound (the single-query rule of
+// R3Kdtree.cpp:740-751 applied per lane), so each lane's result is the same K smallest
+// (d2, index) pairs with d2 <= r2 as the per-query search.
+// Visit order: at each node the packet descends first into the side holding the majority
+// of its queries (recomputed identically on the way up, which makes the walk stackless).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ float rlane(float v, int j) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+}
+
+__device__ __forceinline__ void kheap_push(uint64_t *h, int size, uint64_t key) {
+  int c = size;
+  while (c > 0) {
+    int p = (c - 1) >> 1;
+    uint64_t pk = h[p * 64];
+    if (pk >= key) break;
+    h[c * 64] = pk;
+    c = p;
+  }
+  h[c * 64] = key;
+}
+
+__device__ __forceinline__ void kheap_replace_top(uint64_t *h, int size, uint64_t key) {
+  int c = 0;
+  while (true) {
+    int l = 2 * c + 1;
+    if (l >= size) break;
+    uint64_t lk = h[l * 64];
+    if (l + 1 < size) {
+      uint64_t rk = h[(l + 1) * 64];
+      if (rk > lk) { l = l + 1; lk = rk; }
+    }
+    if (key >= lk) break;
+    h[c * 64] = lk;
+    c = l;
+  }
+  h[c * 64] = key;
+}
+
+__global__ __launch_bounds__(64) void knn_packet_kernel(KnnArgs a) {
+  extern __shared__ uint64_t hs[];
+  const int lane = threadIdx.x;
+  uint64_t *h = hs + lane;
+  const float2 *nodes = reinterpret_cast<const float2 *>(a.map.nodes);
+  const float4 *pos = reinterpret_cast<const float4 *>(a.map.pos4);
+  const int L = a.map.nleaves;
+  const int64_t N = a.map.n;
+  const int K = a.K;
+  const int64_t q = (int64_t)blockIdx.x * 64 + lane;
+  const bool valid = q < a.nq;
+  int64_t qi = 0;
+  float4 qp = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (valid) {
+    int64_t qg = a.q0 + q;
+    qi = a.perm ? (int64_t)a.perm[qg] : qg;
+    qp = a.qpos[qi];
+  }
+  int size = 0;
+  uint64_t thr = valid ? ((uint64_t)__float_as_uint(a.r2f) << 32) + 0x100000000ull : 0ull;
+  float pr = valid ? a.r2f : -1.0f;  // prune bound: d2 of the current threshold
+  const uint64_t vmask = __ballot(valid);
+  const int nvalid = __popcll(vmask);
+  uint32_t visited = 0;
+  if (N > 0 && K > 0) {
+    int node = 1;
+    while (true) {
+      // descend: majority side first
+      while (node < L) {
+        float2 nd = nodes[node];
+        int axis = __float_as_int(nd.y);
+        float qa = (axis == 0) ? qp.x : ((axis == 1) ? qp.y : qp.z);
+        int nr = __popcll(__ballot(valid && qa - nd.x >= 0.0f));
+        node = 2 * node + ((2 * nr > nvalid) ? 1 : 0);
+      }
+      int leaf = node - L;
+      int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
+      visited += (uint32_t)(s1 - s0);
+      for (int64_t b = s0; b < s1; b += 64) {
+        int cnt = (int)((s1 - b) < 64 ? (s1 - b) : 64);
+        float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (lane < cnt) p = pos[b + lane];
+        for (int j = 0; j < cnt; j++) {
+          float px = rlane(p.x, j), py = rlane(p.y, j), pz = rlane(p.z, j);
+          float dx = qp.x - px, dy = qp.y - py, dz = qp.z - pz;
+          float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
+          if (d2 <= pr) {
+            uint64_t key = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)(uint32_t)(b + j);
+            if (key < thr) {
+              if (size < K) {
+                kheap_push(h, size, key);
+                size++;
+                if (size == K) thr = h[0];
+              } else {
+                kheap_replace_top(h, size, key);
+                thr = h[0];
+              }
+              if (size == K) pr = __uint_as_float((uint32_t)(thr >> 32));
+            }
+          }
+        }
+      }
+      // backtrack to the deepest first-visited child whose sibling some lane still needs
+      bool done = false;
+      while (true) {
+        if (node == 1) { done = true; break; }
+        int parent = node >> 1;
+        float2 nd = nodes[parent];
+        int axis = __float_as_int(nd.y);
+        float qa = (axis == 0) ? qp.x : ((axis == 1) ? qp.y : qp.z);
+        float diff = qa - nd.x;
+        bool right = diff >= 0.0f;
+        int nr = __popcll(__ballot(valid && right));
+        int first = (2 * nr > nvalid) ? 1 : 0;
+        if ((node & 1) == first) {
+          bool need = valid && (((int)right != first) || __fmul_rn(diff, diff) <= pr);
+          if (__ballot(need)) {
+            node ^= 1;
+            break;
+          }
+        }
+        node = parent;
+      }
+      if (done) break;
+    }
+  }
+  int num = size;
+  if (valid) {
+    if (a.mode == KNN_MODE_LIST) {
+      for (int s = 0; s < K; s++) {
+        bool v = s < num;
+        uint64_t key = v ? h[s * 64] : 0ull;
+        a.out_idx[qi * K + s] = v ? (int32_t)(uint32_t)key : -1;
+        a.out_d2[qi * K + s] = v ? __uint_as_float((uint32_t)(key >> 32)) : -1.0f;
+      }
+      a.out_n[qi] = num;
+    } else {
+      double o0 = 0, o1 = 0, o2 = 0;
+      double maxd2 = kEps;
+      if (num > 0) {
+        // max-heap root = K-th distance (photon_utils.cpp:108-111); r_max^2 if fewer (Q4)
+        maxd2 = (num < K) ? a.rmax * a.rmax : (double)__uint_as_float((uint32_t)(h[0] >> 32));
+        if (num == K && maxd2 < kEps) maxd2 = kEps;
+        if (a.mode == KNN_MODE_IRRADIANCE) {
+          // EstimateIrradiance, photon_utils.cpp:209-246
+          for (int s = 0; s < num; s++) {
+            uint32_t e = a.map.rgbe[(uint32_t)h[s * 64]];
+            uint32_t ex = e >> 24;
+            if (ex) {
+              double inv = ldexp(1.0, (int)ex - 128 - 8);
+              o0 += (double)(e & 255u) * inv;
+              o1 += (double)((e >> 8) & 255u) * inv;
+              o2 += (double)((e >> 16) & 255u) * inv;
+            }
+          }
+          double den = kPi * maxd2;
+          o0 /= den; o1 /= den; o2 /= den;
+        } else {
+          // EstimateRadiance, photon_utils.cpp:113-158
+          const QShade &sh = a.qshade[qi];
+          uint32_t meta = __float_as_uint(qp.w);
+          uint32_t sign = meta & 3u;
+          const DMaterial &m = a.mats[meta >> 2];
+          double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
+          double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
+          bool spec = (m.flags & MF_SPECULAR) || (m.n < 0);
+          double c1 = 1.0, c2 = 1.0, tw = 0;
+          if (a.filter == 1) c1 = 1.0 / (a.fk * sqrt(maxd2));
+          else if (a.filter == 2) {
+            c1 = pow(2.7182818284590452354, -a.fb);
+            c2 = 1.0 / (2.0 * maxd2);
+          }
+          for (int s = 0; s < num; s++) {
+            uint64_t key = h[s * 64];
+            uint32_t id = (uint32_t)key;
+            double d2 = (double)__uint_as_float((uint32_t)(key >> 32));
+            uint32_t dcode = __float_as_uint(a.map.pos4[4 * (int64_t)id + 3]) & 0xffffu;
+            double ix = a.lut[3 * dcode], iy = a.lut[3 * dcode + 1], iz = a.lut[3 * dcode + 2];
+            double perp = N0 * ix + N1 * iy + N2 * iz;
+            if ((sign == 2u && perp < 0) || (sign == 1u && perp > 0)) continue;
+            uint32_t e = a.map.rgbe[id];
+            uint32_t ee = e >> 24;
+            double inv = ee ? ldexp(1.0, (int)ee - 128 - 8) : 0.0;
+            double p0 = ee ? (double)(e & 255u) * inv : 0.0;
+            double p1 = ee ? (double)((e >> 8) & 255u) * inv : 0.0;
+            double p2 = ee ? (double)((e >> 16) & 255u) * inv : 0.0;
+            double ca = E0 * -ix + E1 * -iy + E2 * -iz;
+            if (ca < 0) ca = 0;
+            double ap = fabs(perp);
+            double pw = spec ? pow(ca, m.n) : 0.0;
+            p0 *= ap * m.kd[0] + pw * m.ks[0];
+            p1 *= ap * m.kd[1] + pw * m.ks[1];
+            p2 *= ap * m.kd[2] + pw * m.ks[2];
+            if (a.filter == 1) {
+              double f = (1.0 - c1 * sqrt(d2));
+              p0 *= f; p1 *= f; p2 *= f;
+            } else if (a.filter == 2) {
+              double w = (1.0 - (1.0 - pow(c1, c2 * d2)) / (1.0 - c1));
+              p0 *= w; p1 *= w; p2 *= w;
+              tw += w;
+            }
+            o0 += p0; o1 += p1; o2 += p2;
+          }
+          bool ok = true;
+          if (a.filter == 0 && maxd2 > 0) {
+            double den = kPi * maxd2;
+            o0 /= den; o1 /= den; o2 /= den;
+          } else if (a.filter == 1 && maxd2 > 0) {
+            double den = (1.0 - 2.0 / 3.0 / a.fk) * kPi * maxd2;
+            o0 /= den; o1 /= den; o2 /= den;
+          } else if (a.filter == 2 && tw > 0 && maxd2 > 0) {
+            double sc = a.fa * (num / tw) / (kPi * maxd2);
+            o0 *= sc; o1 *= sc; o2 *= sc;
+          } else {
+            ok = false;
+          }
+          if (ok) {
+            o0 *= sh.w[0]; o1 *= sh.w[1]; o2 *= sh.w[2];
+          } else {
+            o0 = o1 = o2 = 0;
+          }
+        }
+      }
+      a.out[3 * qi] = o0;
+      a.out[3 * qi + 1] = o1;
+      a.out[3 * qi + 2] = o2;
+      if (a.out_n) a.out_n[qi] = num;
+      if (a.out_maxd2) a.out_maxd2[qi] = (num > 0) ? (float)maxd2 : 0.0f;
+    }
+  }
+  if (a.stats) {
+    uint64_t nq_done = valid ? 1 : 0, found = valid ? (uint64_t)num : 0,
+             vis = valid ? (uint64_t)visited : 0;
+    wave_add(&a.stats[ST_KNN], nq_done);
+    wave_add(&a.stats[ST_KNN_PHOTONS], found);
+    wave_add(&a.stats[ST_KNN_VISITED], vis);
+  }
+}
+
+bool launch_knn_packet(const KnnArgs &a, hipStream_t st) {
+  if (a.nq == 0) return true;
+  size_t lds = (size_t)(a.K > 0 ? a.K : 1) * 64 * sizeof(uint64_t);
+  if (lds > 160 * 1024) return false;
+  if (lds > 64 * 1024)
+    hipFuncSetAttribute((const void *)knn_packet_kernel,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  unsigned grid = (unsigned)((a.nq + 63) / 64);
+  knn_packet_kernel<<<grid, 64, lds, st>>>(a);
+  return true;
+}
+
+bool launch_knn_wave(const KnnArgs &a, hipStream_t st) {
+  if (a.nq == 0) return true;
+  int need = a.K + 64;
+  int64_t grid = a.nq < (1 << 16) ? a.nq : (1 << 16);
+  if (need <= 128) knn_wave_kernel<128><<<(unsigned)grid, 64, 0, st>>>(a);
+  else if (need <= 256) knn_wave_kernel<256><<<(unsigned)grid, 64, 0, st>>>(a);
+  else if (need <= 512) knn_wave_kernel<512><<<(unsigned)grid, 64, 0, st>>>(a);
+  else if (need <= 1024) knn_wave_kernel<1024><<<(unsigned)grid, 64, 0, st>>>(a);
+  else return false;
+  return true;
+}
+
+}  // namespace gi

@@ -1,0 +1,24 @@
+// gi_sort.h -- Morton ordering of query batches (gi_sort.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gi {
+struct SortScratch {
+  void *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *v1 = nullptr, *tmp = nullptr;
+  size_t k0_cap = 0, k1_cap = 0, v0_cap = 0, v1_cap = 0, tmp_cap = 0;
+};
+// returns a device permutation (sorted position -> query index) valid until the next call
+hipError_t morton_order(const float4 *q, int64_t n, const float bmin[3], const float bmax[3],
+                        SortScratch &s, uint32_t **perm_out, hipStream_t st);
+void sort_scratch_release(SortScratch &s);
+
+struct KeySortScratch {
+  void *k1 = nullptr, *v0 = nullptr, *v1 = nullptr, *tmp = nullptr;
+  size_t k1_cap = 0, v0_cap = 0, v1_cap = 0, tmp_cap = 0;
+};
+// stable order of 64-bit keys: sorted keys + the original slot of each
+hipError_t key_order(const uint64_t *keys, int64_t n, int key_bits, KeySortScratch &s,
+                     uint64_t **skeys, uint32_t **sslots, hipStream_t st);
+void sort_scratch_release(KeySortScratch &s);
+}  // namespace gi

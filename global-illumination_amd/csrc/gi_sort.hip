@@ -1,0 +1,130 @@
+// gi_sort.hip -- spatial ordering of photon-map queries.
+//
+// The reference answers k-NN queries one at a time in path order (photon_utils.cpp:79), so
+// consecutive queries land anywhere in the scene. On the GPU a wave runs 64 queries in
+// lock-step: ordering queries along a 30-bit Morton curve over the scene box makes a wave's
+// lanes walk the same kd-tree nodes and leaves (coherent control flow, L1/L2 reuse). The
+// results are written back to each query's original slot, so the order is invisible to the
+// per-pixel reduction.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+#include "gi_sort.h"
+
+namespace gi {
+
+__device__ __forceinline__ uint32_t spread10(uint32_t v) {
+  v &= 0x3ffu;
+  v = (v | (v << 16)) & 0x030000FFu;
+  v = (v | (v << 8)) & 0x0300F00Fu;
+  v = (v | (v << 4)) & 0x030C30C3u;
+  v = (v | (v << 2)) & 0x09249249u;
+  return v;
+}
+
+__global__ void morton_kernel(const float4 *q, int64_t n, float ox, float oy, float oz,
+                              float sx, float sy, float sz, uint32_t *keys, uint32_t *vals) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float4 p = q[i];
+  float fx = fminf(fmaxf((p.x - ox) * sx, 0.0f), 1023.0f);
+  float fy = fminf(fmaxf((p.y - oy) * sy, 0.0f), 1023.0f);
+  float fz = fminf(fmaxf((p.z - oz) * sz, 0.0f), 1023.0f);
+  keys[i] = (spread10((uint32_t)fx) << 2) | (spread10((uint32_t)fy) << 1) | spread10((uint32_t)fz);
+  vals[i] = (uint32_t)i;
+}
+
+hipError_t morton_order(const float4 *q, int64_t n, const float bmin[3], const float bmax[3],
+                        SortScratch &s, uint32_t **perm_out, hipStream_t st) {
+  *perm_out = nullptr;
+  if (n <= 0) return hipSuccess;
+  hipError_t e;
+  auto grow = [&](void *&p, size_t &cap, size_t bytes) -> hipError_t {
+    if (bytes <= cap && p) return hipSuccess;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t r = hipMalloc(&p, bytes);
+    if (r == hipSuccess) cap = bytes;
+    return r;
+  };
+  size_t b4 = (size_t)n * 4;
+  if ((e = grow(s.k0, s.k0_cap, b4)) != hipSuccess) return e;
+  if ((e = grow(s.k1, s.k1_cap, b4)) != hipSuccess) return e;
+  if ((e = grow(s.v0, s.v0_cap, b4)) != hipSuccess) return e;
+  if ((e = grow(s.v1, s.v1_cap, b4)) != hipSuccess) return e;
+  float sc[3];
+  for (int i = 0; i < 3; i++) {
+    float ext = bmax[i] - bmin[i];
+    sc[i] = ext > 0 ? 1023.0f / ext : 0.0f;
+  }
+  morton_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(
+      q, n, bmin[0], bmin[1], bmin[2], sc[0], sc[1], sc[2], (uint32_t *)s.k0, (uint32_t *)s.v0);
+  size_t tb = 0;
+  e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t *)s.k0, (uint32_t *)s.k1,
+                                         (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0, 30,
+                                         st);
+  if (e != hipSuccess) return e;
+  if ((e = grow(s.tmp, s.tmp_cap, tb + 256)) != hipSuccess) return e;
+  e = hipcub::DeviceRadixSort::SortPairs(s.tmp, tb, (const uint32_t *)s.k0, (uint32_t *)s.k1,
+                                         (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0, 30,
+                                         st);
+  if (e != hipSuccess) return e;
+  *perm_out = (uint32_t *)s.v1;
+  return hipSuccess;
+}
+
+__global__ void iota_kernel(uint32_t *v, int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) v[i] = (uint32_t)i;
+}
+
+hipError_t key_order(const uint64_t *keys, int64_t n, int key_bits, KeySortScratch &s,
+                     uint64_t **skeys, uint32_t **sslots, hipStream_t st) {
+  *skeys = nullptr;
+  *sslots = nullptr;
+  if (n <= 0) return hipSuccess;
+  hipError_t e;
+  auto grow = [&](void *&p, size_t &cap, size_t bytes) -> hipError_t {
+    if (bytes <= cap && p) return hipSuccess;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t r = hipMalloc(&p, bytes);
+    if (r == hipSuccess) cap = bytes;
+    return r;
+  };
+  if ((e = grow(s.k1, s.k1_cap, (size_t)n * 8)) != hipSuccess) return e;
+  if ((e = grow(s.v0, s.v0_cap, (size_t)n * 4)) != hipSuccess) return e;
+  if ((e = grow(s.v1, s.v1_cap, (size_t)n * 4)) != hipSuccess) return e;
+  iota_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>((uint32_t *)s.v0, n);
+  size_t tb = 0;
+  e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, (uint64_t *)s.k1,
+                                         (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0,
+                                         key_bits, st);
+  if (e != hipSuccess) return e;
+  if ((e = grow(s.tmp, s.tmp_cap, tb + 256)) != hipSuccess) return e;
+  e = hipcub::DeviceRadixSort::SortPairs(s.tmp, tb, keys, (uint64_t *)s.k1,
+                                         (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0,
+                                         key_bits, st);
+  if (e != hipSuccess) return e;
+  *skeys = (uint64_t *)s.k1;
+  *sslots = (uint32_t *)s.v1;
+  return hipSuccess;
+}
+
+void sort_scratch_release(KeySortScratch &s) {
+  void *ps[] = {s.k1, s.v0, s.v1, s.tmp};
+  for (void *p : ps)
+    if (p) hipFree(p);
+  s = KeySortScratch();
+}
+
+void sort_scratch_release(SortScratch &s) {
+  void *ps[] = {s.k0, s.k1, s.v0, s.v1, s.tmp};
+  for (void *p : ps)
+    if (p) hipFree(p);
+  s = SortScratch();
+}
+
+}  // namespace gi

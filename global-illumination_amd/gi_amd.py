@@ -28,7 +28,8 @@ EXPORTED = [
     "gi_params_default", "gi_parse_args", "gi_create", "gi_destroy", "gi_last_error",
     "gi_set_params", "gi_read_scene", "gi_scene_info", "gi_map_photons", "gi_set_photon_map",
     "gi_get_photon_map", "gi_render_image", "gi_render_tiles", "gi_quantize",
-    "gi_estimate_radiance_batch", "gi_knn_batch", "gi_intersect_batch", "gi_write_image",
+    "gi_estimate_radiance_batch", "gi_knn_batch", "gi_knn_bench", "gi_intersect_batch",
+    "gi_write_image",
 ]
 
 
@@ -67,7 +68,7 @@ class RenderStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "screen_rays", "shadow_rays", "monte_carlo_rays", "transmissive_samples",
         "specular_samples", "indirect_samples", "caustic_samples", "knn_queries",
-        "knn_photons")] + [("render_s", C.c_double), ("knn_kernel_ms", C.c_double),
+        "knn_photons", "knn_visited")] + [("render_s", C.c_double), ("knn_kernel_ms", C.c_double),
                            ("knn_kernel_launches", C.c_double)]
 
 
@@ -108,6 +109,9 @@ def lib():
                                                  C.c_void_p, C.c_void_p, C.c_void_p]
         L.gi_knn_batch.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_int,
                                    C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.gi_knn_bench.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p,
+                                   C.c_void_p, C.c_int, C.c_int, C.c_int, P(C.c_double),
+                                   P(C.c_double), P(C.c_double)]
         L.gi_intersect_batch.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
                                          C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_void_p]
@@ -234,6 +238,19 @@ class Renderer:
         self._check(lib().gi_knn_batch(self._ctx, which, n, pts.ctypes.data, k, max_dist,
                                        idx.ctypes.data, d2.ctypes.data, nf.ctypes.data))
         return idx, d2, nf
+
+    def knn_bench(self, which, points, normals=None, materials=None, mode=0, kernel=-1,
+                  iters=3):
+        """Time the k-NN estimate kernel on resident queries (diagnostics; gi_knn_bench)."""
+        pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
+        nrm = None if normals is None else np.ascontiguousarray(normals, dtype=np.float64)
+        mat = None if materials is None else np.ascontiguousarray(materials, dtype=np.int32)
+        ms, fq, vq = C.c_double(), C.c_double(), C.c_double()
+        self._check(lib().gi_knn_bench(
+            self._ctx, which, len(pts), pts.ctypes.data,
+            None if nrm is None else nrm.ctypes.data, None if mat is None else mat.ctypes.data,
+            mode, kernel, iters, C.byref(ms), C.byref(fq), C.byref(vq)))
+        return ms.value, fq.value, vq.value
 
     def Intersects(self, org, dirs):
         org = np.ascontiguousarray(org, dtype=np.float64).reshape(-1, 3)

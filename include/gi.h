@@ -132,6 +132,7 @@ typedef struct gi_render_stats {
   uint64_t screen_rays, shadow_rays, monte_carlo_rays, transmissive_samples;
   uint64_t specular_samples, indirect_samples, caustic_samples;
   uint64_t knn_queries, knn_photons;   /* sum over queries of photons returned */
+  uint64_t knn_visited;                /* photons distance-tested by the k-NN search */
   double render_s;                     /* wall time of the render phase       */
   double knn_kernel_ms;                /* summed k-NN kernel time (HIP events) */
   double knn_kernel_launches;
@@ -179,6 +180,14 @@ int gi_estimate_radiance_batch(gi_ctx *ctx, int map, int64_t n, const gi_radianc
                                double *rgb_out, int32_t *nfound, float *max_d2);
 int gi_knn_batch(gi_ctx *ctx, int map, int64_t n, const double *points, int k, double max_dist,
                  int32_t *idx_out, float *d2_out, int32_t *nfound);
+/* Diagnostics: time the k-NN estimate kernel over n resident queries (Morton-ordered as in
+ * rendering; mode 0 radiance, 1 irradiance, 2 list) for `iters` launches with the given
+ * kernel (-1 = default, 0 per-lane, 1 query-per-wave, 2 packet). Uses the context's
+ * estimate size / distance / filter for `map`. Outputs average ms per launch and the
+ * photons found / visited per query. No reference counterpart (measurement only). */
+int gi_knn_bench(gi_ctx *ctx, int map, int64_t n, const double *points, const double *normals,
+                 const int32_t *materials, int mode, int kernel, int iters, double *ms_per_launch,
+                 double *found_per_query, double *visited_per_query);
 int gi_intersect_batch(gi_ctx *ctx, int64_t n, const double *org, const double *dir,
                        int32_t *hit, double *t, double *point, double *normal, int32_t *material);
 

@@ -48,6 +48,22 @@ def parse():
     return ap.parse_args()
 
 
+def load_traffic(a):
+    """HBM bytes per launch of the roofline kernel from a committed PMC pass
+    (tools/pmc_traffic.py -> profiles/knn_traffic.json), if it was taken on this workload."""
+    path = os.path.join(ROOT, "profiles", "knn_traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    wl = t.get("workload", {})
+    if (wl.get("res"), wl.get("aa"), wl.get("global"), wl.get("caustic")) != (
+            a.res, a.aa, a.global_photons, a.caustic_photons):
+        return None
+    return t.get("bytes_per_launch")
+
+
 def cpu_baseline(a):
     """Oracle restatement (port) of the reference path timed on this host: same scene, flags
     and photon counts, on a res x res pixel sample of the same image plane (uniform sub-grid,
@@ -118,43 +134,55 @@ def main():
         step()
     barrier()
     t0 = time.perf_counter()
-    agg = {"knn_photons": 0, "knn_queries": 0, "knn_visited": 0, "knn_kernel_ms": 0.0,
-           "knn_kernel_launches": 0.0}
+    keys = ("q0", "q1", "ph0", "ph1", "vis0", "vis1", "ms0", "ms1", "n0", "n1")
+    agg = dict.fromkeys(keys, 0.0)
     for _ in range(a.steps):
         st = step()
-        for k in agg:
-            agg[k] += st[k]
+        for m in (0, 1):
+            agg[f"q{m}"] += st["knn_map_queries"][m]
+            agg[f"ph{m}"] += st["knn_map_photons"][m]
+            agg[f"vis{m}"] += st["knn_map_visited"][m]
+            agg[f"ms{m}"] += st["knn_map_kernel_ms"][m]
+            agg[f"n{m}"] += st["knn_map_launches"][m]
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
         import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64,
-                          device=("cuda" if torch.cuda.is_available() else "cpu"))
+        dev = "cuda" if torch.cuda.is_available() else "cpu"
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-        ag = torch.tensor([agg["knn_photons"], agg["knn_queries"], agg["knn_kernel_ms"]],
-                          dtype=torch.float64, device=tt.device)
+        ag = torch.tensor([agg[k] for k in keys], dtype=torch.float64, device=dev)
         dist.all_reduce(ag)  # sums over ranks (kernel ms summed over GPUs)
-        agg["knn_photons"], agg["knn_queries"], agg["knn_kernel_ms"] = [float(x) for x in ag.tolist()]
+        agg = dict(zip(keys, [float(x) for x in ag.tolist()]))
     samples_per_frame = w * h * 4 ** aa * p.dof_test
     value = samples_per_frame * a.steps / elapsed / 1e6
     ms_per_step = elapsed / a.steps * 1000.0
 
     if rank == 0:
-        # roofline of the dominant kernel (k-NN radiance estimate), HIP-event timed in-library
-        knn_s = agg["knn_kernel_ms"] / 1000.0
-        alg_bytes = agg["knn_photons"] * BYTES_PER_PHOTON
-        achieved = alg_bytes / knn_s / 1e9 if knn_s > 0 else 0.0
-        if world > 1:
-            achieved *= 1.0  # bytes and kernel seconds both summed over GPUs: per-GPU rate
-        roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None,
-                    "kernel": "knn_kernel<true> (k-NN + EstimateRadiance)",
-                    "bytes_per_unit": "16 B per photon returned",
-                    "photons_per_frame": agg["knn_photons"] / a.steps,
-                    "queries_per_frame": agg["knn_queries"] / a.steps,
-                    "visited_per_query": agg["knn_visited"] / max(1, agg["knn_queries"]),
-                    "knn_ms_per_frame": agg["knn_kernel_ms"] / a.steps / max(1, world)}
+        # roofline of the dominant kernel: the global-map k-NN radiance estimate
+        # (knn_kernel<true>, K=50), HIP-event timed in-library on the render stream
+        def kstats(m):
+            ms = agg[f"ms{m}"]
+            launches = max(1.0, agg[f"n{m}"])
+            photons = agg[f"ph{m}"]
+            ach = photons * BYTES_PER_PHOTON / (ms / 1000.0) / 1e9 if ms > 0 else 0.0
+            return {"achieved_GBps": round(ach, 2),
+                    "launches": agg[f"n{m}"],
+                    "avg_launch_ms": round(ms / launches, 3),
+                    "alg_bytes_per_launch": photons * BYTES_PER_PHOTON / launches,
+                    "queries_per_launch": agg[f"q{m}"] / launches,
+                    "photons_per_query": photons / max(1.0, agg[f"q{m}"]),
+                    "visited_per_query": agg[f"vis{m}"] / max(1.0, agg[f"q{m}"]),
+                    "ms_per_frame": ms / a.steps / max(1, world)}
+        g, c = kstats(0), kstats(1)
+        traffic = load_traffic(a)
+        roofline = {"bound": "hbm", "achieved": g["achieved_GBps"], "peak": HBM_PEAK_GBPS,
+                    "unit": "GB/s", "frac": round(g["achieved_GBps"] / HBM_PEAK_GBPS, 5),
+                    "traffic": traffic,
+                    "kernel": "gi::knn_kernel<true> (global map k-NN + EstimateRadiance)",
+                    "bytes_per_unit": "16 B per photon returned (SURVEY.md 8(d))",
+                    "global": g, "caustic_kernel": dict(c, kernel="gi::knn_wave_kernel<512>")}
         cpu = None
         if not a.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(a)

@@ -78,7 +78,7 @@ struct HostMap {
   std::vector<int32_t> perm;       // kd order -> storage index
   std::vector<float> pos4;
   std::vector<uint32_t> rgbe;
-  std::vector<float> nodes;  // float2 per node
+  std::vector<float> nodes;  // 8 floats per node: {lo.xyz, split}, {hi.xyz, axis bits}
   int nleaves = 1, levels = 0;
   float bmin[3] = {0, 0, 0}, bmax[3] = {0, 0, 0};
 };
@@ -107,9 +107,9 @@ void kd_rec(HostMap &M, int node, int a, int b, int depth_par) {
   } else if (hi > lo) {
     split = mx[axis];
   }
-  M.nodes[2 * node] = split;
+  M.nodes[8 * node + 3] = split;
   int ai = axis;
-  memcpy(&M.nodes[2 * node + 1], &ai, 4);
+  memcpy(&M.nodes[8 * node + 7], &ai, 4);
   if (depth_par > 0) {
     std::thread t([&]() { kd_rec(M, 2 * node, a, midleaf, depth_par - 1); });
     kd_rec(M, 2 * node + 1, midleaf, b, depth_par - 1);
@@ -127,10 +127,11 @@ void kd_build(HostMap &M, int leaf_size, int threads) {
   while ((int64_t)M.nleaves * leaf_size < n) { M.nleaves *= 2; M.levels++; }
   M.perm.resize(n);
   for (int64_t i = 0; i < n; i++) M.perm[i] = (int32_t)i;
-  M.nodes.assign(2 * (size_t)M.nleaves, 0.0f);
+  const int L = M.nleaves;
+  M.nodes.assign(8 * 2 * (size_t)L, 0.0f);
   int par = 0;
   while ((1 << par) < threads && par < 4) par++;
-  if (n > 0) kd_rec(M, 1, 0, M.nleaves, par);
+  if (n > 0) kd_rec(M, 1, 0, L, par);
   M.pos4.resize(4 * (size_t)n);
   M.rgbe.resize(n);
   for (int k = 0; k < 3; k++) { M.bmin[k] = FLT_MAX; M.bmax[k] = -FLT_MAX; }
@@ -145,6 +146,27 @@ void kd_build(HostMap &M, int leaf_size, int threads) {
     for (int k = 0; k < 3; k++) {
       M.bmin[k] = std::min(M.bmin[k], p.pos[k]);
       M.bmax[k] = std::max(M.bmax[k], p.pos[k]);
+    }
+  }
+  // tight boxes: leaves from their photons, internal nodes as the union of their children
+  // (an empty leaf gets lo = +inf, hi = -inf: its box distance is +inf)
+  for (int l = 0; l < L; l++) {
+    float *b = &M.nodes[8 * (size_t)(L + l)];
+    b[0] = b[1] = b[2] = INFINITY;
+    b[4] = b[5] = b[6] = -INFINITY;
+    int64_t s0 = (int64_t)l * n / L, s1 = (int64_t)(l + 1) * n / L;
+    for (int64_t i = s0; i < s1; i++)
+      for (int k = 0; k < 3; k++) {
+        b[k] = std::min(b[k], M.pos4[4 * i + k]);
+        b[4 + k] = std::max(b[4 + k], M.pos4[4 * i + k]);
+      }
+  }
+  for (int v = L - 1; v >= 1; v--) {
+    float *b = &M.nodes[8 * (size_t)v];
+    const float *c0 = &M.nodes[8 * (size_t)(2 * v)], *c1 = &M.nodes[8 * (size_t)(2 * v + 1)];
+    for (int k = 0; k < 3; k++) {
+      b[k] = std::min(c0[k], c1[k]);
+      b[4 + k] = std::max(c0[4 + k], c1[4 + k]);
     }
   }
 }
@@ -189,7 +211,7 @@ struct gi_ctx {
   DBuf qpos[2], qshade[2], qkey[2], qout[2];
   size_t qcap_hint[2] = {0, 0};
   KeySortScratch keysort[2];
-  int knn_kernel_kind = 2;  // 2 = packet (wave-shared traversal), 1 = query per wave, 0 = per-lane
+  int knn_kernel_kind = -1;  // -1 auto, 0 per-lane heap, 1 query per wave, 2 packet
   DBuf scan_lvl[8], scan_out[8];
   // photon tracing scratch
   DBuf pcounts, poffs, pbuf;
@@ -446,13 +468,16 @@ KnnArgs knn_args(gi_ctx *c, int mi) {
   k.fb = P.filter_const_b;
   k.fk = P.filter_const_k;
   k.stats = c->d_stats.as<unsigned long long>();
+  k.stat_off = mi == GI_MAP_GLOBAL ? 0 : ST_KNN_MAP;
   return k;
 }
 
 // run a k-NN launch over nq queries (chunked when the heap lives in global scratch)
 int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
-  // packet traversal while the per-lane heaps fit LDS at >= 2 waves/CU, else one query/wave
+  // auto (-1): per-lane LDS heaps while they fit (K <= 64), else one query per wave
+  // (measured with tools/knn_micro.py on cornell 1M+1M maps)
   int kind = c->knn_kernel_kind;
+  if (kind < 0) kind = (k.K <= 64) ? 0 : 1;
   if (kind == 2 && (int64_t)k.K * 64 * 8 > 80 * 1024) kind = 1;
   if ((kind == 1 && k.K + 64 <= 1024) || kind == 2) {
     k.nq = nq;
@@ -528,7 +553,7 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
   int64_t per_pix = (int64_t)af * af * dof;
   int64_t npix_total = (int64_t)pix_xy.size() / 2;
   int64_t pix_batch = std::max<int64_t>(1, c->prim_per_batch / per_pix);
-  double knn_ms = 0, launches = 0;
+  double knn_ms[2] = {0, 0}, launches[2] = {0, 0};
   HIPCHK(c, upload(c->pixels, pix_xy.data(), pix_xy.size() * 4, c->stream));
   HIPCHK(c, c->qcount.ensure(16));
   HIPCHK(c, c->stats_bak.ensure(ST_COUNT * 8));
@@ -603,9 +628,9 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
         HIPCHK(c, hipMemsetAsync(c->qout[l].p, 0, (size_t)nq[l] * 24, c->stream));
       } else {
         int rc = knn_list(c, l, a.qpos[l], a.qshade[l], nq[l], c->qout[l].as<double>(),
-                          rs ? &knn_ms : nullptr);
+                          rs ? &knn_ms[l] : nullptr);
         if (rc) return rc;
-        launches++;
+        launches[l]++;
       }
       uint64_t *sk = nullptr;
       uint32_t *ss = nullptr;
@@ -623,8 +648,12 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (rs) {
-    rs->knn_kernel_ms += knn_ms;
-    rs->knn_kernel_launches += launches;
+    for (int l = 0; l < 2; l++) {
+      rs->knn_map_kernel_ms[l] += knn_ms[l];
+      rs->knn_map_launches[l] += launches[l];
+      rs->knn_kernel_ms += knn_ms[l];
+      rs->knn_kernel_launches += launches[l];
+    }
   }
   return GI_OK;
 }
@@ -665,7 +694,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_LEAF_SIZE")) c->leaf_size = std::max(1, atoi(s));
   if (const char *s = getenv("GI_SORT_QUERIES")) c->sort_queries = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_KERNEL")) c->knn_kernel_kind = atoi(s);
-  if (c->knn_kernel_kind >= 1 && !getenv("GI_LEAF_SIZE")) c->leaf_size = 64;
+  if (!getenv("GI_LEAF_SIZE")) c->leaf_size = 64;
   *out = c;
   return GI_OK;
 }
@@ -893,9 +922,16 @@ static int render_common(gi_ctx *c, int aa, int w, int h, const std::vector<int3
     st->specular_samples = s[ST_SPEC];
     st->indirect_samples = s[ST_INDIRECT];
     st->caustic_samples = s[ST_CAUSTIC];
-    st->knn_queries = s[ST_KNN];
-    st->knn_photons = s[ST_KNN_PHOTONS];
-    st->knn_visited = s[ST_KNN_VISITED];
+    for (int m = 0; m < 2; m++) {
+      st->knn_map_queries[m] = s[ST_KNN + m * ST_KNN_MAP];
+      st->knn_map_photons[m] = s[ST_KNN_PHOTONS + m * ST_KNN_MAP];
+      st->knn_map_visited[m] = s[ST_KNN_VISITED + m * ST_KNN_MAP];
+      st->knn_map_kernel_ms[m] = local.knn_map_kernel_ms[m];
+      st->knn_map_launches[m] = local.knn_map_launches[m];
+    }
+    st->knn_queries = st->knn_map_queries[0] + st->knn_map_queries[1];
+    st->knn_photons = st->knn_map_photons[0] + st->knn_map_photons[1];
+    st->knn_visited = st->knn_map_visited[0] + st->knn_map_visited[1];
     st->knn_kernel_ms = local.knn_kernel_ms;
     st->knn_kernel_launches = local.knn_kernel_launches;
     st->render_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -1095,9 +1131,10 @@ int gi_knn_bench(gi_ctx *c, int map, int64_t n, const double *pts, const double 
   HIPCHK(c, hipMemcpyAsync(st, c->d_stats.p, sizeof st, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (ms_out) *ms_out = ms / iters;
-  double nqd = (double)std::max<unsigned long long>(1, st[ST_KNN]);
-  if (found_out) *found_out = (double)st[ST_KNN_PHOTONS] / nqd;
-  if (visited_out) *visited_out = (double)st[ST_KNN_VISITED] / nqd;
+  int so = map * ST_KNN_MAP;
+  double nqd = (double)std::max<unsigned long long>(1, st[ST_KNN + so]);
+  if (found_out) *found_out = (double)st[ST_KNN_PHOTONS + so] / nqd;
+  if (visited_out) *visited_out = (double)st[ST_KNN_VISITED + so] / nqd;
   return GI_OK;
 }
 

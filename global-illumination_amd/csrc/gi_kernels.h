@@ -35,7 +35,11 @@ struct QShade {
 
 enum {
   ST_RAY = 0, ST_SHADOW, ST_MONTE, ST_TRANS, ST_SPEC, ST_INDIRECT, ST_CAUSTIC,
-  ST_KNN, ST_KNN_PHOTONS, ST_KNN_VISITED, ST_COUNT = 16
+  ST_KNN, ST_KNN_PHOTONS, ST_KNN_VISITED,        // global map (caustic map: + ST_KNN_MAP)
+  ST_KNN_C, ST_KNN_C_PHOTONS, ST_KNN_C_VISITED,
+  ST_COUNT = 16
+};
+enum { ST_KNN_MAP = ST_KNN_C - ST_KNN
 };
 
 struct RenderArgs {
@@ -70,6 +74,27 @@ struct RenderArgs {
   unsigned long long *stats;
 };
 
+// kd node record (KdView::nodes): lo = {min xyz, split}, hi = {max xyz, axis bits}
+struct KdNode {
+  float4 lo, hi;
+};
+
+// squared distance from q to a node's tight box, evaluated with the same fp32 operation
+// sequence as the photon metric (d2 = fma(dz,dz, fma(dy,dy, dx*dx))): every rounding step is
+// monotone, so box_d2 <= metric d2 of every photon inside the box -- pruning on
+// box_d2 > bound never drops a photon the exact search would keep.
+__device__ __forceinline__ float kd_box_d2(const float4 &lo, const float4 &hi, float qx, float qy,
+                                           float qz) {
+  float gx = fmaxf(fmaxf(lo.x - qx, qx - hi.x), 0.0f);
+  float gy = fmaxf(fmaxf(lo.y - qy, qy - hi.y), 0.0f);
+  float gz = fmaxf(fmaxf(lo.z - qz, qz - hi.z), 0.0f);
+  return __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, __fmul_rn(gx, gx)));
+}
+
+__device__ __forceinline__ float kd_axis_q(int axis, float qx, float qy, float qz) {
+  return (axis == 0) ? qx : ((axis == 1) ? qy : qz);
+}
+
 // wave-level counter reduction (one atomic per wave)
 __device__ __forceinline__ void wave_add(unsigned long long *dst, uint64_t v) {
 #pragma unroll
@@ -91,7 +116,7 @@ struct KnnArgs {
   int32_t K;
   int32_t filter;
   int32_t mode;
-  int32_t pad;
+  int32_t stat_off;        // 0 (global map) or ST_KNN_MAP (caustic map)
   float r2f;               // (float)(r*r) accept radius
   double rmax;
   double fa, fb, fk;       // FILTER_CONST_A/B/K

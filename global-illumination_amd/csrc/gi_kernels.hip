@@ -464,7 +464,27 @@ __device__ __forceinline__ float metric_d2(float qx, float qy, float qz, float4 
   return __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
 }
 
+// Stackless backtrack: move to the far sibling of the deepest near child on the path from
+// the root to `node`; false when the walk is complete.
+__device__ __forceinline__ bool kd_next(const KdNode *nodes, int &node, float qx, float qy,
+                                        float qz) {
+  while (node != 1) {
+    const KdNode &pn = nodes[node >> 1];
+    float q = kd_axis_q(__float_as_int(pn.hi.w), qx, qy, qz);
+    int near_is_right = (q - pn.lo.w >= 0.0f) ? 1 : 0;
+    if ((node & 1) == near_is_right) break;
+    node >>= 1;
+  }
+  if (node == 1) return false;
+  node ^= 1;
+  return true;
+}
+
 // Find the K best photons of query (qx,qy,qz) within r2; returns heap size.
+// "While-while" structure: each lane walks internal nodes until it holds its next leaf
+// (or finishes); only then does the wave run the leaf loop, for all lanes at once. A single
+// loop mixing descend and leaf steps would re-run the 64-photon leaf loop whenever any one
+// lane reached a leaf (measured ~15x instruction overhead from divergence).
 __device__ __forceinline__ int knn_search(const KdView &M, float qx, float qy, float qz, float r2,
                                           int K, HeapRef h, uint32_t &visited) {
   int size = 0;
@@ -472,57 +492,56 @@ __device__ __forceinline__ int knn_search(const KdView &M, float qx, float qy, f
   float topd = 0.f;
   int topi = 0;
   if (M.n == 0) return 0;
-  const float2 *nodes = reinterpret_cast<const float2 *>(M.nodes);
+  const KdNode *nodes = reinterpret_cast<const KdNode *>(M.nodes);
   const float4 *pos = reinterpret_cast<const float4 *>(M.pos4);
   const int L = M.nleaves;
   int node = 1;
-  bool done = false;
-  while (!done) {
-    // descend to the near leaf
-    while (node < L) {
-      float2 nd = nodes[node];
-      int axis = __float_as_int(nd.y);
-      float q = (axis == 0) ? qx : ((axis == 1) ? qy : qz);
-      node = 2 * node + ((q - nd.x >= 0.0f) ? 1 : 0);
+  bool live = true;
+  while (true) {
+    // walk to the next leaf whose tight box is within the current bound
+    int leaf = -1;
+    while (live) {
+      KdNode nd = nodes[node];
+      if (kd_box_d2(nd.lo, nd.hi, qx, qy, qz) <= maxd2) {
+        if (node < L) {
+          float q = kd_axis_q(__float_as_int(nd.hi.w), qx, qy, qz);
+          node = 2 * node + ((q - nd.lo.w >= 0.0f) ? 1 : 0);
+          continue;
+        }
+        leaf = node - L;
+        break;
+      }
+      live = kd_next(nodes, node, qx, qy, qz);
     }
-    int leaf = node - L;
+    if (leaf < 0) break;
     int64_t s0 = ((int64_t)leaf * M.n) / L, s1 = ((int64_t)(leaf + 1) * M.n) / L;
-    for (int64_t ii = s0; ii < s1; ii++) {
-      float4 p = pos[ii];
-      float d2 = metric_d2(qx, qy, qz, p);
-      if (d2 <= maxd2) {
-        int id = (int)ii;
-        if (size < K) {
-          heap_push(h, size, d2, id);
-          if (size == K) {
+    for (int64_t ii = s0; ii < s1; ii += 4) {
+      float4 p[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) p[u] = pos[(ii + u < s1) ? ii + u : s1 - 1];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        float d2 = metric_d2(qx, qy, qz, p[u]);
+        if (ii + u < s1 && d2 <= maxd2) {
+          int id = (int)(ii + u);
+          if (size < K) {
+            heap_push(h, size, d2, id);
+            if (size == K) {
+              topd = h.d2[0];
+              topi = h.idx[0];
+              maxd2 = topd;
+            }
+          } else if (heap_less(d2, id, topd, topi)) {
+            heap_replace_top(h, size, d2, id);
             topd = h.d2[0];
             topi = h.idx[0];
             maxd2 = topd;
           }
-        } else if (heap_less(d2, id, topd, topi)) {
-          heap_replace_top(h, size, d2, id);
-          topd = h.d2[0];
-          topi = h.idx[0];
-          maxd2 = topd;
         }
       }
     }
     visited += (uint32_t)(s1 - s0);
-    // backtrack to the nearest unvisited far child that may hold candidates
-    while (true) {
-      if (node == 1) { done = true; break; }
-      int parent = node >> 1;
-      float2 nd = nodes[parent];
-      int axis = __float_as_int(nd.y);
-      float q = (axis == 0) ? qx : ((axis == 1) ? qy : qz);
-      float diff = q - nd.x;
-      int near_is_right = (diff >= 0.0f) ? 1 : 0;
-      if ((node & 1) == near_is_right && __fmul_rn(diff, diff) <= maxd2) {
-        node ^= 1;  // far sibling
-        break;
-      }
-      node = parent;
-    }
+    live = kd_next(nodes, node, qx, qy, qz);
   }
   return size;
 }
@@ -657,9 +676,9 @@ __global__ __launch_bounds__(64) void knn_kernel(KnnArgs a) {
     }
   }
   if (a.stats) {
-    wave_add(&a.stats[ST_KNN], nq_done);
-    wave_add(&a.stats[ST_KNN_PHOTONS], nfound_total);
-    wave_add(&a.stats[ST_KNN_VISITED], visited_total);
+    wave_add(&a.stats[ST_KNN + a.stat_off], nq_done);
+    wave_add(&a.stats[ST_KNN_PHOTONS + a.stat_off], nfound_total);
+    wave_add(&a.stats[ST_KNN_VISITED + a.stat_off], visited_total);
   }
 }
 
@@ -678,7 +697,7 @@ __global__ __launch_bounds__(64) void cached_kernel(KnnArgs a) {
     double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
     double out0 = 0, out1 = 0, out2 = 0;
     double closest = 0;
-    const float2 *nodes = reinterpret_cast<const float2 *>(a.map.nodes);
+    const KdNode *nodes = reinterpret_cast<const KdNode *>(a.map.nodes);
     const float4 *pos = reinterpret_cast<const float4 *>(a.map.pos4);
     const int L = a.map.nleaves;
     for (int guard = 0; guard < 1 << 20 && a.map.n > 0; guard++) {
@@ -687,37 +706,33 @@ __global__ __launch_bounds__(64) void cached_kernel(KnnArgs a) {
       float best2 = a.r2f;
       int best = -1;
       int node = 1;
-      bool done = false;
-      while (!done) {
-        while (node < L) {
-          float2 nd = nodes[node];
-          int axis = __float_as_int(nd.y);
-          float qq = (axis == 0) ? qp.x : ((axis == 1) ? qp.y : qp.z);
-          node = 2 * node + ((qq - nd.x >= 0.0f) ? 1 : 0);
-        }
-        int leaf = node - L;
-        int64_t s0 = ((int64_t)leaf * a.map.n) / L, s1 = ((int64_t)(leaf + 1) * a.map.n) / L;
-        for (int64_t ii = s0; ii < s1; ii++) {
-          float d2 = metric_d2(qp.x, qp.y, qp.z, pos[ii]);
-          if (d2 >= min2 && d2 <= best2 && (d2 < best2 || best < 0 || (int)ii < best)) {
-            best2 = d2;
-            best = (int)ii;
+      while (true) {
+        KdNode nd = nodes[node];
+        if (kd_box_d2(nd.lo, nd.hi, qp.x, qp.y, qp.z) <= best2) {
+          if (node < L) {
+            float qq = kd_axis_q(__float_as_int(nd.hi.w), qp.x, qp.y, qp.z);
+            node = 2 * node + ((qq - nd.lo.w >= 0.0f) ? 1 : 0);
+            continue;
+          }
+          int leaf = node - L;
+          int64_t s0 = ((int64_t)leaf * a.map.n) / L, s1 = ((int64_t)(leaf + 1) * a.map.n) / L;
+          for (int64_t ii = s0; ii < s1; ii++) {
+            float d2 = metric_d2(qp.x, qp.y, qp.z, pos[ii]);
+            if (d2 >= min2 && d2 <= best2 && (d2 < best2 || best < 0 || (int)ii < best)) {
+              best2 = d2;
+              best = (int)ii;
+            }
           }
         }
-        while (true) {
-          if (node == 1) { done = true; break; }
-          int parent = node >> 1;
-          float2 nd = nodes[parent];
-          int axis = __float_as_int(nd.y);
-          float qq = (axis == 0) ? qp.x : ((axis == 1) ? qp.y : qp.z);
-          float diff = qq - nd.x;
-          int near_is_right = (diff >= 0.0f) ? 1 : 0;
-          if ((node & 1) == near_is_right && __fmul_rn(diff, diff) <= best2) {
-            node ^= 1;
-            break;
-          }
-          node = parent;
+        while (node != 1) {
+          const KdNode &pn = nodes[node >> 1];
+          float qq = kd_axis_q(__float_as_int(pn.hi.w), qp.x, qp.y, qp.z);
+          int near_is_right = (qq - pn.lo.w >= 0.0f) ? 1 : 0;
+          if ((node & 1) == near_is_right) break;
+          node >>= 1;
         }
+        if (node == 1) break;
+        node ^= 1;
       }
       closest = sqrt((double)best2);
       if (best < 0) break;
@@ -747,7 +762,7 @@ __global__ __launch_bounds__(64) void cached_kernel(KnnArgs a) {
     a.out[3 * q + 1] = out1;
     a.out[3 * q + 2] = out2;
   }
-  if (a.stats) wave_add(&a.stats[ST_KNN], nq_done);
+  if (a.stats) wave_add(&a.stats[ST_KNN + a.stat_off], nq_done);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -71,7 +71,7 @@ template <int CAP>
 __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
   __shared__ uint64_t buf[CAP];
   const int lane = threadIdx.x;
-  const float2 *nodes = reinterpret_cast<const float2 *>(a.map.nodes);
+  const KdNode *nodes = reinterpret_cast<const KdNode *>(a.map.nodes);
   const float4 *pos = reinterpret_cast<const float4 *>(a.map.pos4);
   const int L = a.map.nleaves;
   const int64_t N = a.map.n;
@@ -88,60 +88,55 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
     uint32_t visited = 0;
     if (N > 0) {
       int node = 1;
-      bool done = false;
-      while (!done) {
-        while (node < L) {
-          float2 nd = nodes[node];
-          int axis = __float_as_int(nd.y);
-          float q = (axis == 0) ? qx : ((axis == 1) ? qy : qz);
-          node = 2 * node + ((q - nd.x >= 0.0f) ? 1 : 0);
-        }
-        int leaf = node - L;
-        int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
-        visited += (uint32_t)(s1 - s0);
-        for (int64_t base = s0; base < s1; base += 64) {
-          int64_t ii = base + lane;
-          uint64_t key = ~0ull;
-          if (ii < s1) {
-            float4 p = pos[ii];
-            float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
-            float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
-            key = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)(uint32_t)ii;
-          }
-          bool pass = key < thr;
-          uint64_t m = __ballot(pass);
-          uint32_t nnew = (uint32_t)__popcll(m);
-          if (nnew == 0) continue;
-          if (count + nnew > (uint32_t)CAP) {
-            select_k<CAP>(buf, lane, count, K, thr);
-            pass = key < thr;
-            m = __ballot(pass);
-            nnew = (uint32_t)__popcll(m);
-            if (nnew == 0) continue;
-          }
-          if (pass) {
-            uint32_t off = count + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-            buf[off] = key;
-          }
-          count += nnew;
-          __syncthreads();
-        }
-        // prune with the current threshold's distance (a bound on the K-th distance)
+      while (true) {
+        KdNode nd = nodes[node];
         float pr = __uint_as_float((uint32_t)((thr - 1ull) >> 32));
-        while (true) {
-          if (node == 1) { done = true; break; }
-          int parent = node >> 1;
-          float2 nd = nodes[parent];
-          int axis = __float_as_int(nd.y);
-          float q = (axis == 0) ? qx : ((axis == 1) ? qy : qz);
-          float diff = q - nd.x;
-          int near_is_right = (diff >= 0.0f) ? 1 : 0;
-          if ((node & 1) == near_is_right && __fmul_rn(diff, diff) <= pr) {
-            node ^= 1;
-            break;
+        if (kd_box_d2(nd.lo, nd.hi, qx, qy, qz) <= pr) {
+          if (node < L) {
+            float q = kd_axis_q(__float_as_int(nd.hi.w), qx, qy, qz);
+            node = 2 * node + ((q - nd.lo.w >= 0.0f) ? 1 : 0);
+            continue;
           }
-          node = parent;
+          int leaf = node - L;
+          int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
+          visited += (uint32_t)(s1 - s0);
+          for (int64_t base = s0; base < s1; base += 64) {
+            int64_t ii = base + lane;
+            uint64_t key = ~0ull;
+            if (ii < s1) {
+              float4 p = pos[ii];
+              float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
+              float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
+              key = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)(uint32_t)ii;
+            }
+            bool pass = key < thr;
+            uint64_t m = __ballot(pass);
+            uint32_t nnew = (uint32_t)__popcll(m);
+            if (nnew == 0) continue;
+            if (count + nnew > (uint32_t)CAP) {
+              select_k<CAP>(buf, lane, count, K, thr);
+              pass = key < thr;
+              m = __ballot(pass);
+              nnew = (uint32_t)__popcll(m);
+              if (nnew == 0) continue;
+            }
+            if (pass) {
+              uint32_t off = count + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+              buf[off] = key;
+            }
+            count += nnew;
+            __syncthreads();
+          }
         }
+        while (node != 1) {
+          const KdNode &pn = nodes[node >> 1];
+          float q = kd_axis_q(__float_as_int(pn.hi.w), qx, qy, qz);
+          int near_is_right = (q - pn.lo.w >= 0.0f) ? 1 : 0;
+          if ((node & 1) == near_is_right) break;
+          node >>= 1;
+        }
+        if (node == 1) break;
+        node ^= 1;
       }
     }
     // exact K best
@@ -272,9 +267,9 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
     __syncthreads();
   }
   if (a.stats && lane == 0) {
-    if (st_q) atomicAdd(&a.stats[ST_KNN], (unsigned long long)st_q);
-    if (st_found) atomicAdd(&a.stats[ST_KNN_PHOTONS], (unsigned long long)st_found);
-    if (st_vis) atomicAdd(&a.stats[ST_KNN_VISITED], (unsigned long long)st_vis);
+    if (st_q) atomicAdd(&a.stats[ST_KNN + a.stat_off], (unsigned long long)st_q);
+    if (st_found) atomicAdd(&a.stats[ST_KNN_PHOTONS + a.stat_off], (unsigned long long)st_found);
+    if (st_vis) atomicAdd(&a.stats[ST_KNN_VISITED + a.stat_off], (unsigned long long)st_vis);
   }
 }
 
@@ -328,7 +323,7 @@ __global__ __launch_bounds__(64) void knn_packet_kernel(KnnArgs a) {
   extern __shared__ uint64_t hs[];
   const int lane = threadIdx.x;
   uint64_t *h = hs + lane;
-  const float2 *nodes = reinterpret_cast<const float2 *>(a.map.nodes);
+  const KdNode *nodes = reinterpret_cast<const KdNode *>(a.map.nodes);
   const float4 *pos = reinterpret_cast<const float4 *>(a.map.pos4);
   const int L = a.map.nleaves;
   const int64_t N = a.map.n;
@@ -351,63 +346,56 @@ __global__ __launch_bounds__(64) void knn_packet_kernel(KnnArgs a) {
   if (N > 0 && K > 0) {
     int node = 1;
     while (true) {
-      // descend: majority side first
-      while (node < L) {
-        float2 nd = nodes[node];
-        int axis = __float_as_int(nd.y);
-        float qa = (axis == 0) ? qp.x : ((axis == 1) ? qp.y : qp.z);
-        int nr = __popcll(__ballot(valid && qa - nd.x >= 0.0f));
-        node = 2 * node + ((2 * nr > nvalid) ? 1 : 0);
-      }
-      int leaf = node - L;
-      int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
-      visited += (uint32_t)(s1 - s0);
-      for (int64_t b = s0; b < s1; b += 64) {
-        int cnt = (int)((s1 - b) < 64 ? (s1 - b) : 64);
-        float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (lane < cnt) p = pos[b + lane];
-        for (int j = 0; j < cnt; j++) {
-          float px = rlane(p.x, j), py = rlane(p.y, j), pz = rlane(p.z, j);
-          float dx = qp.x - px, dy = qp.y - py, dz = qp.z - pz;
-          float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
-          if (d2 <= pr) {
-            uint64_t key = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)(uint32_t)(b + j);
-            if (key < thr) {
-              if (size < K) {
-                kheap_push(h, size, key);
-                size++;
-                if (size == K) thr = h[0];
-              } else {
-                kheap_replace_top(h, size, key);
-                thr = h[0];
+      KdNode nd = nodes[node];
+      bool need = valid && kd_box_d2(nd.lo, nd.hi, qp.x, qp.y, qp.z) <= pr;
+      if (__ballot(need)) {
+        if (node < L) {
+          // descend: the side holding the majority of the packet first
+          float qa = kd_axis_q(__float_as_int(nd.hi.w), qp.x, qp.y, qp.z);
+          int nr = __popcll(__ballot(valid && qa - nd.lo.w >= 0.0f));
+          node = 2 * node + ((2 * nr > nvalid) ? 1 : 0);
+          continue;
+        }
+        int leaf = node - L;
+        int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
+        visited += (uint32_t)(s1 - s0);
+        for (int64_t b = s0; b < s1; b += 64) {
+          int cnt = (int)((s1 - b) < 64 ? (s1 - b) : 64);
+          float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (lane < cnt) p = pos[b + lane];
+          if (!need) continue;
+          for (int j = 0; j < cnt; j++) {
+            float px = rlane(p.x, j), py = rlane(p.y, j), pz = rlane(p.z, j);
+            float dx = qp.x - px, dy = qp.y - py, dz = qp.z - pz;
+            float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
+            if (d2 <= pr) {
+              uint64_t key = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)(uint32_t)(b + j);
+              if (key < thr) {
+                if (size < K) {
+                  kheap_push(h, size, key);
+                  size++;
+                  if (size == K) thr = h[0];
+                } else {
+                  kheap_replace_top(h, size, key);
+                  thr = h[0];
+                }
+                if (size == K) pr = __uint_as_float((uint32_t)(thr >> 32));
               }
-              if (size == K) pr = __uint_as_float((uint32_t)(thr >> 32));
             }
           }
         }
       }
-      // backtrack to the deepest first-visited child whose sibling some lane still needs
-      bool done = false;
-      while (true) {
-        if (node == 1) { done = true; break; }
-        int parent = node >> 1;
-        float2 nd = nodes[parent];
-        int axis = __float_as_int(nd.y);
-        float qa = (axis == 0) ? qp.x : ((axis == 1) ? qp.y : qp.z);
-        float diff = qa - nd.x;
-        bool right = diff >= 0.0f;
-        int nr = __popcll(__ballot(valid && right));
+      // backtrack: first-visited child whose sibling is unvisited (majority rule recomputed)
+      while (node != 1) {
+        const KdNode &pn = nodes[node >> 1];
+        float qa = kd_axis_q(__float_as_int(pn.hi.w), qp.x, qp.y, qp.z);
+        int nr = __popcll(__ballot(valid && qa - pn.lo.w >= 0.0f));
         int first = (2 * nr > nvalid) ? 1 : 0;
-        if ((node & 1) == first) {
-          bool need = valid && (((int)right != first) || __fmul_rn(diff, diff) <= pr);
-          if (__ballot(need)) {
-            node ^= 1;
-            break;
-          }
-        }
-        node = parent;
+        if ((node & 1) == first) break;
+        node >>= 1;
       }
-      if (done) break;
+      if (node == 1) break;
+      node ^= 1;
     }
   }
   int num = size;
@@ -517,9 +505,9 @@ __global__ __launch_bounds__(64) void knn_packet_kernel(KnnArgs a) {
   if (a.stats) {
     uint64_t nq_done = valid ? 1 : 0, found = valid ? (uint64_t)num : 0,
              vis = valid ? (uint64_t)visited : 0;
-    wave_add(&a.stats[ST_KNN], nq_done);
-    wave_add(&a.stats[ST_KNN_PHOTONS], found);
-    wave_add(&a.stats[ST_KNN_VISITED], vis);
+    wave_add(&a.stats[ST_KNN + a.stat_off], nq_done);
+    wave_add(&a.stats[ST_KNN_PHOTONS + a.stat_off], found);
+    wave_add(&a.stats[ST_KNN_VISITED + a.stat_off], vis);
   }
 }
 

@@ -97,7 +97,8 @@ struct DCamera {
 struct KdView {
   const float *pos4;       // float4
   const uint32_t *rgbe;
-  const float *nodes;      // float2 per node (index 0 unused)
+  const float *nodes;      // 2 x float4 per node (index 0 unused): {lo.xyz, split},
+                           // {hi.xyz, axis bits}; nodes [L, 2L) are the leaves
   int64_t n;
   int32_t nleaves;
   int32_t levels;

@@ -69,7 +69,18 @@ class RenderStats(C.Structure):
         "screen_rays", "shadow_rays", "monte_carlo_rays", "transmissive_samples",
         "specular_samples", "indirect_samples", "caustic_samples", "knn_queries",
         "knn_photons", "knn_visited")] + [("render_s", C.c_double), ("knn_kernel_ms", C.c_double),
-                           ("knn_kernel_launches", C.c_double)]
+                           ("knn_kernel_launches", C.c_double)] + [
+        ("knn_map_queries", C.c_uint64 * 2), ("knn_map_photons", C.c_uint64 * 2),
+        ("knn_map_visited", C.c_uint64 * 2), ("knn_map_kernel_ms", C.c_double * 2),
+        ("knn_map_launches", C.c_double * 2)]
+
+
+def _stats_dict(st):
+    out = {}
+    for f, _ in type(st)._fields_:
+        v = getattr(st, f)
+        out[f] = list(v) if isinstance(v, C.Array) else v
+    return out
 
 
 _lib = None
@@ -207,7 +218,7 @@ class Renderer:
         self._check(lib().gi_render_image(self._ctx, aa, width, height, rgb.ctypes.data,
                                           rgbf.ctypes.data if want_float else None,
                                           C.byref(st)))
-        stats = {f: getattr(st, f) for f, _ in RenderStats._fields_}
+        stats = _stats_dict(st)
         return (rgb, rgbf, stats) if want_float else (rgb, stats)
 
     def render_tiles(self, aa, width, height, tile, shard, nshards, rgbf=None):
@@ -216,7 +227,7 @@ class Renderer:
         st = RenderStats()
         self._check(lib().gi_render_tiles(self._ctx, aa, width, height, tile, shard, nshards,
                                           rgbf.ctypes.data, C.byref(st)))
-        return rgbf, {f: getattr(st, f) for f, _ in RenderStats._fields_}
+        return rgbf, _stats_dict(st)
 
     def EstimateRadiance(self, which, queries):
         q = np.ascontiguousarray(queries, dtype=QUERY_DTYPE)

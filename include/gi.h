@@ -136,6 +136,9 @@ typedef struct gi_render_stats {
   double render_s;                     /* wall time of the render phase       */
   double knn_kernel_ms;                /* summed k-NN kernel time (HIP events) */
   double knn_kernel_launches;
+  /* the same split per photon map (0 = global, 1 = caustic) */
+  uint64_t knn_map_queries[2], knn_map_photons[2], knn_map_visited[2];
+  double knn_map_kernel_ms[2], knn_map_launches[2];
 } gi_render_stats;
 
 typedef struct gi_ctx gi_ctx;

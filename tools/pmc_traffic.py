@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch of one kernel from a rocprofv3 `--pmc FETCH_SIZE` pass.
+
+FETCH_SIZE is reported in KiB (rocprofv3 counter description). MI355X_MICROARCH.md (HBM
+section): on gfx950 FETCH_SIZE reports 1/2 of the bytes actually read -> bytes = 2 * 1024 * KiB.
+Writes profiles/knn_traffic.json, read by bench.py for roofline.traffic when the workload
+matches.
+
+usage: pmc_traffic.py <counter_collection.csv> <kernel-substring> <res> <aa> <global> <caustic>
+"""
+import csv
+import json
+import os
+import sys
+
+
+def main():
+    path, kname = sys.argv[1], sys.argv[2]
+    res, aa, glob, caus = (int(x) for x in sys.argv[3:7])
+    per = {}
+    for r in csv.DictReader(open(path)):
+        if kname not in r["Kernel_Name"] or r["Counter_Name"] != "FETCH_SIZE":
+            continue
+        per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    if not per:
+        sys.exit(f"no FETCH_SIZE rows for {kname!r} in {path}")
+    kib = sum(per.values()) / len(per)
+    out = {"kernel": kname, "dispatches": len(per), "fetch_size_kib_per_launch": kib,
+           "correction": "x2 (gfx950 FETCH_SIZE = 1/2 of bytes read, MI355X_MICROARCH.md) x1024",
+           "bytes_per_launch": kib * 1024 * 2,
+           "workload": {"res": res, "aa": aa, "global": glob, "caustic": caus},
+           "source": os.path.relpath(path)}
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "profiles", "knn_traffic.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -133,7 +133,7 @@ GI_HD bool box_contains(const double *mn, const double *mx, V p) {  // R3Cont.cp
 }
 
 // R3Intersects(ray, box), R3Isect.cpp:883-942
-__device__ __noinline__ bool ray_box(V o, V d, const double *mn, const double *mx, double *t_out,
+__device__ __forceinline__ bool ray_box(V o, V d, const double *mn, const double *mx, double *t_out,
                                      V *n_out) {
   if (mn[0] > mx[0] || mn[1] > mx[1] || mn[2] > mx[2]) return false;
   bool inside = box_contains(mn, mx, o);
@@ -227,7 +227,7 @@ GI_HD bool ray_circle(V o, V d, V c, V n, double r, double &t, V &p) {
 
 // R3Shape::Intersects dispatch (R3Shape.cpp:328-329); SK_MESH is R3Intersects(ray,
 // R3TriangleArray) (R3Isect.cpp:800-833): min t over ALL triangles, t >= -1e-6 allowed (Q2).
-__device__ __noinline__ bool shape_intersect(const SceneView &S, const DShape &sh, V o, V d,
+__device__ __forceinline__ bool shape_intersect(const SceneView &S, const DShape &sh, V o, V d,
                                              double &t, V &p, V &n) {
   switch (sh.kind) {
     case SK_TRI: {
@@ -296,7 +296,9 @@ struct Hit {
 // visited in the graph's pre-order; an element "hits" only if it strictly improves on the
 // current closest t (its "closest_t == max_t -> FALSE" rule), so earlier elements win ties.
 // Ray direction is renormalised per graph level (R3Line::InverseTransform, R3Line.cpp:140).
-__device__ __noinline__ bool scene_intersect(const SceneView &S, V org, V dir, Hit &h) {
+// Inlined at every call site: node/element/shape records are wave-uniform (scalar loads) and
+// the root-first transform chain is precomputed per node, so nothing lives in scratch.
+__device__ __forceinline__ bool scene_intersect(const SceneView &S, V org, V dir, Hit &h) {
   double closest = kInf;  // world-frame t (rigid transforms keep t; scale handled below)
   bool found = false;
   V hp = mk(0, 0, 0), hn = mk(0, 0, 0);
@@ -304,15 +306,12 @@ __device__ __noinline__ bool scene_intersect(const SceneView &S, V org, V dir, H
   for (int ni = 0; ni < S.nnodes; ni++) {
     const DNode &nd = S.nodes[ni];
     if (nd.elem_count == 0) continue;
-    // local ray: walk the parent chain (depth is tiny in .scn files)
-    int chain[8];
-    int depth = 0;
-    for (int c = ni; c >= 0 && depth < 8; c = S.nodes[c].parent) chain[depth++] = c;
+    // local ray: apply the chain root -> node
     V lo = org, ldir = dir;
     double scale = 1.0;
     bool ok = true;
-    for (int k = depth - 1; k >= 0; k--) {
-      const DNode &a = S.nodes[chain[k]];
+    for (int k = 0; k < nd.depth; k++) {
+      const DNode &a = S.nodes[nd.chain[k]];
       double lv;
       if (a.identity) {
         lv = len(ldir);

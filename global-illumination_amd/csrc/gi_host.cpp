@@ -207,7 +207,7 @@ struct gi_ctx {
   bool map_valid[2] = {false, false};
   int leaf_size = 16;
   // render scratch
-  DBuf spawn, npaths, path_off, base, pixels, rgbf, rgb8, gheap_d2, gheap_idx, qcount, stats_bak;
+  DBuf spawn, npaths, path_off, nmc, mc_off, nind, ind_off, base, pixels, rgbf, rgb8, gheap_d2, gheap_idx, qcount, stats_bak;
   DBuf qpos[2], qshade[2], qkey[2], qout[2];
   size_t qcap_hint[2] = {0, 0};
   KeySortScratch keysort[2];
@@ -576,18 +576,35 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     HIPCHK(c, c->spawn.ensure((size_t)nprim * sizeof(Spawn)));
     HIPCHK(c, c->npaths.ensure((size_t)nprim * 4));
     HIPCHK(c, c->path_off.ensure((size_t)(nprim + 1) * 4));
+    HIPCHK(c, c->nmc.ensure((size_t)nprim * 4));
+    HIPCHK(c, c->mc_off.ensure((size_t)(nprim + 1) * 4));
+    HIPCHK(c, c->nind.ensure((size_t)nprim * 4));
+    HIPCHK(c, c->ind_off.ensure((size_t)(nprim + 1) * 4));
     a.spawn = c->spawn.as<Spawn>();
     a.npaths = c->npaths.as<uint32_t>();
+    a.nmc = c->nmc.as<uint32_t>();
+    a.nind = c->nind.as<uint32_t>();
     a.path_off = c->path_off.as<uint32_t>();
+    a.mc_off = c->mc_off.as<uint32_t>();
+    a.ind_off = c->ind_off.as<uint32_t>();
     launch_primary(a, c->stream);
     HIPCHK(c, hipGetLastError());
     ScanTemp t = scan_temp(c, nprim);
     HIPCHK(c, launch_scan(a.npaths, c->path_off.as<uint32_t>(), nprim, t, c->stream));
-    uint32_t total_paths = 0;
-    HIPCHK(c, hipMemcpyAsync(&total_paths, c->path_off.as<uint32_t>() + nprim, 4,
+    HIPCHK(c, launch_scan(a.nmc, c->mc_off.as<uint32_t>(), nprim, t, c->stream));
+    HIPCHK(c, launch_scan(a.nind, c->ind_off.as<uint32_t>(), nprim, t, c->stream));
+    uint32_t totals[3] = {0, 0, 0};
+    HIPCHK(c, hipMemcpyAsync(&totals[0], c->path_off.as<uint32_t>() + nprim, 4,
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&totals[1], c->mc_off.as<uint32_t>() + nprim, 4,
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&totals[2], c->ind_off.as<uint32_t>() + nprim, 4,
                              hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    uint32_t total_paths = totals[0];
     a.total_paths = total_paths;
+    a.total_mc = totals[1];
+    a.total_ind = totals[2];
     HIPCHK(c, c->base.ensure((size_t)total_paths * 24));
     a.base = c->base.as<double>();
     // single Monte Carlo pass; grow the query lists and re-run on overflow
@@ -660,6 +677,8 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
 
 int check_ready(gi_ctx *c) {
   if (!c->have_scene) return fail(c, GI_ERR_STATE, "no scene loaded (gi_read_scene)");
+  if (c->scene.unsupported_depth)
+    return fail(c, GI_ERR_UNSUPPORTED, "scene graph deeper than 16 levels");
   if (c->scene.unsupported_shapes)
     return fail(c, GI_ERR_UNSUPPORTED,
                 "scene contains cylinder/cone/line shapes: not yet on the device path");

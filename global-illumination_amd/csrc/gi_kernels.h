@@ -54,8 +54,13 @@ struct RenderArgs {
   int64_t nprim;        // npix * af^2 * dof_test
   int64_t total_paths;
   Spawn *spawn;
-  uint32_t *npaths;     // [nprim]
-  const uint32_t *path_off;  // [nprim + 1]
+  uint32_t *npaths;     // [nprim] 1 + transmissive + specular + indirect paths
+  uint32_t *nmc;        // [nprim] transmissive + specular (Monte Carlo path) samples
+  uint32_t *nind;       // [nprim] indirect samples
+  const uint32_t *path_off;  // [nprim + 1] exclusive scans of the three counts
+  const uint32_t *mc_off;
+  const uint32_t *ind_off;
+  int64_t total_mc, total_ind;
   // query lists (0 = global map, 1 = caustic map): appended with an atomic counter; each
   // query carries key = path_slot << 20 | index-in-path so the per-pixel reduction can sum
   // them in a deterministic order after a key sort
@@ -151,7 +156,7 @@ struct ScanTemp {
 hipError_t launch_scan(const uint32_t *in, uint32_t *out, int64_t n, ScanTemp &tmp,
                        hipStream_t st);
 void launch_primary(const RenderArgs &a, hipStream_t st);
-void launch_path(const RenderArgs &a, hipStream_t st);
+void launch_path(const RenderArgs &a, hipStream_t st);  // slot0 + indirect + Monte Carlo
 void launch_reduce(const RenderArgs &a, hipStream_t st);
 void launch_knn(const KnnArgs &a, bool lds_heap, hipStream_t st);
 bool launch_knn_wave(const KnnArgs &a, hipStream_t st);

@@ -149,6 +149,8 @@ __global__ __launch_bounds__(256) void primary_kernel(RenderArgs a) {
     }
     a.spawn[b] = sp;
     a.npaths[b] = 1u + (uint32_t)(sp.n_t + sp.n_s + sp.n_i);
+    a.nmc[b] = (uint32_t)(sp.n_t + sp.n_s);
+    a.nind[b] = (uint32_t)sp.n_i;
     c_shadow = cnt.shadow;
   }
   wave_add(&a.stats[ST_RAY], c_ray);
@@ -200,7 +202,7 @@ __device__ __forceinline__ void global_query(PathCtx &P, V p, V n, V ex, double 
 }
 
 // MonteCarlo_IndirectSample, montecarlo.cpp:177-305 (W = outer weight of this path)
-__device__ __noinline__ void mc_indirect(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
+__device__ __forceinline__ void mc_indirect_body(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
   const SceneView &S = *P.S;
   const Flags &F = *P.F;
   C3 tw = rgb(1, 1, 1);
@@ -246,6 +248,10 @@ __device__ __noinline__ void mc_indirect(PathCtx &P, V org, V dir, Rng &rng, C3 
     org = ray_start;
     dir = sb;
   }
+}
+
+__device__ __noinline__ void mc_indirect(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
+  mc_indirect_body(P, org, dir, rng, W);
 }
 
 // MonteCarlo_PathTrace, montecarlo.cpp:16-171
@@ -320,89 +326,139 @@ __device__ __noinline__ void mc_path(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
   }
 }
 
-// Expand path slot g of the batch: slot 0 of a primary sample = its own photon-map queries
-// (CausticIllumination / EstimateGlobalIllumination at the primary hit) and base colour;
-// slots 1.. = transmissive, specular and indirect sample paths (raytracer.cpp:47-135).
-__global__ __launch_bounds__(128) void path_kernel(RenderArgs a) {
-  int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  Counts cnt = {0, 0, 0, 0, 0, 0};
-  if (g < a.total_paths) {
-    // primary sample owning this slot: last p with path_off[p] <= g
-    int64_t lo = 0, hi = a.nprim;
-    while (hi - lo > 1) {
-      int64_t mid = (lo + hi) >> 1;
-      if ((int64_t)a.path_off[mid] <= g) lo = mid; else hi = mid;
-    }
-    int64_t pb = lo;
-    int slot = (int)(g - a.path_off[pb]);
-    const Spawn &sp = a.spawn[pb];
-    PathCtx P;
-    P.S = &a.S;
-    P.F = &a.F;
-    P.A = &a;
-    P.g = (uint64_t)g;
-    P.j = 0;
-    P.base = rgb(0, 0, 0);
-    P.cnt = cnt;
-    if (slot == 0) {
-      P.base = ldc(sp.base);
-      if (sp.hit) {
-        V p = ld3(sp.p), n = ld3(sp.n), view = ld3(sp.v);
-        V ex = reflective_bounce(n, view, sp.ct);
-        if (sp.q_caus) {
-          put_query(P, 1, p, n, ex, sp.ct, sp.mat, rgb(1, 1, 1));
-          P.cnt.caustic++;
-        }
-        if (sp.q_glob) put_query(P, 0, p, n, ex, sp.ct, sp.mat, rgb(1, 1, 1));
-      }
-    } else {
-      int pix, i, j, k;
-      uint64_t psample;
-      decode_primary(a, pb, pix, i, j, k, psample);
-      const SceneView &S = a.S;
-      const Flags &F = a.F;
-      const DMaterial &m = S.mats[sp.mat];
-      V p = ld3(sp.p), n = ld3(sp.n), view = ld3(sp.v);
-      double ct = sp.ct, R = sp.R;
-      int s = slot - 1;
-      Rng rng;
-      if (s < sp.n_t) {
-        // TransmissiveIllumination sample s (raytracer.cpp:47-77)
-        rng.init(F.seed, KIND_TRANS, psample, (uint64_t)s);
-        V ex = transmissive_bounce(F.ir_air, n, view, ct, m.ir);
-        C3 tw = (1.0 - R) * ldc(m.kt);
-        V sb = F.distrib_trans ? specular_sample(ex, m.n, ct, rng) : ex;
-        mc_path(P, p + sb * kEps, sb, rng, tw / (double)sp.n_t);
-        P.cnt.trans++;
-      } else if (s < sp.n_t + sp.n_s) {
-        // SpecularIllumination sample (raytracer.cpp:80-109)
-        s -= sp.n_t;
-        rng.init(F.seed, KIND_SPEC, psample, (uint64_t)s);
-        V ex = reflective_bounce(n, view, ct);
-        C3 tw = ldc(m.kt) * R + ldc(m.ks);
-        V sb = F.distrib_spec ? specular_sample(ex, m.n, ct, rng) : ex;
-        mc_path(P, p + sb * kEps, sb, rng, tw / (double)sp.n_s);
-        P.cnt.spec++;
-      } else {
-        // IndirectIllumination sample (raytracer.cpp:112-135)
-        s -= sp.n_t + sp.n_s;
-        rng.init(F.seed, KIND_IND, psample, (uint64_t)s);
-        V sb = diffuse_sample(n, ct, rng);
-        mc_indirect(P, p + sb * kEps, sb, rng, ldc(m.kd) / (double)sp.n_i);
-        P.cnt.indirect++;
-      }
-    }
-    a.base[3 * g] = P.base.r;
-    a.base[3 * g + 1] = P.base.g;
-    a.base[3 * g + 2] = P.base.b;
-    cnt = P.cnt;
+// last p in [0, n) with off[p] <= t (off is an exclusive scan, off[0] = 0)
+__device__ __forceinline__ int64_t scan_owner(const uint32_t *off, int64_t n, int64_t t) {
+  int64_t lo = 0, hi = n;
+  while (hi - lo > 1) {
+    int64_t mid = (lo + hi) >> 1;
+    if ((int64_t)off[mid] <= t) lo = mid; else hi = mid;
   }
+  return lo;
+}
+
+__device__ __forceinline__ void path_init(PathCtx &P, const RenderArgs &a, int64_t g) {
+  P.S = &a.S;
+  P.F = &a.F;
+  P.A = &a;
+  P.g = (uint64_t)g;
+  P.j = 0;
+  P.base = rgb(0, 0, 0);
+  Counts z = {0, 0, 0, 0, 0, 0};
+  P.cnt = z;
+}
+
+__device__ __forceinline__ void path_stats(const RenderArgs &a, const Counts &cnt) {
   wave_add(&a.stats[ST_SHADOW], cnt.shadow);
   wave_add(&a.stats[ST_MONTE], cnt.monte);
   wave_add(&a.stats[ST_TRANS], cnt.trans);
   wave_add(&a.stats[ST_SPEC], cnt.spec);
   wave_add(&a.stats[ST_INDIRECT], cnt.indirect);
   wave_add(&a.stats[ST_CAUSTIC], cnt.caustic);
+}
+
+// Path slots of primary sample p are [path_off[p], path_off[p+1]): slot 0 = the sample's own
+// photon-map queries (CausticIllumination / EstimateGlobalIllumination at the primary hit) and
+// base colour; then n_t transmissive, n_s specular and n_i indirect sample paths
+// (raytracer.cpp:47-135). The three kinds run as separate launches so the ~90 % of paths
+// that are indirect samples (one bounce to a diffuse hit, then a query) get a lean,
+// call-free kernel instead of the Monte Carlo megakernel's register footprint.
+__global__ __launch_bounds__(256) void slot0_kernel(RenderArgs a) {
+  int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  Counts cnt = {0, 0, 0, 0, 0, 0};
+  if (b < a.nprim) {
+    int64_t g = a.path_off[b];
+    const Spawn &sp = a.spawn[b];
+    PathCtx P;
+    path_init(P, a, g);
+    P.base = ldc(sp.base);
+    if (sp.hit) {
+      V p = ld3(sp.p), n = ld3(sp.n), view = ld3(sp.v);
+      V ex = reflective_bounce(n, view, sp.ct);
+      if (sp.q_caus) {
+        put_query(P, 1, p, n, ex, sp.ct, sp.mat, rgb(1, 1, 1));
+        P.cnt.caustic++;
+      }
+      if (sp.q_glob) put_query(P, 0, p, n, ex, sp.ct, sp.mat, rgb(1, 1, 1));
+    }
+    a.base[3 * g] = P.base.r;
+    a.base[3 * g + 1] = P.base.g;
+    a.base[3 * g + 2] = P.base.b;
+    cnt = P.cnt;
+  }
+  path_stats(a, cnt);
+}
+
+// IndirectIllumination sample s of primary pb (raytracer.cpp:112-135)
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void ind_kernel(RenderArgs a) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  Counts cnt = {0, 0, 0, 0, 0, 0};
+  if (t < a.total_ind) {
+    int64_t pb = scan_owner(a.ind_off, a.nprim, t);
+    int s = (int)(t - a.ind_off[pb]);
+    const Spawn &sp = a.spawn[pb];
+    int64_t g = (int64_t)a.path_off[pb] + 1 + sp.n_t + sp.n_s + s;
+    int pix, i, j, k;
+    uint64_t psample;
+    decode_primary(a, pb, pix, i, j, k, psample);
+    const DMaterial &m = a.S.mats[sp.mat];
+    PathCtx P;
+    path_init(P, a, g);
+    Rng rng;
+    rng.init(a.F.seed, KIND_IND, psample, (uint64_t)s);
+    V p = ld3(sp.p), n = ld3(sp.n);
+    V sb = diffuse_sample(n, sp.ct, rng);
+    mc_indirect_body(P, p + sb * kEps, sb, rng, ldc(m.kd) / (double)sp.n_i);
+    P.cnt.indirect++;
+    a.base[3 * g] = P.base.r;
+    a.base[3 * g + 1] = P.base.g;
+    a.base[3 * g + 2] = P.base.b;
+    cnt = P.cnt;
+  }
+  path_stats(a, cnt);
+}
+
+// TransmissiveIllumination / SpecularIllumination sample (raytracer.cpp:47-109)
+__global__ __launch_bounds__(128) void mc_kernel(RenderArgs a) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  Counts cnt = {0, 0, 0, 0, 0, 0};
+  if (t < a.total_mc) {
+    int64_t pb = scan_owner(a.mc_off, a.nprim, t);
+    int s = (int)(t - a.mc_off[pb]);
+    const Spawn &sp = a.spawn[pb];
+    int64_t g = (int64_t)a.path_off[pb] + 1 + s;
+    int pix, i, j, k;
+    uint64_t psample;
+    decode_primary(a, pb, pix, i, j, k, psample);
+    const SceneView &S = a.S;
+    const Flags &F = a.F;
+    const DMaterial &m = S.mats[sp.mat];
+    V p = ld3(sp.p), n = ld3(sp.n), view = ld3(sp.v);
+    double ct = sp.ct, R = sp.R;
+    PathCtx P;
+    path_init(P, a, g);
+    Rng rng;
+    if (s < sp.n_t) {
+      rng.init(F.seed, KIND_TRANS, psample, (uint64_t)s);
+      V ex = transmissive_bounce(F.ir_air, n, view, ct, m.ir);
+      C3 tw = (1.0 - R) * ldc(m.kt);
+      V sb = F.distrib_trans ? specular_sample(ex, m.n, ct, rng) : ex;
+      mc_path(P, p + sb * kEps, sb, rng, tw / (double)sp.n_t);
+      P.cnt.trans++;
+    } else {
+      s -= sp.n_t;
+      rng.init(F.seed, KIND_SPEC, psample, (uint64_t)s);
+      V ex = reflective_bounce(n, view, ct);
+      C3 tw = ldc(m.kt) * R + ldc(m.ks);
+      V sb = F.distrib_spec ? specular_sample(ex, m.n, ct, rng) : ex;
+      mc_path(P, p + sb * kEps, sb, rng, tw / (double)sp.n_s);
+      P.cnt.spec++;
+    }
+    a.base[3 * g] = P.base.r;
+    a.base[3 * g + 1] = P.base.g;
+    a.base[3 * g + 2] = P.base.b;
+    cnt = P.cnt;
+  }
+  path_stats(a, cnt);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1033,8 +1089,9 @@ void launch_primary(const RenderArgs &a, hipStream_t st) {
   primary_kernel<<<nblk(a.nprim, 256), 256, 0, st>>>(a);
 }
 void launch_path(const RenderArgs &a, hipStream_t st) {
-  if (a.total_paths == 0) return;
-  path_kernel<<<nblk(a.total_paths, 128), 128, 0, st>>>(a);
+  if (a.nprim > 0) slot0_kernel<<<nblk(a.nprim, 256), 256, 0, st>>>(a);
+  if (a.total_ind > 0) ind_kernel<<<nblk(a.total_ind, 128), 128, 0, st>>>(a);
+  if (a.total_mc > 0) mc_kernel<<<nblk(a.total_mc, 128), 128, 0, st>>>(a);
 }
 void launch_reduce(const RenderArgs &a, hipStream_t st) {
   reduce_kernel<<<nblk(a.npix, 64), 64, 0, st>>>(a);

@@ -86,6 +86,7 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
     // keys accepted while key < thr; start: every d2 <= r2
     uint64_t thr = ((uint64_t)__float_as_uint(a.r2f) << 32) + 0x100000000ull;
     uint32_t visited = 0;
+    bool tight = false;
     if (N > 0) {
       int node = 1;
       while (true) {
@@ -126,6 +127,12 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
             }
             count += nnew;
             __syncthreads();
+          }
+          // first time K candidates are held: select now so the prune bound tightens from
+          // r^2 to the K-th distance early (otherwise it stays r^2 until the buffer fills)
+          if (!tight && count >= (uint32_t)K) {
+            select_k<CAP>(buf, lane, count, K, thr);
+            tight = true;
           }
         }
         while (node != 1) {

@@ -47,12 +47,17 @@ struct DElement {
   double bmin[3], bmax[3];  // element bbox in node-local coordinates
 };
 
+constexpr int GI_MAX_DEPTH = 16;  // scene-graph depth supported on the device
+
 struct DNode {
   double Tinv[12];     // world(parent)->local rows 0..2 of R4Matrix inverse
   double T[12];        // local->parent
   int32_t parent;      // -1 for root
   int32_t identity;    // transform is exactly the identity
   int32_t elem_first, elem_count;
+  int32_t depth;       // nodes on the path root..this node
+  int32_t chain[GI_MAX_DEPTH];  // that path, root first (precomputed: no per-ray walk)
+  int32_t pad;
 };
 
 struct DMaterial {

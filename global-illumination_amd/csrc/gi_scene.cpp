@@ -581,6 +581,18 @@ bool load_scene(const std::string &path, bool real, HostScene &S, std::string &e
     return false;
   }
   Bx sb = flatten(G, 0, -1, S);
+  // per-node transform chain, root first (the device walks it per ray without a stack)
+  for (size_t ni = 0; ni < S.nodes.size(); ni++) {
+    int path[256];
+    int d = 0;
+    for (int c = (int)ni; c >= 0 && d < 256; c = S.nodes[c].parent) path[d++] = c;
+    if (d > GI_MAX_DEPTH) {
+      S.unsupported_depth = true;
+      d = GI_MAX_DEPTH;
+    }
+    S.nodes[ni].depth = d;
+    for (int k = 0; k < d; k++) S.nodes[ni].chain[k] = path[d - 1 - k];
+  }
   S.mats = G.mats;
   S.lights = G.lights;
   for (int i = 0; i < 3; i++) {

@@ -20,6 +20,7 @@ struct HostScene {
   double bmin[3], bmax[3];
   double radius = 0, centroid[3] = {0, 0, 0};
   bool unsupported_shapes = false;  // cylinder / cone present
+  bool unsupported_depth = false;   // scene graph deeper than GI_MAX_DEPTH
 };
 
 // ReadScene (utils/io_utils.cpp:219-250) -> R3Scene::ReadFile (R3Scene.cpp:514-587)

@@ -205,10 +205,13 @@ struct gi_ctx {
   HostMap hmap[2];
   DevMap dmap[2];
   bool map_valid[2] = {false, false};
-  int leaf_size = 16;
+  int leaf_size[2] = {64, 512};  // photons per kd leaf, per map (global, caustic)
+  int wave_cap_mul = 1;
+  int sel_slack = 64;           // query-per-wave kernel: candidate buffer = mul * pow2(K+64)
   // render scratch
   DBuf spawn, npaths, path_off, nmc, mc_off, nind, ind_off, base, pixels, rgbf, rgb8, gheap_d2, gheap_idx, qcount, stats_bak;
   DBuf qpos[2], qshade[2], qkey[2], qout[2];
+  DBuf list_idx, list_d2, list_n;  // K-best lists of the query-per-wave k-NN path
   size_t qcap_hint[2] = {0, 0};
   KeySortScratch keysort[2];
   int knn_kernel_kind = -1;  // -1 auto, 0 per-lane heap, 1 query per wave, 2 packet
@@ -350,7 +353,7 @@ int set_map(gi_ctx *c, int mi, const gi_photon *ph, int64_t n) {
   HostMap &H = c->hmap[mi];
   H = HostMap();
   H.storage.assign(ph, ph + n);
-  kd_build(H, c->leaf_size, std::max(1, c->P.threads));
+  kd_build(H, c->leaf_size[mi], std::max(1, c->P.threads));
   return upload_map(c, mi);
 }
 
@@ -469,6 +472,7 @@ KnnArgs knn_args(gi_ctx *c, int mi) {
   k.fk = P.filter_const_k;
   k.stats = c->d_stats.as<unsigned long long>();
   k.stat_off = mi == GI_MAP_GLOBAL ? 0 : ST_KNN_MAP;
+  k.sel_slack = c->sel_slack;
   return k;
 }
 
@@ -482,9 +486,25 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
   if ((kind == 1 && k.K + 64 <= 1024) || kind == 2) {
     k.nq = nq;
     k.q0 = 0;
+    if (kind == 1) {
+      // search writes per-query K-best lists, a second kernel estimates from them
+      if (k.mode == KNN_MODE_LIST) {
+        k.list_idx = k.out_idx;
+        k.list_d2 = k.out_d2;
+        k.list_n = k.out_n;
+      } else {
+        size_t slots = (size_t)nq * (size_t)k.K;
+        HIPCHK(c, c->list_idx.ensure(slots * 4));
+        HIPCHK(c, c->list_d2.ensure(slots * 4));
+        HIPCHK(c, c->list_n.ensure((size_t)nq * 4));
+        k.list_idx = c->list_idx.as<int32_t>();
+        k.list_d2 = c->list_d2.as<float>();
+        k.list_n = c->list_n.as<int32_t>();
+      }
+    }
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     if (kind == 2) launch_knn_packet(k, c->stream);
-    else launch_knn_wave(k, c->stream);
+    else launch_knn_wave(k, c->wave_cap_mul, c->stream);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     if (ms) {
@@ -710,10 +730,13 @@ int gi_create(gi_ctx **out, int dev) {
   }
   hipStreamSynchronize(c->stream);
   if (const char *s = getenv("GI_PRIM_PER_BATCH")) c->prim_per_batch = std::max(1LL, atoll(s));
-  if (const char *s = getenv("GI_LEAF_SIZE")) c->leaf_size = std::max(1, atoi(s));
+  // tuning knobs (measurement only; defaults are the measured best)
+  if (const char *s = getenv("GI_LEAF_SIZE")) c->leaf_size[0] = c->leaf_size[1] = std::max(1, atoi(s));
+  if (const char *s = getenv("GI_LEAF_SIZE_C")) c->leaf_size[1] = std::max(1, atoi(s));
+  if (const char *s = getenv("GI_WAVE_CAP_MUL")) c->wave_cap_mul = std::max(1, atoi(s));
+  if (const char *s = getenv("GI_SEL_SLACK")) c->sel_slack = std::max(1, atoi(s));
   if (const char *s = getenv("GI_SORT_QUERIES")) c->sort_queries = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_KERNEL")) c->knn_kernel_kind = atoi(s);
-  if (!getenv("GI_LEAF_SIZE")) c->leaf_size = 64;
   *out = c;
   return GI_OK;
 }

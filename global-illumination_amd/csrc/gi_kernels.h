@@ -122,6 +122,8 @@ struct KnnArgs {
   int32_t filter;
   int32_t mode;
   int32_t stat_off;        // 0 (global map) or ST_KNN_MAP (caustic map)
+  int32_t sel_slack;       // query-per-wave kernel: re-select once K + slack candidates held
+  int32_t pad2;
   float r2f;               // (float)(r*r) accept radius
   double rmax;
   double fa, fb, fk;       // FILTER_CONST_A/B/K
@@ -130,6 +132,9 @@ struct KnnArgs {
   float *out_maxd2;        // optional
   int32_t *out_idx;        // KNN_MODE_LIST
   float *out_d2;
+  int32_t *list_idx;       // query-per-wave kernel: K-best lists [nq][K] (kd-order index)
+  float *list_d2;          //   and their d2; -1 past list_n[q]
+  int32_t *list_n;
   float *gheap_d2;         // global heap scratch (K > 64)
   int32_t *gheap_idx;
   unsigned long long *stats;
@@ -159,7 +164,7 @@ void launch_primary(const RenderArgs &a, hipStream_t st);
 void launch_path(const RenderArgs &a, hipStream_t st);  // slot0 + indirect + Monte Carlo
 void launch_reduce(const RenderArgs &a, hipStream_t st);
 void launch_knn(const KnnArgs &a, bool lds_heap, hipStream_t st);
-bool launch_knn_wave(const KnnArgs &a, hipStream_t st);
+bool launch_knn_wave(const KnnArgs &a, int cap_mul, hipStream_t st);
 bool launch_knn_packet(const KnnArgs &a, hipStream_t st);
 void launch_cached(const KnnArgs &a, hipStream_t st);
 void launch_photons(const PhotonArgs &a, bool emit, hipStream_t st);

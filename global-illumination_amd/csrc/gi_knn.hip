@@ -7,7 +7,7 @@
 //   * leaves hold <= 64 photons: one photon per lane, one coalesced 16-B load per lane;
 //   * candidates with key = (d2 bits << 32 | photon index) below the current threshold are
 //     appended to an LDS buffer by ballot/mbcnt compaction; when the buffer cannot take the
-//     next leaf, a bitonic sort of the buffer keeps the K best and tightens the threshold
+//     next leaf, a radix select (LDS histograms) keeps the K best and tightens the threshold
 //     (the reference's delayed make_heap + replace-max, R3Kdtree.cpp:753-782, as a batched
 //     selection). Result set: the K smallest (d2, index) pairs with d2 <= r2 -- identical
 //     to the reference's set up to ties at the K-th distance.
@@ -33,43 +33,98 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-// bitonic sort of buf[0, CAP) ascending (CAP power of two, 64 lanes)
-template <int CAP>
-__device__ __forceinline__ void bitonic_sort(uint64_t *buf, int lane) {
-#pragma unroll 1
-  for (int k = 2; k <= CAP; k <<= 1) {
-#pragma unroll 1
-    for (int j = k >> 1; j > 0; j >>= 1) {
+// Wave-level radix select over the candidate buffer buf[0, count): find the K-th smallest
+// key T, keep exactly the keys <= T (compacted to buf[0, K)) and set thr = T (a later
+// candidate must be < T). Digits: the 4 bytes of the d2 bits, MSB first, each a 256-bin LDS
+// histogram + wave prefix scan; the index bytes are resolved only when several keys share
+// the K-th distance. Keys are re-read from LDS on every pass (no per-lane key arrays: the
+// register budget sets this kernel's occupancy).
+__device__ __forceinline__ uint32_t radix_pick(uint32_t *hist, int lane, uint32_t &need) {
+  uint32_t c0 = hist[4 * lane], c1 = hist[4 * lane + 1], c2 = hist[4 * lane + 2],
+           c3 = hist[4 * lane + 3];
+  uint32_t sum = c0 + c1 + c2 + c3, inc = sum;
 #pragma unroll
-      for (int p = lane; p < CAP / 2; p += 64) {
-        int i = 2 * p - (p & (j - 1));
-        int ixj = i + j;
-        uint64_t x = buf[i], y = buf[ixj];
-        bool up = (i & k) == 0;
-        if ((x > y) == up) {
-          buf[i] = y;
-          buf[ixj] = x;
-        }
-      }
-      __syncthreads();
-    }
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t t = (uint32_t)__shfl_up((int)inc, o, 64);
+    if (lane >= o) inc += t;
   }
+  uint32_t exc = inc - sum;
+  uint64_t hit = __ballot(exc < need && need <= inc);
+  int L = __ffsll((long long)hit) - 1;
+  uint32_t d = 0, before = exc;
+  if (lane == L) {
+    if (need <= before + c0) d = 0;
+    else if (need <= before + c0 + c1) { d = 1; before += c0; }
+    else if (need <= before + c0 + c1 + c2) { d = 2; before += c0 + c1; }
+    else { d = 3; before += c0 + c1 + c2; }
+    d = 4 * (uint32_t)lane + d;
+  }
+  need -= (uint32_t)__shfl((int)before, L, 64);
+  return (uint32_t)__shfl((int)d, L, 64);
 }
 
 template <int CAP>
-__device__ __forceinline__ void select_k(uint64_t *buf, int lane, uint32_t &count, int K,
-                                         uint64_t &thr) {
-  for (int s = lane; s < CAP; s += 64)
-    if ((uint32_t)s >= count) buf[s] = ~0ull;
+__device__ __forceinline__ void select_k(uint64_t *buf, uint32_t *hist, int lane, uint32_t &count,
+                                         int K, uint64_t &thr) {
+  uint32_t need = (uint32_t)K, prefix = 0;
+#pragma unroll 1
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    hist[4 * lane] = hist[4 * lane + 1] = hist[4 * lane + 2] = hist[4 * lane + 3] = 0u;
+    __syncthreads();
+    uint32_t hm = (shift == 24) ? 0u : (0xffffffffu << (shift + 8));
+    for (uint32_t s = (uint32_t)lane; s < count; s += 64) {
+      uint32_t h = (uint32_t)(buf[s] >> 32);
+      if (((h ^ prefix) & hm) == 0u) atomicAdd(&hist[(h >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    prefix |= radix_pick(hist, lane, need) << shift;
+    __syncthreads();
+  }
+  // prefix = d2 bits of the K-th key; `need` of the keys with exactly that d2 are kept
+  uint32_t eq = 0;
+  for (uint32_t s0 = 0; s0 < count; s0 += 64) {
+    uint32_t s = s0 + (uint32_t)lane;
+    eq += (uint32_t)__popcll(__ballot(s < count && (uint32_t)(buf[s < count ? s : 0] >> 32) == prefix));
+  }
+  uint32_t tidx = 0xffffffffu;
+  if (need < eq) {
+    uint32_t lp = 0;
+#pragma unroll 1
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      hist[4 * lane] = hist[4 * lane + 1] = hist[4 * lane + 2] = hist[4 * lane + 3] = 0u;
+      __syncthreads();
+      uint32_t lm = (shift == 24) ? 0u : (0xffffffffu << (shift + 8));
+      for (uint32_t s = (uint32_t)lane; s < count; s += 64) {
+        uint64_t k = buf[s];
+        uint32_t h = (uint32_t)(k >> 32), l = (uint32_t)k;
+        if (h == prefix && ((l ^ lp) & lm) == 0u) atomicAdd(&hist[(l >> shift) & 255u], 1u);
+      }
+      __syncthreads();
+      lp |= radix_pick(hist, lane, need) << shift;
+      __syncthreads();
+    }
+    tidx = lp;
+  }
+  uint64_t T = ((uint64_t)prefix << 32) | (uint64_t)tidx;
+  // compact the keys <= T (exactly K) to buf[0, K); writes never pass unread entries
+  uint32_t base = 0;
+  for (uint32_t s0 = 0; s0 < count; s0 += 64) {
+    uint32_t s = s0 + (uint32_t)lane;
+    uint64_t k = (s < count) ? buf[s] : ~0ull;
+    bool keep = (s < count) && k <= T;
+    uint64_t m = __ballot(keep);
+    if (keep) buf[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = k;
+    base += (uint32_t)__popcll(m);
+  }
   __syncthreads();
-  bitonic_sort<CAP>(buf, lane);
-  if (count > (uint32_t)K) count = (uint32_t)K;
-  if (count == (uint32_t)K) thr = buf[K - 1];  // candidates must beat the K-th
+  count = base;  // == K
+  thr = T;
 }
 
 template <int CAP>
 __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
   __shared__ uint64_t buf[CAP];
+  __shared__ uint32_t hist[256];
   const int lane = threadIdx.x;
   const KdNode *nodes = reinterpret_cast<const KdNode *>(a.map.nodes);
   const float4 *pos = reinterpret_cast<const float4 *>(a.map.pos4);
@@ -115,7 +170,7 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
             uint32_t nnew = (uint32_t)__popcll(m);
             if (nnew == 0) continue;
             if (count + nnew > (uint32_t)CAP) {
-              select_k<CAP>(buf, lane, count, K, thr);
+              select_k<CAP>(buf, hist, lane, count, K, thr);
               pass = key < thr;
               m = __ballot(pass);
               nnew = (uint32_t)__popcll(m);
@@ -130,8 +185,8 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
           }
           // first time K candidates are held: select now so the prune bound tightens from
           // r^2 to the K-th distance early (otherwise it stays r^2 until the buffer fills)
-          if (!tight && count >= (uint32_t)K) {
-            select_k<CAP>(buf, lane, count, K, thr);
+          if (K > 0 && count >= (uint32_t)K + (tight ? (uint32_t)a.sel_slack : 0u)) {
+            select_k<CAP>(buf, hist, lane, count, K, thr);
             tight = true;
           }
         }
@@ -147,25 +202,38 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
       }
     }
     // exact K best
-    if (count > (uint32_t)K) select_k<CAP>(buf, lane, count, K, thr);
+    if (count > (uint32_t)K) select_k<CAP>(buf, hist, lane, count, K, thr);
     int num = (int)count;
     st_q += 1;
     st_found += (uint64_t)num;
     st_vis += visited;
-    if (a.mode == KNN_MODE_LIST) {
-      if (count > 0 && a.K > 0) {
-        // sort for a deterministic listing
-        select_k<CAP>(buf, lane, count, K, thr);
-      }
-      for (int s = lane; s < K; s += 64) {
-        bool v = s < num;
-        a.out_idx[qi * K + s] = v ? (int32_t)(uint32_t)buf[s] : -1;
-        a.out_d2[qi * K + s] = v ? __uint_as_float((uint32_t)(buf[s] >> 32)) : -1.0f;
-      }
-      if (lane == 0) a.out_n[qi] = num;
-      __syncthreads();
-      continue;
+    for (int s = lane; s < K; s += 64) {
+      bool v = s < num;
+      a.list_idx[qi * K + s] = v ? (int32_t)(uint32_t)buf[s] : -1;
+      a.list_d2[qi * K + s] = v ? __uint_as_float((uint32_t)(buf[s] >> 32)) : -1.0f;
     }
+    if (lane == 0) a.list_n[qi] = num;
+    __syncthreads();
+  }
+  if (a.stats && lane == 0) {
+    if (st_q) atomicAdd(&a.stats[ST_KNN + a.stat_off], (unsigned long long)st_q);
+    if (st_found) atomicAdd(&a.stats[ST_KNN_PHOTONS + a.stat_off], (unsigned long long)st_found);
+    if (st_vis) atomicAdd(&a.stats[ST_KNN_VISITED + a.stat_off], (unsigned long long)st_vis);
+  }
+}
+
+// EstimateRadiance / EstimateIrradiance (photon_utils.cpp:72-162, 209-246) over the K-best
+// lists written by knn_wave_kernel: one wave per query, photons spread over the lanes,
+// fp64 partial sums reduced across the wave. Split from the search so the search kernel
+// keeps a small register footprint (50 VGPRs: 7 waves/SIMD instead of 3).
+__global__ __launch_bounds__(64) void knn_list_estimate_kernel(KnnArgs a) {
+  const int lane = threadIdx.x;
+  const int K = a.K;
+  for (int64_t qq = blockIdx.x; qq < a.nq; qq += gridDim.x) {
+    int64_t qg = a.q0 + qq;
+    int64_t qi = a.perm ? (int64_t)a.perm[qg] : qg;
+    float4 qp = a.qpos[qi];
+    int num = a.list_n[qi];
     double maxd2 = kEps;
     double o0 = 0, o1 = 0, o2 = 0;
     if (num > 0) {
@@ -174,7 +242,7 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
       } else {
         double lm = 0.0;
         for (int s = lane; s < num; s += 64) {
-          double d = (double)__uint_as_float((uint32_t)(buf[s] >> 32));
+          double d = (double)a.list_d2[qi * K + s];
           lm = d > lm ? d : lm;
         }
 #pragma unroll
@@ -186,7 +254,7 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
       }
       if (a.mode == KNN_MODE_IRRADIANCE) {
         for (int s = lane; s < num; s += 64) {
-          uint32_t e = a.map.rgbe[(uint32_t)buf[s]];
+          uint32_t e = a.map.rgbe[(uint32_t)a.list_idx[qi * K + s]];
           uint32_t ee = e >> 24;
           if (ee) {
             double inv = ldexp(1.0, (int)ee - 128 - 8);
@@ -213,8 +281,8 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
           c2 = 1.0 / (2.0 * maxd2);
         }
         for (int s = lane; s < num; s += 64) {
-          uint32_t id = (uint32_t)buf[s];
-          double d2 = (double)__uint_as_float((uint32_t)(buf[s] >> 32));
+          uint32_t id = (uint32_t)a.list_idx[qi * K + s];
+          double d2 = (double)a.list_d2[qi * K + s];
           uint32_t dcode = __float_as_uint(a.map.pos4[4 * (int64_t)id + 3]) & 0xffffu;
           double ix = a.lut[3 * dcode], iy = a.lut[3 * dcode + 1], iz = a.lut[3 * dcode + 2];
           double perp = N0 * ix + N1 * iy + N2 * iz;
@@ -271,12 +339,6 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
       if (a.out_n) a.out_n[qi] = num;
       if (a.out_maxd2) a.out_maxd2[qi] = (num > 0) ? (float)maxd2 : 0.0f;
     }
-    __syncthreads();
-  }
-  if (a.stats && lane == 0) {
-    if (st_q) atomicAdd(&a.stats[ST_KNN + a.stat_off], (unsigned long long)st_q);
-    if (st_found) atomicAdd(&a.stats[ST_KNN_PHOTONS + a.stat_off], (unsigned long long)st_found);
-    if (st_vis) atomicAdd(&a.stats[ST_KNN_VISITED + a.stat_off], (unsigned long long)st_vis);
   }
 }
 
@@ -530,15 +592,16 @@ bool launch_knn_packet(const KnnArgs &a, hipStream_t st) {
   return true;
 }
 
-bool launch_knn_wave(const KnnArgs &a, hipStream_t st) {
+bool launch_knn_wave(const KnnArgs &a, int cap_mul, hipStream_t st) {
   if (a.nq == 0) return true;
-  int need = a.K + 64;
+  int need = (a.K + 64) * cap_mul;
   int64_t grid = a.nq < (1 << 16) ? a.nq : (1 << 16);
   if (need <= 128) knn_wave_kernel<128><<<(unsigned)grid, 64, 0, st>>>(a);
   else if (need <= 256) knn_wave_kernel<256><<<(unsigned)grid, 64, 0, st>>>(a);
   else if (need <= 512) knn_wave_kernel<512><<<(unsigned)grid, 64, 0, st>>>(a);
   else if (need <= 1024) knn_wave_kernel<1024><<<(unsigned)grid, 64, 0, st>>>(a);
   else return false;
+  if (a.mode != KNN_MODE_LIST) knn_list_estimate_kernel<<<(unsigned)grid, 64, 0, st>>>(a);
   return true;
 }
 

@@ -25,11 +25,17 @@ def main():
     ap.add_argument("--modes", default="0")
     ap.add_argument("--maps", default="0,1")
     ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--capmul", default="1", help="GI_WAVE_CAP_MUL values")
+    ap.add_argument("--slack", default="64", help="GI_SEL_SLACK values")
     a = ap.parse_args()
     rng = np.random.default_rng(7)
     scene = os.path.join(ROOT, "tests", "scenes", "cornell.scn")
-    for leaf in a.leaf.split(","):
+    combos = [(lf, cm, sl) for lf in a.leaf.split(",") for cm in a.capmul.split(",")
+              for sl in a.slack.split(",")]
+    for leaf, capmul, slack in combos:
         os.environ["GI_LEAF_SIZE"] = leaf
+        os.environ["GI_WAVE_CAP_MUL"] = capmul
+        os.environ["GI_SEL_SLACK"] = slack
         import gi_amd
         args = [scene, "/tmp/x.png", "-global", "1000000", "-caustic", "1000000"]
         p, sc, _o, w, h, aa, real = gi_amd.ParseArgs(args)
@@ -47,7 +53,7 @@ def main():
                 for mode in [int(x) for x in a.modes.split(",")]:
                     ms, fq, vq = r.knn_bench(mp, pt, nr, mat, mode=mode, kernel=kern,
                                              iters=a.iters)
-                    print(f"leaf={leaf} map={mp} kernel={kern} mode={mode} nq={len(pt)} "
+                    print(f"leaf={leaf} capmul={capmul} slack={slack} map={mp} kernel={kern} mode={mode} nq={len(pt)} "
                           f"ms={ms:.2f} ns/q={ms * 1e6 / len(pt):.2f} found={fq:.1f} "
                           f"visited={vq:.1f}", flush=True)
         r.close()

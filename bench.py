@@ -161,7 +161,7 @@ def main():
 
     if rank == 0:
         # roofline of the dominant kernel: the global-map k-NN radiance estimate
-        # (knn_kernel<true>, K=50), HIP-event timed in-library on the render stream
+        # (knn_lane_kernel, K=50), HIP-event timed in-library on the render stream
         def kstats(m):
             ms = agg[f"ms{m}"]
             launches = max(1.0, agg[f"n{m}"])
@@ -180,9 +180,9 @@ def main():
         roofline = {"bound": "hbm", "achieved": g["achieved_GBps"], "peak": HBM_PEAK_GBPS,
                     "unit": "GB/s", "frac": round(g["achieved_GBps"] / HBM_PEAK_GBPS, 5),
                     "traffic": traffic,
-                    "kernel": "gi::knn_kernel<true> (global map k-NN + EstimateRadiance)",
+                    "kernel": "gi::knn_lane_kernel<8,4> (global map k-NN + EstimateRadiance)",
                     "bytes_per_unit": "16 B per photon returned (SURVEY.md 8(d))",
-                    "global": g, "caustic_kernel": dict(c, kernel="gi::knn_wave_kernel<512>")}
+                    "global": g, "caustic_kernel": dict(c, kernel="gi::knn_wave_kernel<512> + knn_list_estimate_kernel")}
         cpu = None
         if not a.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(a)

@@ -207,7 +207,12 @@ struct gi_ctx {
   bool map_valid[2] = {false, false};
   int leaf_size[2] = {64, 512};  // photons per kd leaf, per map (global, caustic)
   int wave_cap_mul = 1;
-  int sel_slack = 64;           // query-per-wave kernel: candidate buffer = mul * pow2(K+64)
+  int sel_slack = 64;
+  bool force_gheap = false;
+  int knn_qpl = 1;
+  int lane_chunk = 8;             // per-lane kernel: photon loads in flight per lane
+  int group_lanes = 16;           // group kernel: lanes per query
+  int heap_arity = 4;             // per-lane kernel: d-ary heap                // per-lane kernel: sorted queries per lane (bound reuse)       // per-lane kernel: heap in global memory even for K <= 64           // query-per-wave kernel: candidate buffer = mul * pow2(K+64)
   // render scratch
   DBuf spawn, npaths, path_off, nmc, mc_off, nind, ind_off, base, pixels, rgbf, rgb8, gheap_d2, gheap_idx, qcount, stats_bak;
   DBuf qpos[2], qshade[2], qkey[2], qout[2];
@@ -473,20 +478,36 @@ KnnArgs knn_args(gi_ctx *c, int mi) {
   k.stats = c->d_stats.as<unsigned long long>();
   k.stat_off = mi == GI_MAP_GLOBAL ? 0 : ST_KNN_MAP;
   k.sel_slack = c->sel_slack;
+  k.qpl = c->knn_qpl;
   return k;
 }
 
 // run a k-NN launch over nq queries (chunked when the heap lives in global scratch)
 int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
-  // auto (-1): per-lane LDS heaps while they fit (K <= 64), else one query per wave
+  // auto (-1): per-lane 4-ary LDS heaps while they fit (K <= 64), else one query per wave
   // (measured with tools/knn_micro.py on cornell 1M+1M maps)
   int kind = c->knn_kernel_kind;
-  if (kind < 0) kind = (k.K <= 64) ? 0 : 1;
+  if (kind < 0) kind = (k.K <= 64) ? 3 : 1;
   if (kind == 2 && (int64_t)k.K * 64 * 8 > 80 * 1024) kind = 1;
-  if ((kind == 1 && k.K + 64 <= 1024) || kind == 2) {
+  if (kind == 3 && (size_t)k.K * 512 <= 64 * 1024) {
     k.nq = nq;
     k.q0 = 0;
-    if (kind == 1) {
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    launch_knn_lane(k, c->lane_chunk, c->heap_arity, c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    if (ms) {
+      HIPCHK(c, hipEventSynchronize(c->ev1));
+      float t = 0;
+      HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+      *ms += t;
+    }
+    return GI_OK;
+  }
+  if ((kind == 1 && k.K + 64 <= 1024) || kind == 2 || kind == 4) {
+    k.nq = nq;
+    k.q0 = 0;
+    if (kind == 1 || kind == 4) {
       // search writes per-query K-best lists, a second kernel estimates from them
       if (k.mode == KNN_MODE_LIST) {
         k.list_idx = k.out_idx;
@@ -503,8 +524,13 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
       }
     }
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    if (kind == 2) launch_knn_packet(k, c->stream);
-    else launch_knn_wave(k, c->wave_cap_mul, c->stream);
+    bool ok = true;
+    if (kind == 2) ok = launch_knn_packet(k, c->stream);
+    else if (kind == 4)
+      ok = launch_knn_group(k, c->group_lanes, c->stream) ||
+           launch_knn_wave(k, c->wave_cap_mul, c->stream);  // K too large for the groups
+    else ok = launch_knn_wave(k, c->wave_cap_mul, c->stream);
+    if (!ok) return fail(c, GI_ERR_ARG, "k-NN launch: unsupported estimate size for this kernel");
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     if (ms) {
@@ -515,7 +541,7 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
     }
     return GI_OK;
   }
-  bool lds = k.K <= 64;
+  bool lds = k.K <= 64 && !c->force_gheap;
   const int64_t CH = lds ? nq : (int64_t)(1 << 20);
   for (int64_t s = 0; s < nq; s += CH) {
     int64_t m = std::min(CH, nq - s);
@@ -735,6 +761,11 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_LEAF_SIZE_C")) c->leaf_size[1] = std::max(1, atoi(s));
   if (const char *s = getenv("GI_WAVE_CAP_MUL")) c->wave_cap_mul = std::max(1, atoi(s));
   if (const char *s = getenv("GI_SEL_SLACK")) c->sel_slack = std::max(1, atoi(s));
+  if (const char *s = getenv("GI_KNN_GHEAP")) c->force_gheap = atoi(s) != 0;
+  if (const char *s = getenv("GI_KNN_QPL")) c->knn_qpl = std::max(1, atoi(s));
+  if (const char *s = getenv("GI_LANE_CHUNK")) c->lane_chunk = std::max(1, atoi(s));
+  if (const char *s = getenv("GI_GROUP_LANES")) c->group_lanes = std::max(1, atoi(s));
+  if (const char *s = getenv("GI_HEAP_ARITY")) c->heap_arity = std::max(2, atoi(s));
   if (const char *s = getenv("GI_SORT_QUERIES")) c->sort_queries = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_KERNEL")) c->knn_kernel_kind = atoi(s);
   *out = c;

@@ -100,6 +100,22 @@ __device__ __forceinline__ float kd_axis_q(int axis, float qx, float qy, float q
   return (axis == 0) ? qx : ((axis == 1) ? qy : qz);
 }
 
+// Stackless backtrack: move to the far sibling of the deepest near child on the path from
+// the root to `node`; false when the walk is complete.
+__device__ __forceinline__ bool kd_next(const KdNode *nodes, int &node, float qx, float qy,
+                                        float qz) {
+  while (node != 1) {
+    const KdNode &pn = nodes[node >> 1];
+    float q = kd_axis_q(__float_as_int(pn.hi.w), qx, qy, qz);
+    int near_is_right = (q - pn.lo.w >= 0.0f) ? 1 : 0;
+    if ((node & 1) == near_is_right) break;
+    node >>= 1;
+  }
+  if (node == 1) return false;
+  node ^= 1;
+  return true;
+}
+
 // wave-level counter reduction (one atomic per wave)
 __device__ __forceinline__ void wave_add(unsigned long long *dst, uint64_t v) {
 #pragma unroll
@@ -123,7 +139,7 @@ struct KnnArgs {
   int32_t mode;
   int32_t stat_off;        // 0 (global map) or ST_KNN_MAP (caustic map)
   int32_t sel_slack;       // query-per-wave kernel: re-select once K + slack candidates held
-  int32_t pad2;
+  int32_t qpl;             // per-lane kernel: consecutive (sorted) queries per lane
   float r2f;               // (float)(r*r) accept radius
   double rmax;
   double fa, fb, fk;       // FILTER_CONST_A/B/K
@@ -166,6 +182,9 @@ void launch_reduce(const RenderArgs &a, hipStream_t st);
 void launch_knn(const KnnArgs &a, bool lds_heap, hipStream_t st);
 bool launch_knn_wave(const KnnArgs &a, int cap_mul, hipStream_t st);
 bool launch_knn_packet(const KnnArgs &a, hipStream_t st);
+bool launch_knn_lane(const KnnArgs &a, int chunk, int arity, hipStream_t st);
+bool launch_knn_group(const KnnArgs &a, int lanes, hipStream_t st);
+void launch_list_estimate(const KnnArgs &a, hipStream_t st);
 void launch_cached(const KnnArgs &a, hipStream_t st);
 void launch_photons(const PhotonArgs &a, bool emit, hipStream_t st);
 void launch_intersect(const SceneView &S, int64_t n, const double *org, const double *dir,

@@ -520,22 +520,6 @@ __device__ __forceinline__ float metric_d2(float qx, float qy, float qz, float4 
   return __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
 }
 
-// Stackless backtrack: move to the far sibling of the deepest near child on the path from
-// the root to `node`; false when the walk is complete.
-__device__ __forceinline__ bool kd_next(const KdNode *nodes, int &node, float qx, float qy,
-                                        float qz) {
-  while (node != 1) {
-    const KdNode &pn = nodes[node >> 1];
-    float q = kd_axis_q(__float_as_int(pn.hi.w), qx, qy, qz);
-    int near_is_right = (q - pn.lo.w >= 0.0f) ? 1 : 0;
-    if ((node & 1) == near_is_right) break;
-    node >>= 1;
-  }
-  if (node == 1) return false;
-  node ^= 1;
-  return true;
-}
-
 // Find the K best photons of query (qx,qy,qz) within r2; returns heap size.
 // "While-while" structure: each lane walks internal nodes until it holds its next leaf
 // (or finishes); only then does the wave run the leaf loop, for all lanes at once. A single
@@ -602,32 +586,48 @@ __device__ __forceinline__ int knn_search(const KdView &M, float qx, float qy, f
   return size;
 }
 
+// Each lane answers a.qpl Morton-consecutive queries (q = (block*qpl + it)*64 + lane). After
+// the first, the search starts from a proven bound instead of r^2: the K photons found for
+// the previous query p all lie within d_K(p) + |q - p| of q (triangle inequality), so
+// d_K(q)^2 <= (d_K(p) + |q - p|)^2. A 1e-5 relative margin covers the fp32 metric's
+// rounding; the bound only prunes, the result set is unchanged.
 template <bool LDS_HEAP>
 __global__ __launch_bounds__(64) void knn_kernel(KnnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int lane = threadIdx.x;
-  int64_t q = (int64_t)blockIdx.x * 64 + lane;
   uint64_t nfound_total = 0, visited_total = 0, nq_done = 0;
-  if (q < a.nq) {
-    HeapRef h;
-    if (LDS_HEAP) {
-      h.d2 = reinterpret_cast<float *>(smem) + lane;
-      h.idx = reinterpret_cast<int32_t *>(smem + (size_t)a.K * 64 * sizeof(float)) + lane;
-      h.stride = 64;
-    } else {
-      int64_t slot_stride = (int64_t)gridDim.x * 64;
-      h.d2 = a.gheap_d2 + q;
-      h.idx = a.gheap_idx + q;
-      h.stride = (int)slot_stride;
-    }
+  HeapRef h;
+  if (LDS_HEAP) {
+    h.d2 = reinterpret_cast<float *>(smem) + lane;
+    h.idx = reinterpret_cast<int32_t *>(smem + (size_t)a.K * 64 * sizeof(float)) + lane;
+    h.stride = 64;
+  } else {
+    int64_t t = (int64_t)blockIdx.x * 64 + lane;
+    h.d2 = a.gheap_d2 + t;
+    h.idx = a.gheap_idx + t;
+    h.stride = (int)((int64_t)gridDim.x * 64);
+  }
+  float px = 0.f, py = 0.f, pz = 0.f, pk2 = -1.0f;  // previous query and its K-th d2
+  for (int it = 0; it < a.qpl; it++) {
+    int64_t q = ((int64_t)blockIdx.x * a.qpl + it) * 64 + lane;
+    if (q >= a.nq) break;
     int64_t qg = a.q0 + q;
     int64_t qi = a.perm ? (int64_t)a.perm[qg] : qg;
     float4 qp = a.qpos[qi];
+    float bound = a.r2f;
+    if (pk2 >= 0.0f) {
+      double dx = (double)qp.x - px, dy = (double)qp.y - py, dz = (double)qp.z - pz;
+      double rb = (sqrt((double)pk2) + sqrt(dx * dx + dy * dy + dz * dz)) * (1.0 + 1e-5);
+      float b2 = __double2float_ru(rb * rb);
+      if (b2 < bound) bound = b2;
+    }
     uint32_t visited = 0;
-    int num = knn_search(a.map, qp.x, qp.y, qp.z, a.r2f, a.K, h, visited);
-    nfound_total = num;
-    visited_total = visited;
-    nq_done = 1;
+    int num = knn_search(a.map, qp.x, qp.y, qp.z, bound, a.K, h, visited);
+    px = qp.x; py = qp.y; pz = qp.z;
+    pk2 = (num == a.K) ? h.d2[0] : -1.0f;
+    nfound_total += num;
+    visited_total += visited;
+    nq_done += 1;
     if (a.mode == KNN_MODE_LIST) {
       for (int s = 0; s < a.K; s++) {
         a.out_idx[qi * a.K + s] = (s < num) ? h.idx[s * h.stride] : -1;
@@ -1100,9 +1100,9 @@ void launch_knn(const KnnArgs &a, bool lds_heap, hipStream_t st) {
   if (a.nq == 0) return;
   if (lds_heap) {
     size_t sm = (size_t)a.K * 64 * (sizeof(float) + sizeof(int32_t));
-    knn_kernel<true><<<nblk(a.nq, 64), 64, sm, st>>>(a);
+    knn_kernel<true><<<nblk(a.nq, 64 * a.qpl), 64, sm, st>>>(a);
   } else {
-    knn_kernel<false><<<nblk(a.nq, 64), 64, 0, st>>>(a);
+    knn_kernel<false><<<nblk(a.nq, 64 * a.qpl), 64, 0, st>>>(a);
   }
 }
 void launch_cached(const KnnArgs &a, hipStream_t st) {

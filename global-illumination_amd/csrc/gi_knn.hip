@@ -342,23 +342,6 @@ __global__ __launch_bounds__(64) void knn_list_estimate_kernel(KnnArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// Packet k-NN: 64 spatially adjacent queries (Morton order) per wave share ONE wave-uniform
-// traversal of the kd-tree, so each node and leaf fetch serves 64 queries. Every lane keeps
-// its own exact max-heap of the K best keys (d2 bits << 32 | photon index) in LDS laid out
-// [slot][lane] (8-B stride across lanes: conflict-free ds_read/write_b64).
-//
-// Exactness: a subtree is skipped only if, for EVERY lane, the query lies on the visited side
-// of the split and diff^2 > that lane's current bound (the single-query rule of
-// R3Kdtree.cpp:740-751 applied per lane), so each lane's result is the same K smallest
-// (d2, index) pairs with d2 <= r2 as the per-query search.
-// Visit order: at each node the packet descends first into the side holding the majority
-// of its queries (recomputed identically on the way up, which makes the walk stackless).
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ float rlane(float v, int j) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
-}
-
 __device__ __forceinline__ void kheap_push(uint64_t *h, int size, uint64_t key) {
   int c = size;
   while (c > 0) {
@@ -386,6 +369,277 @@ __device__ __forceinline__ void kheap_replace_top(uint64_t *h, int size, uint64_
     c = l;
   }
   h[c * 64] = key;
+}
+
+// ---------------------------------------------------------------------------------------
+// Per-lane k-NN (the default for K <= 64): one query per lane, exact K-best keys
+// (d2 bits << 32 | kd-order index) in a 4-ary max-heap in LDS laid out [slot][lane].
+// Measured: this kernel is bound by dependent LDS round trips in the heap updates, at the
+// ~6 waves/CU that the heaps' LDS allows. So:
+//   * the first K accepted keys are appended unordered and heapified once (Floyd), instead
+//     of K sift-ups that each run at the SIMD-max depth;
+//   * the heap is 4-ary: a replacement sifts ~3 levels for K = 50 (binary: ~6), and the 4
+//     child loads of a level are in flight together;
+//   * the walk is "while-while": lanes step through internal nodes until each holds a leaf,
+//     then the wave runs the leaf loop together, CH photon loads in flight per lane.
+// Result set: the K smallest (d2, index) keys with d2 <= r2 (R3Kdtree.cpp:688-784 semantics).
+// ---------------------------------------------------------------------------------------
+template <int ARY>
+__device__ __forceinline__ void heapn_sift(uint64_t *h, int n, int c, uint64_t key) {
+  while (true) {
+    int f = ARY * c + 1;
+    if (f >= n) break;
+    uint64_t kk[ARY];
+#pragma unroll
+    for (int j = 0; j < ARY; j++) kk[j] = (f + j < n) ? h[(f + j) * 64] : 0ull;
+    int m = f;
+    uint64_t mk = kk[0];
+#pragma unroll
+    for (int j = 1; j < ARY; j++)
+      if (kk[j] > mk) { mk = kk[j]; m = f + j; }
+    if (key >= mk) break;
+    h[c * 64] = mk;
+    c = m;
+  }
+  h[c * 64] = key;
+}
+
+template <int ARY>
+__device__ __forceinline__ void heapn_build(uint64_t *h, int n) {
+  for (int i = (n - 2) / ARY; i >= 0; i--) heapn_sift<ARY>(h, n, i, h[i * 64]);
+}
+
+// accept one candidate (key < lim already checked)
+template <int ARY>
+__device__ __forceinline__ void heapn_accept(uint64_t *h, int &size, int K, uint64_t key,
+                                             uint64_t &lim) {
+  if (size < K) {
+    h[size * 64] = key;
+    size++;
+    if (size == K) {
+      heapn_build<ARY>(h, K);
+      lim = h[0];
+    }
+  } else {
+    heapn_sift<ARY>(h, K, 0, key);
+    lim = h[0];
+  }
+}
+
+template <int CH, int ARY>
+__global__ __launch_bounds__(64) void knn_lane_kernel(KnnArgs a) {
+  extern __shared__ uint64_t lsm[];
+  const int lane = threadIdx.x;
+  const int K = a.K;
+  uint64_t *h = lsm + lane;  // [K][64]
+  const KdNode *nodes = reinterpret_cast<const KdNode *>(a.map.nodes);
+  const float4 *pos = reinterpret_cast<const float4 *>(a.map.pos4);
+  const int L = a.map.nleaves;
+  const int64_t N = a.map.n;
+  const int64_t q = (int64_t)blockIdx.x * 64 + lane;
+  const bool valid = q < a.nq;
+  int64_t qi = 0;
+  float4 qp = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (valid) {
+    int64_t qg = a.q0 + q;
+    qi = a.perm ? (int64_t)a.perm[qg] : qg;
+    qp = a.qpos[qi];
+  }
+  int size = 0;
+  // accept key < lim; start: every d2 <= r2
+  uint64_t lim = ((uint64_t)__float_as_uint(a.r2f) + 1ull) << 32;
+  uint32_t visited = 0;
+  int node = 1;
+  bool live = valid && N > 0 && K > 0;
+  while (__ballot(live)) {
+    // walk to the next leaf within the bound
+    int leaf = -1;
+    float pr = __uint_as_float((uint32_t)((lim - 1ull) >> 32));
+    while (live) {
+      KdNode nd = nodes[node];
+      if (kd_box_d2(nd.lo, nd.hi, qp.x, qp.y, qp.z) <= pr) {
+        if (node < L) {
+          float qa = kd_axis_q(__float_as_int(nd.hi.w), qp.x, qp.y, qp.z);
+          node = 2 * node + ((qa - nd.lo.w >= 0.0f) ? 1 : 0);
+          continue;
+        }
+        leaf = node - L;
+        break;
+      }
+      live = kd_next(nodes, node, qp.x, qp.y, qp.z);
+    }
+    int64_t s0 = 0, s1 = 0;
+    if (leaf >= 0) {
+      s0 = ((int64_t)leaf * N) / L;
+      s1 = ((int64_t)(leaf + 1) * N) / L;
+      visited += (uint32_t)(s1 - s0);
+    }
+    // converged leaf loop: CH photon loads in flight per lane
+    int steps = (int)((s1 - s0 + CH - 1) / CH);
+    int msteps = steps;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) msteps = max(msteps, __shfl_xor(msteps, o, 64));
+    for (int st = 0; st < msteps; st++) {
+      if (st < steps) {
+        int64_t ii = s0 + CH * (int64_t)st;
+        float4 p[CH];
+#pragma unroll
+        for (int u = 0; u < CH; u++) p[u] = pos[(ii + u < s1) ? ii + u : s1 - 1];
+#pragma unroll
+        for (int u = 0; u < CH; u++) {
+          float dx = qp.x - p[u].x, dy = qp.y - p[u].y, dz = qp.z - p[u].z;
+          float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
+          uint64_t key = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)(uint32_t)(ii + u);
+          if (ii + u < s1 && key < lim) heapn_accept<ARY>(h, size, K, key, lim);
+        }
+      }
+    }
+    if (leaf >= 0) live = kd_next(nodes, node, qp.x, qp.y, qp.z);
+  }
+  int num = size;
+  if (valid) {
+    if (a.mode == KNN_MODE_LIST) {
+      for (int s = 0; s < K; s++) {
+        bool v = s < num;
+        uint64_t key = v ? h[s * 64] : 0ull;
+        a.out_idx[qi * K + s] = v ? (int32_t)(uint32_t)key : -1;
+        a.out_d2[qi * K + s] = v ? __uint_as_float((uint32_t)(key >> 32)) : -1.0f;
+      }
+      a.out_n[qi] = num;
+    } else {
+      double o0 = 0, o1 = 0, o2 = 0;
+      double maxd2 = kEps;
+      if (num > 0) {
+        // max-heap root = K-th distance (photon_utils.cpp:108-111); r_max^2 if fewer (Q4)
+        maxd2 = (num < K) ? a.rmax * a.rmax : (double)__uint_as_float((uint32_t)(h[0] >> 32));
+        if (num == K && maxd2 < kEps) maxd2 = kEps;
+        if (a.mode == KNN_MODE_IRRADIANCE) {
+          // EstimateIrradiance, photon_utils.cpp:209-246
+          for (int s = 0; s < num; s++) {
+            uint32_t e = a.map.rgbe[(uint32_t)h[s * 64]];
+            uint32_t ex = e >> 24;
+            if (ex) {
+              double inv = ldexp(1.0, (int)ex - 128 - 8);
+              o0 += (double)(e & 255u) * inv;
+              o1 += (double)((e >> 8) & 255u) * inv;
+              o2 += (double)((e >> 16) & 255u) * inv;
+            }
+          }
+          double den = kPi * maxd2;
+          o0 /= den; o1 /= den; o2 /= den;
+        } else {
+          // EstimateRadiance, photon_utils.cpp:113-158
+          const QShade &sh = a.qshade[qi];
+          uint32_t meta = __float_as_uint(qp.w);
+          uint32_t sign = meta & 3u;
+          const DMaterial &m = a.mats[meta >> 2];
+          double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
+          double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
+          bool spec = (m.flags & MF_SPECULAR) || (m.n < 0);
+          double c1 = 1.0, c2 = 1.0, tw = 0;
+          if (a.filter == 1) c1 = 1.0 / (a.fk * sqrt(maxd2));
+          else if (a.filter == 2) {
+            c1 = pow(2.7182818284590452354, -a.fb);
+            c2 = 1.0 / (2.0 * maxd2);
+          }
+          for (int s = 0; s < num; s++) {
+            uint64_t key = h[s * 64];
+            uint32_t id = (uint32_t)key;
+            double d2 = (double)__uint_as_float((uint32_t)(key >> 32));
+            uint32_t dcode = __float_as_uint(a.map.pos4[4 * (int64_t)id + 3]) & 0xffffu;
+            double ix = a.lut[3 * dcode], iy = a.lut[3 * dcode + 1], iz = a.lut[3 * dcode + 2];
+            double perp = N0 * ix + N1 * iy + N2 * iz;
+            if ((sign == 2u && perp < 0) || (sign == 1u && perp > 0)) continue;
+            uint32_t e = a.map.rgbe[id];
+            uint32_t ee = e >> 24;
+            double inv = ee ? ldexp(1.0, (int)ee - 128 - 8) : 0.0;
+            double p0 = ee ? (double)(e & 255u) * inv : 0.0;
+            double p1 = ee ? (double)((e >> 8) & 255u) * inv : 0.0;
+            double p2 = ee ? (double)((e >> 16) & 255u) * inv : 0.0;
+            double ca = E0 * -ix + E1 * -iy + E2 * -iz;
+            if (ca < 0) ca = 0;
+            double ap = fabs(perp);
+            double pw = spec ? pow(ca, m.n) : 0.0;
+            p0 *= ap * m.kd[0] + pw * m.ks[0];
+            p1 *= ap * m.kd[1] + pw * m.ks[1];
+            p2 *= ap * m.kd[2] + pw * m.ks[2];
+            if (a.filter == 1) {
+              double f = (1.0 - c1 * sqrt(d2));
+              p0 *= f; p1 *= f; p2 *= f;
+            } else if (a.filter == 2) {
+              double w = (1.0 - (1.0 - pow(c1, c2 * d2)) / (1.0 - c1));
+              p0 *= w; p1 *= w; p2 *= w;
+              tw += w;
+            }
+            o0 += p0; o1 += p1; o2 += p2;
+          }
+          bool ok = true;
+          if (a.filter == 0 && maxd2 > 0) {
+            double den = kPi * maxd2;
+            o0 /= den; o1 /= den; o2 /= den;
+          } else if (a.filter == 1 && maxd2 > 0) {
+            double den = (1.0 - 2.0 / 3.0 / a.fk) * kPi * maxd2;
+            o0 /= den; o1 /= den; o2 /= den;
+          } else if (a.filter == 2 && tw > 0 && maxd2 > 0) {
+            double sc = a.fa * (num / tw) / (kPi * maxd2);
+            o0 *= sc; o1 *= sc; o2 *= sc;
+          } else {
+            ok = false;
+          }
+          if (ok) {
+            o0 *= sh.w[0]; o1 *= sh.w[1]; o2 *= sh.w[2];
+          } else {
+            o0 = o1 = o2 = 0;
+          }
+        }
+      }
+      a.out[3 * qi] = o0;
+      a.out[3 * qi + 1] = o1;
+      a.out[3 * qi + 2] = o2;
+      if (a.out_n) a.out_n[qi] = num;
+      if (a.out_maxd2) a.out_maxd2[qi] = (num > 0) ? (float)maxd2 : 0.0f;
+    }
+  }
+  if (a.stats) {
+    wave_add(&a.stats[ST_KNN + a.stat_off], valid ? 1ull : 0ull);
+    wave_add(&a.stats[ST_KNN_PHOTONS + a.stat_off], valid ? (uint64_t)num : 0ull);
+    wave_add(&a.stats[ST_KNN_VISITED + a.stat_off], valid ? (uint64_t)visited : 0ull);
+  }
+}
+
+bool launch_knn_lane(const KnnArgs &a, int chunk, int arity, hipStream_t st) {
+  if (a.nq == 0) return true;
+  size_t lds = (size_t)(a.K > 0 ? a.K : 1) * 64 * sizeof(uint64_t);
+  if (lds > 64 * 1024) return false;
+  unsigned grid = (unsigned)((a.nq + 63) / 64);
+  if (arity <= 2) {
+    if (chunk <= 4) knn_lane_kernel<4, 2><<<grid, 64, lds, st>>>(a);
+    else knn_lane_kernel<8, 2><<<grid, 64, lds, st>>>(a);
+  } else if (arity <= 4) {
+    if (chunk <= 4) knn_lane_kernel<4, 4><<<grid, 64, lds, st>>>(a);
+    else knn_lane_kernel<8, 4><<<grid, 64, lds, st>>>(a);
+  } else {
+    if (chunk <= 4) knn_lane_kernel<4, 8><<<grid, 64, lds, st>>>(a);
+    else knn_lane_kernel<8, 8><<<grid, 64, lds, st>>>(a);
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------
+// Packet k-NN: 64 spatially adjacent queries (Morton order) per wave share ONE wave-uniform
+// traversal of the kd-tree, so each node and leaf fetch serves 64 queries. Every lane keeps
+// its own exact max-heap of the K best keys (d2 bits << 32 | photon index) in LDS laid out
+// [slot][lane] (8-B stride across lanes: conflict-free ds_read/write_b64).
+//
+// Exactness: a subtree is skipped only if, for EVERY lane, the query lies on the visited side
+// of the split and diff^2 > that lane's current bound (the single-query rule of
+// R3Kdtree.cpp:740-751 applied per lane), so each lane's result is the same K smallest
+// (d2, index) pairs with d2 <= r2 as the per-query search.
+// Visit order: at each node the packet descends first into the side holding the majority
+// of its queries (recomputed identically on the way up, which makes the walk stackless).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ float rlane(float v, int j) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
 }
 
 __global__ __launch_bounds__(64) void knn_packet_kernel(KnnArgs a) {
@@ -590,6 +844,12 @@ bool launch_knn_packet(const KnnArgs &a, hipStream_t st) {
   unsigned grid = (unsigned)((a.nq + 63) / 64);
   knn_packet_kernel<<<grid, 64, lds, st>>>(a);
   return true;
+}
+
+void launch_list_estimate(const KnnArgs &a, hipStream_t st) {
+  if (a.nq == 0) return;
+  int64_t grid = a.nq < (1 << 16) ? a.nq : (1 << 16);
+  knn_list_estimate_kernel<<<(unsigned)grid, 64, 0, st>>>(a);
 }
 
 bool launch_knn_wave(const KnnArgs &a, int cap_mul, hipStream_t st) {

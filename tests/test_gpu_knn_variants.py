@@ -1,0 +1,88 @@
+"""Every k-NN kernel variant against the oracle (R3Kdtree::FindClosestQuick, R3Kdtree.cpp:
+688-848; EstimateRadiance photon_utils.cpp:72-162).
+
+The variants are chosen when a context is created (gi_host.cpp tuning environment):
+GI_KNN_KERNEL 0 = per-lane LDS heap, 1 = query per wave, 2 = packet, 3 = per-lane with
+batched inserts, 4 = L-lane groups (GI_GROUP_LANES). Each must return the oracle's k-NN sets
+exactly: the fp32 metric is shared, and only photons tied at the k-th distance may differ.
+It must also return its EstimateRadiance within rtol 1e-10 (fp64 sums in a different order).
+Leaf sizes are varied too, because the result set may not depend on the tree shape."""
+import os
+
+import numpy as np
+import pytest
+
+import gi_amd
+import oracle_lib
+import synth
+from gi_amd import GLOBAL, DISK, CONE
+
+pytestmark = pytest.mark.gpu
+
+VARIANTS = [
+    {"GI_KNN_KERNEL": "0", "GI_LEAF_SIZE": "16"},
+    {"GI_KNN_KERNEL": "1", "GI_LEAF_SIZE": "512"},
+    {"GI_KNN_KERNEL": "2"},
+    {"GI_KNN_KERNEL": "3", "GI_LANE_CHUNK": "4"},
+    {"GI_KNN_KERNEL": "3", "GI_LANE_CHUNK": "16", "GI_LEAF_SIZE": "32"},
+    {"GI_KNN_KERNEL": "4", "GI_GROUP_LANES": "8"},
+    {"GI_KNN_KERNEL": "4", "GI_GROUP_LANES": "16", "GI_SEL_SLACK": "1"},
+    {"GI_KNN_KERNEL": "4", "GI_GROUP_LANES": "32", "GI_LEAF_SIZE": "128"},
+]
+
+
+def make_renderer(env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return gi_amd.Renderer(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("env", VARIANTS, ids=lambda e: "-".join(f"{k[3:]}{v}" for k, v in e.items()))
+@pytest.mark.parametrize("n,k,r", [(20000, 50, 2.5), (50000, 225, 0.225), (3000, 50, 0.05),
+                                   (7, 50, 2.5), (100, 1, 0.3)])
+def test_variant_knn_sets(env, n, k, r):
+    r_ = make_renderer(env)
+    try:
+        ph = synth.photon_map(n, seed=n + 1)
+        q = synth.queries(700, seed=k + 3)["point"]
+        r_.set_photon_map(GLOBAL, ph)
+        gi, gd, gn = r_.FindClosestQuick(GLOBAL, q, k, r)
+    finally:
+        r_.close()
+    oi, od, on = oracle_lib.knn(ph, q, k, r)
+    np.testing.assert_array_equal(gn, on)
+    for i in range(len(q)):
+        m = gn[i]
+        np.testing.assert_array_equal(np.sort(gd[i, :m]), od[i, :m])
+        order = np.lexsort((gi[i, :m], gd[i, :m]))
+        got = gi[i, :m][order]
+        mism = got != oi[i, :m]
+        assert np.all(gd[i, :m][order][mism] == od[i, m - 1]), (i, got[mism])
+
+
+@pytest.mark.parametrize("env", VARIANTS, ids=lambda e: "-".join(f"{k[3:]}{v}" for k, v in e.items()))
+@pytest.mark.parametrize("filt,k,r", [(DISK, 50, 2.5), (CONE, 50, 0.3)])
+def test_variant_estimate(env, filt, k, r):
+    r_ = make_renderer(env)
+    try:
+        ph = synth.photon_map(30000, seed=11)
+        q = synth.queries(900, seed=5, k=k, r=r, filt=filt, spec=True)
+        fk = 1.25 if filt == CONE else 1.0
+        p = gi_amd.default_params()
+        p.filter_const_k = fk
+        r_.set_params(p)
+        r_.set_photon_map(GLOBAL, ph)
+        g, gn, gm = r_.EstimateRadiance(GLOBAL, q)
+    finally:
+        r_.close()
+    o, on, om = oracle_lib.estimate_radiance(ph, q, filter_k=fk)
+    np.testing.assert_array_equal(gn, on)
+    np.testing.assert_array_equal(gm, om)
+    np.testing.assert_allclose(g, o, rtol=1e-10, atol=1e-300)

@@ -4,10 +4,14 @@
 Photon maps: cornell.scn, 1M global + 1M caustic photons (bench.py's C2 maps).
 Queries: surface points hit by rays from random points inside the box in random directions
 (the distribution of Monte Carlo bounce vertices), Morton-ordered inside gi_knn_bench.
-Prints one line per (leaf size, map, kernel, mode): ms per launch, ns per query, photons found
-and photons visited per query.
+
+Tuning knobs are environment variables read when a context is created (gi_host.cpp):
+  --env GI_LEAF_SIZE=32,64 --env GI_LANE_CHUNK=4,8   sweeps their cartesian product.
+Prints one line per (knob setting, map, kernel, mode): ms per launch, ns per query, photons
+found and photons visited per query.
 """
 import argparse
+import itertools
 import os
 import sys
 
@@ -20,23 +24,23 @@ sys.path.insert(0, os.path.join(ROOT, "global-illumination_amd"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=4_000_000)
-    ap.add_argument("--leaf", default="64")
-    ap.add_argument("--kernels", default="0,1,2")
+    ap.add_argument("--kernels", default="-1", help="-1 auto, 0 lane(old), 1 wave, 2 packet, 3 lane")
     ap.add_argument("--modes", default="0")
     ap.add_argument("--maps", default="0,1")
     ap.add_argument("--iters", type=int, default=3)
-    ap.add_argument("--capmul", default="1", help="GI_WAVE_CAP_MUL values")
-    ap.add_argument("--slack", default="64", help="GI_SEL_SLACK values")
+    ap.add_argument("--env", action="append", default=[], help="NAME=v1,v2,...")
     a = ap.parse_args()
-    rng = np.random.default_rng(7)
+    names, values = [], []
+    for e in a.env:
+        k, v = e.split("=", 1)
+        names.append(k)
+        values.append(v.split(","))
     scene = os.path.join(ROOT, "tests", "scenes", "cornell.scn")
-    combos = [(lf, cm, sl) for lf in a.leaf.split(",") for cm in a.capmul.split(",")
-              for sl in a.slack.split(",")]
-    for leaf, capmul, slack in combos:
-        os.environ["GI_LEAF_SIZE"] = leaf
-        os.environ["GI_WAVE_CAP_MUL"] = capmul
-        os.environ["GI_SEL_SLACK"] = slack
-        import gi_amd
+    import gi_amd
+    for combo in (itertools.product(*values) if values else [()]):
+        for k, v in zip(names, combo):
+            os.environ[k] = v
+        rng = np.random.default_rng(7)
         args = [scene, "/tmp/x.png", "-global", "1000000", "-caustic", "1000000"]
         p, sc, _o, w, h, aa, real = gi_amd.ParseArgs(args)
         r = gi_amd.Renderer(0, p)
@@ -48,12 +52,13 @@ def main():
         hit, t, pt, nr, mat = r.Intersects(org, d)
         sel = hit != 0
         pt, nr, mat = pt[sel], nr[sel], mat[sel]
+        tag = " ".join(f"{k}={v}" for k, v in zip(names, combo))
         for mp in [int(x) for x in a.maps.split(",")]:
             for kern in [int(x) for x in a.kernels.split(",")]:
                 for mode in [int(x) for x in a.modes.split(",")]:
                     ms, fq, vq = r.knn_bench(mp, pt, nr, mat, mode=mode, kernel=kern,
                                              iters=a.iters)
-                    print(f"leaf={leaf} capmul={capmul} slack={slack} map={mp} kernel={kern} mode={mode} nq={len(pt)} "
+                    print(f"{tag} map={mp} kernel={kern} mode={mode} nq={len(pt)} "
                           f"ms={ms:.2f} ns/q={ms * 1e6 / len(pt):.2f} found={fq:.1f} "
                           f"visited={vq:.1f}", flush=True)
         r.close()

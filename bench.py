@@ -112,12 +112,9 @@ def main():
             rgb, st = r.RenderImage(aa, w, h)
             return st
         import torch
-        img, st = r.render_tiles(aa, w, h, a.tile, rank, world)
+        import gi_dist
         dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
-        t = torch.from_numpy(img).to(dev)
-        dist.reduce(t, dst=0)
-        if rank == 0:
-            t.cpu()
+        _img, st = gi_dist.render_sharded(r, aa, w, h, a.tile, rank, world, dist, dev)
         return st
 
     def barrier():

@@ -212,7 +212,8 @@ struct gi_ctx {
   int knn_qpl = 1;
   int lane_chunk = 8;             // per-lane kernel: photon loads in flight per lane
   int group_lanes = 16;           // group kernel: lanes per query
-  int heap_arity = 4;             // per-lane kernel: d-ary heap                // per-lane kernel: sorted queries per lane (bound reuse)       // per-lane kernel: heap in global memory even for K <= 64           // query-per-wave kernel: candidate buffer = mul * pow2(K+64)
+  int heap_arity = 4;             // per-lane kernel: d-ary heap
+  int ind_waves = 2;              // indirect-path kernel occupancy target                // per-lane kernel: sorted queries per lane (bound reuse)       // per-lane kernel: heap in global memory even for K <= 64           // query-per-wave kernel: candidate buffer = mul * pow2(K+64)
   // render scratch
   DBuf spawn, npaths, path_off, nmc, mc_off, nind, ind_off, base, pixels, rgbf, rgb8, gheap_d2, gheap_idx, qcount, stats_bak;
   DBuf qpos[2], qshade[2], qkey[2], qout[2];
@@ -619,6 +620,8 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     a.out_w = w;
     a.nprim = nprim;
     a.stats = c->d_stats.as<unsigned long long>();
+    a.ind_waves = c->ind_waves;
+    if (const char *s = getenv("GI_DBG")) a.dbg = atoi(s);
     HIPCHK(c, c->spawn.ensure((size_t)nprim * sizeof(Spawn)));
     HIPCHK(c, c->npaths.ensure((size_t)nprim * 4));
     HIPCHK(c, c->path_off.ensure((size_t)(nprim + 1) * 4));
@@ -657,9 +660,13 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     uint32_t nq[2] = {0, 0};
     HIPCHK(c, hipMemcpyAsync(c->stats_bak.p, c->d_stats.p, ST_COUNT * 8,
                              hipMemcpyDeviceToDevice, c->stream));
+    // deterministic slots: [0, nprim) per primary sample, then (global list) one per
+    // indirect path; Monte Carlo paths append after qbase[l]
+    uint32_t qbase[2] = {(uint32_t)(nprim + a.total_ind), (uint32_t)nprim};
+    a.qind_base = nprim;
     for (int attempt = 0; attempt < 3; attempt++) {
       for (int l = 0; l < 2; l++) {
-        size_t cap = std::max<size_t>(c->qcap_hint[l], 1024);
+        size_t cap = std::max<size_t>(c->qcap_hint[l], (size_t)qbase[l] + 1024);
         HIPCHK(c, c->qpos[l].ensure(cap * 16));
         HIPCHK(c, c->qshade[l].ensure(cap * sizeof(QShade)));
         HIPCHK(c, c->qkey[l].ensure(cap * 8));
@@ -669,7 +676,7 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
         a.qcap[l] = (uint32_t)std::min<size_t>(cap, 0xFFFFFFF0u);
       }
       a.qcount = c->qcount.as<uint32_t>();
-      HIPCHK(c, hipMemsetAsync(c->qcount.p, 0, 8, c->stream));
+      HIPCHK(c, hipMemcpyAsync(c->qcount.p, qbase, 8, hipMemcpyHostToDevice, c->stream));
       launch_path(a, c->stream);
       HIPCHK(c, hipGetLastError());
       HIPCHK(c, hipMemcpyAsync(nq, c->qcount.p, 8, hipMemcpyDeviceToHost, c->stream));
@@ -766,6 +773,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_LANE_CHUNK")) c->lane_chunk = std::max(1, atoi(s));
   if (const char *s = getenv("GI_GROUP_LANES")) c->group_lanes = std::max(1, atoi(s));
   if (const char *s = getenv("GI_HEAP_ARITY")) c->heap_arity = std::max(2, atoi(s));
+  if (const char *s = getenv("GI_IND_WAVES")) c->ind_waves = std::max(1, atoi(s));
   if (const char *s = getenv("GI_SORT_QUERIES")) c->sort_queries = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_KERNEL")) c->knn_kernel_kind = atoi(s);
   *out = c;

@@ -61,9 +61,15 @@ struct RenderArgs {
   const uint32_t *mc_off;
   const uint32_t *ind_off;
   int64_t total_mc, total_ind;
-  // query lists (0 = global map, 1 = caustic map): appended with an atomic counter; each
-  // query carries key = path_slot << 20 | index-in-path so the per-pixel reduction can sum
-  // them in a deterministic order after a key sort
+  int32_t ind_waves;    // occupancy target of the indirect-path kernel (waves per SIMD)
+  int32_t dbg;          // diagnostics: 1 = skip the indirect trace, 2 = skip diffuse sampling too
+  int64_t qind_base;    // global list: indirect path t owns slot qind_base + t
+  // query lists (0 = global map, 1 = caustic map). Deterministic slots first: list l slot p
+  // = primary sample p's own query (slot-0 path), then (global list only) slot
+  // qind_base + t = indirect path t's single query; unused ones hold QMETA_NONE. Monte Carlo
+  // paths append after those with a wave-aggregated atomic counter. Each query carries key =
+  // path_slot << 20 | index-in-path so the per-pixel reduction can sum them in a
+  // deterministic order after a key sort (empty slots: key ~0).
   float4 *qpos[2];
   QShade *qshade[2];
   uint64_t *qkey[2];
@@ -122,6 +128,9 @@ __device__ __forceinline__ void wave_add(unsigned long long *dst, uint64_t v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, (unsigned long long)v);
 }
+
+// query-list slot with no query (deterministic slots a path did not use): qpos.w bits
+constexpr uint32_t QMETA_NONE = 0xffffffffu;
 
 enum { KNN_MODE_RADIANCE = 0, KNN_MODE_IRRADIANCE = 1, KNN_MODE_LIST = 2 };
 

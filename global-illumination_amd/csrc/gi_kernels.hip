@@ -166,23 +166,35 @@ struct PathCtx {
   uint32_t j;       // queries issued so far by this path
   C3 base;
   Counts cnt;
+  int64_t fixed[2]; // deterministic query slot per list (>= 0), -1 append, -2 used
 };
+
+__device__ __forceinline__ void put_none(const RenderArgs &a, int list, int64_t slot) {
+  a.qpos[list][slot] = make_float4(0.f, 0.f, 0.f, __uint_as_float(QMETA_NONE));
+  a.qkey[list][slot] = ~0ull;
+}
 
 // append one photon-map query (list 0 = global, 1 = caustic): search half (point as f32 +
 // meta) and shading half (normal, exact bounce, path weight)
 __device__ __forceinline__ void put_query(PathCtx &P, int list, V p, V n, V ex, double ct,
                                           int mat, C3 w) {
   const RenderArgs &a = *P.A;
-  // one atomic per wave for all lanes that emit here (a single counter word serialises
-  // ~10^8 atomics/s, MI355X_MICROARCH.md 'dequeue')
-  uint64_t act = __ballot(1);
-  int lane = (int)(threadIdx.x & 63);
-  int leader = __ffsll((long long)act) - 1;
-  uint32_t rank = (uint32_t)__popcll(act & ((1ull << lane) - 1ull));
-  uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(&a.qcount[list], (uint32_t)__popcll(act));
-  base = (uint32_t)__shfl((int)base, leader, 64);
-  uint32_t slot = base + rank;
+  uint32_t slot;
+  if (P.fixed[list] >= 0) {
+    slot = (uint32_t)P.fixed[list];
+    P.fixed[list] = -2;
+  } else {
+    // one atomic per wave for all lanes that emit here (a single counter word serialises
+    // ~10^8 atomics/s, MI355X_MICROARCH.md 'dequeue')
+    uint64_t act = __ballot(1);
+    int lane = (int)(threadIdx.x & 63);
+    int leader = __ffsll((long long)act) - 1;
+    uint32_t rank = (uint32_t)__popcll(act & ((1ull << lane) - 1ull));
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&a.qcount[list], (uint32_t)__popcll(act));
+    base = (uint32_t)__shfl((int)base, leader, 64);
+    slot = base + rank;
+  }
   uint64_t key = (P.g << 20) | (uint64_t)(P.j++);
   if (slot >= a.qcap[list]) return;  // overflow: the host grows the lists and re-runs
   uint32_t sign = (ct > 0) ? 1u : ((ct < 0) ? 2u : 0u);
@@ -345,6 +357,7 @@ __device__ __forceinline__ void path_init(PathCtx &P, const RenderArgs &a, int64
   P.base = rgb(0, 0, 0);
   Counts z = {0, 0, 0, 0, 0, 0};
   P.cnt = z;
+  P.fixed[0] = P.fixed[1] = -1;
 }
 
 __device__ __forceinline__ void path_stats(const RenderArgs &a, const Counts &cnt) {
@@ -370,6 +383,7 @@ __global__ __launch_bounds__(256) void slot0_kernel(RenderArgs a) {
     const Spawn &sp = a.spawn[b];
     PathCtx P;
     path_init(P, a, g);
+    P.fixed[0] = P.fixed[1] = b;
     P.base = ldc(sp.base);
     if (sp.hit) {
       V p = ld3(sp.p), n = ld3(sp.n), view = ld3(sp.v);
@@ -380,6 +394,8 @@ __global__ __launch_bounds__(256) void slot0_kernel(RenderArgs a) {
       }
       if (sp.q_glob) put_query(P, 0, p, n, ex, sp.ct, sp.mat, rgb(1, 1, 1));
     }
+    if (P.fixed[0] >= 0) put_none(a, 0, b);
+    if (P.fixed[1] >= 0) put_none(a, 1, b);
     a.base[3 * g] = P.base.r;
     a.base[3 * g + 1] = P.base.g;
     a.base[3 * g + 2] = P.base.b;
@@ -389,7 +405,8 @@ __global__ __launch_bounds__(256) void slot0_kernel(RenderArgs a) {
 }
 
 // IndirectIllumination sample s of primary pb (raytracer.cpp:112-135)
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void ind_kernel(RenderArgs a) {
+template <int W>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void ind_kernel(RenderArgs a) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   Counts cnt = {0, 0, 0, 0, 0, 0};
   if (t < a.total_ind) {
@@ -403,11 +420,14 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void i
     const DMaterial &m = a.S.mats[sp.mat];
     PathCtx P;
     path_init(P, a, g);
+    P.fixed[0] = a.qind_base + t;  // at most one (global) query per indirect path
     Rng rng;
     rng.init(a.F.seed, KIND_IND, psample, (uint64_t)s);
     V p = ld3(sp.p), n = ld3(sp.n);
-    V sb = diffuse_sample(n, sp.ct, rng);
-    mc_indirect_body(P, p + sb * kEps, sb, rng, ldc(m.kd) / (double)sp.n_i);
+    V sb = (a.dbg >= 2) ? n : diffuse_sample(n, sp.ct, rng);
+    if (a.dbg == 0) mc_indirect_body(P, p + sb * kEps, sb, rng, ldc(m.kd) / (double)sp.n_i);
+    else P.base = rgb(sb.x, sb.y, sb.z);
+    if (P.fixed[0] >= 0) put_none(a, 0, P.fixed[0]);
     P.cnt.indirect++;
     a.base[3 * g] = P.base.r;
     a.base[3 * g + 1] = P.base.g;
@@ -614,6 +634,7 @@ __global__ __launch_bounds__(64) void knn_kernel(KnnArgs a) {
     int64_t qg = a.q0 + q;
     int64_t qi = a.perm ? (int64_t)a.perm[qg] : qg;
     float4 qp = a.qpos[qi];
+    if (__float_as_uint(qp.w) == QMETA_NONE) continue;  // empty deterministic slot
     float bound = a.r2f;
     if (pk2 >= 0.0f) {
       double dx = (double)qp.x - px, dy = (double)qp.y - py, dz = (double)qp.z - pz;
@@ -743,9 +764,9 @@ __global__ __launch_bounds__(64) void knn_kernel(KnnArgs a) {
 __global__ __launch_bounds__(64) void cached_kernel(KnnArgs a) {
   int64_t q = (int64_t)blockIdx.x * 64 + threadIdx.x;
   uint64_t nq_done = 0;
-  if (q < a.nq) {
-    nq_done = 1;
+  if (q < a.nq && __float_as_uint(a.qpos[q].w) != QMETA_NONE) {
     float4 qp = a.qpos[q];
+    nq_done = 1;
     const QShade &sh = a.qshade[q];
     uint32_t meta = __float_as_uint(qp.w);
     uint32_t sign = meta & 3u;
@@ -1090,7 +1111,13 @@ void launch_primary(const RenderArgs &a, hipStream_t st) {
 }
 void launch_path(const RenderArgs &a, hipStream_t st) {
   if (a.nprim > 0) slot0_kernel<<<nblk(a.nprim, 256), 256, 0, st>>>(a);
-  if (a.total_ind > 0) ind_kernel<<<nblk(a.total_ind, 128), 128, 0, st>>>(a);
+  if (a.total_ind > 0) {
+    unsigned g = nblk(a.total_ind, 128);
+    if (a.ind_waves <= 1) ind_kernel<1><<<g, 128, 0, st>>>(a);
+    else if (a.ind_waves == 2) ind_kernel<2><<<g, 128, 0, st>>>(a);
+    else if (a.ind_waves == 3) ind_kernel<3><<<g, 128, 0, st>>>(a);
+    else ind_kernel<4><<<g, 128, 0, st>>>(a);
+  }
   if (a.total_mc > 0) mc_kernel<<<nblk(a.total_mc, 128), 128, 0, st>>>(a);
 }
 void launch_reduce(const RenderArgs &a, hipStream_t st) {

@@ -136,6 +136,10 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
     int64_t qg = a.q0 + qq;
     int64_t qi = a.perm ? (int64_t)a.perm[qg] : qg;
     float4 qp = a.qpos[qi];
+    if (__float_as_uint(qp.w) == QMETA_NONE) {  // empty deterministic slot
+      if (lane == 0) a.list_n[qi] = 0;
+      continue;
+    }
     float qx = ffirst(qp.x), qy = ffirst(qp.y), qz = ffirst(qp.z);
     uint32_t count = 0;
     // keys accepted while key < thr; start: every d2 <= r2
@@ -437,13 +441,14 @@ __global__ __launch_bounds__(64) void knn_lane_kernel(KnnArgs a) {
   const int L = a.map.nleaves;
   const int64_t N = a.map.n;
   const int64_t q = (int64_t)blockIdx.x * 64 + lane;
-  const bool valid = q < a.nq;
+  bool valid = q < a.nq;
   int64_t qi = 0;
   float4 qp = make_float4(0.f, 0.f, 0.f, 0.f);
   if (valid) {
     int64_t qg = a.q0 + q;
     qi = a.perm ? (int64_t)a.perm[qg] : qg;
     qp = a.qpos[qi];
+    valid = __float_as_uint(qp.w) != QMETA_NONE;  // empty deterministic slot
   }
   int size = 0;
   // accept key < lim; start: every d2 <= r2
@@ -652,13 +657,14 @@ __global__ __launch_bounds__(64) void knn_packet_kernel(KnnArgs a) {
   const int64_t N = a.map.n;
   const int K = a.K;
   const int64_t q = (int64_t)blockIdx.x * 64 + lane;
-  const bool valid = q < a.nq;
+  bool valid = q < a.nq;
   int64_t qi = 0;
   float4 qp = make_float4(0.f, 0.f, 0.f, 0.f);
   if (valid) {
     int64_t qg = a.q0 + q;
     qi = a.perm ? (int64_t)a.perm[qg] : qg;
     qp = a.qpos[qi];
+    valid = __float_as_uint(qp.w) != QMETA_NONE;
   }
   int size = 0;
   uint64_t thr = valid ? ((uint64_t)__float_as_uint(a.r2f) << 32) + 0x100000000ull : 0ull;

@@ -143,13 +143,17 @@ __global__ __launch_bounds__(64) void knn_group_kernel(KnnArgs a) {
   uint64_t st_q = 0, st_found = 0, st_vis = 0;
   for (int64_t base = (int64_t)blockIdx.x * G; base < a.nq; base += (int64_t)gridDim.x * G) {
     const int64_t qq = base + g;
-    const bool valid = qq < a.nq;
+    bool valid = qq < a.nq;
     int64_t qi = 0;
     float4 qp = make_float4(0.f, 0.f, 0.f, 0.f);
     if (valid) {
       int64_t qg = a.q0 + qq;
       qi = a.perm ? (int64_t)a.perm[qg] : qg;
       qp = a.qpos[qi];
+      if (__float_as_uint(qp.w) == QMETA_NONE) {  // empty deterministic slot
+        if (r == 0) a.list_n[qi] = 0;
+        valid = false;
+      }
     }
     uint32_t count = 0, visited = 0;
     uint64_t thr = ((uint64_t)__float_as_uint(a.r2f) + 1ull) << 32;  // accept key < thr

@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 import gi_amd
+import gi_dist
 import oracle_lib
 
 pytestmark = pytest.mark.gpu
@@ -103,7 +104,11 @@ def test_tiles_compose_full_image(renderer):
     renderer.ReadScene(sc)
     full, ff, _ = renderer.RenderImage(aa, w, h, want_float=True)
     acc = np.zeros((h, w, 3), dtype=np.float32)
+    owner = gi_dist.tile_owner_map(w, h, 16, 3)
     for s in range(3):
         part, _ = renderer.render_tiles(aa, w, h, 16, s, 3)
+        # the shard touches exactly the pixels gi_dist assigns to it (bench.py's gather)
+        assert not part[owner != s].any()
+        np.testing.assert_array_equal(part[owner == s], ff[owner == s])
         acc += part
     np.testing.assert_array_equal(acc, ff)

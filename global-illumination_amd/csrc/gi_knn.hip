@@ -700,14 +700,7 @@ __global__ __launch_bounds__(64) void knn_packet_kernel(KnnArgs a) {
             if (d2 <= pr) {
               uint64_t key = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)(uint32_t)(b + j);
               if (key < thr) {
-                if (size < K) {
-                  kheap_push(h, size, key);
-                  size++;
-                  if (size == K) thr = h[0];
-                } else {
-                  kheap_replace_top(h, size, key);
-                  thr = h[0];
-                }
+                heapn_accept<4>(h, size, K, key, thr);
                 if (size == K) pr = __uint_as_float((uint32_t)(thr >> 32));
               }
             }

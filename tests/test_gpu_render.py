@@ -112,3 +112,25 @@ def test_tiles_compose_full_image(renderer):
         np.testing.assert_array_equal(part[owner == s], ff[owner == s])
         acc += part
     np.testing.assert_array_equal(acc, ff)
+
+
+# Full-GI parity on the other BASELINE configs, shrunk to oracle-friendly sizes:
+# C3 jensen (rect light with soft shadows + glass caustics), C4 stilllife (boxes and meshes under
+# translate nodes, 4 point lights), C5 teapot (1,452-triangle mesh, depth of field).
+@pytest.mark.parametrize("name,extra,exact", [
+    ("jensen.scn", ["-global", "4000", "-caustic", "20000", "-lt", "4", "-ss", "4", "-it", "16"],
+     0.95),
+    ("stilllife.scn", ["-global", "20000", "-no_caustic", "-it", "16"], 0.95),
+    ("teapot.scn", ["-global", "20000", "-no_caustic", "-it", "8", "-dof", "2", "8.0", "0.05"],
+     0.95),
+])
+def test_full_gi_configs_match_oracle(renderer, name, extra, exact):
+    args = [scene(name), "/tmp/x.png", "-resolution", "20", "20", "-aa", "0", "-tt", "8",
+            "-st", "8", "-seed", "9"] + extra
+    g, gst, gp = run_gpu(renderer, args)
+    o, ost = oracle_lib.render(args, 20, 20)
+    if gp is not None:
+        assert gp["global_stored"] == ost["global_stored"]
+        assert gp["caustic_stored"] == ost["caustic_stored"]
+    assert gst["screen_rays"] == ost["screen_rays"]
+    compare(g, o, exact, 0.99, 0.5)

@@ -225,6 +225,98 @@ GI_HD bool ray_circle(V o, V d, V c, V n, double r, double &t, V &p) {
   return true;
 }
 
+// R3Intersects(ray, plane, NULL, &t), R3Isect.cpp:700-732: a ray lying in the plane counts
+// as an intersection and leaves t unchanged.
+GI_HD bool ray_plane_t(V o, V d, V n, double pd, double &t) {
+  double denom = dot(n, d);
+  double sd = o.x * n.x + o.y * n.y + o.z * n.z + pd;  // R3SignedDistance, R3Dist.cpp:603-607
+  if (isZero(denom)) return isZero(sd);
+  double s = -(sd) / denom;
+  if (isNeg(s)) return false;
+  t = s;
+  return true;
+}
+
+// R3Intersects(ray, R3Cylinder), R3Isect.cpp:1025-1200 (Graphics Gems IV p.356): cylinder
+// p1 -> p2 (unit axis, R3Span.cpp:63-70), radius r, cap planes through p1 (normal -A) and p2
+// (normal +A) (R3Cylinder / R3Circle / R3Plane constructors). `line` is a radius-1e-3
+// cylinder (R3Scene.cpp:1667-1687).
+GI_HD bool ray_cylinder(V o, V R, V p1, V p2, double radius, double &t_out, V &p_out, V &n_out) {
+  const double INF = 1.0e6;  // RN_INFINITY
+  V A = p2 - p1;
+  double alen = len(A);
+  if (!isZero(alen)) A = A / alen;
+  V nT = A, nB = -A;
+  double dT = -(nT.x * p2.x + nT.y * p2.y + nT.z * p2.z);
+  double dB = -(nB.x * p1.x + nB.y * p1.y + nB.z * p1.z);
+  double cyl_t1, cyl_t2;
+  V D = cross(R, A);
+  double a = len(D);
+  if (isZero(a)) {
+    double d = len(cross(A, p1 - o));  // R3Distance(point, line), R3Dist.cpp:59-65
+    if (!isNegOrZero(d - radius)) return false;
+    cyl_t1 = 0.0;
+    cyl_t2 = INF;
+  } else {
+    D = D / a;
+    V RC = o - p1;
+    double d = dot(RC, D);
+    if (d < 0.0) d = -d;
+    if (isPos(d - radius)) return false;
+    double t = dot(cross(RC, A), D) / -a;
+    double s;
+    V O = normalize(cross(D, A));
+    double b = radius * radius - d * d;
+    if (isPos(b)) {
+      double e = dot(R, O);
+      s = sqrt(b) / e;
+      if (s < 0.0) s = -s;
+    } else {
+      s = 0.0;
+    }
+    cyl_t2 = t + s;
+    if (isNeg(cyl_t2)) return false;
+    cyl_t1 = t - s;
+    if (cyl_t1 < 0.0) cyl_t1 = 0.0;
+  }
+  double cap_t1 = 0, cap_t2 = 0;
+  double dv = dot(R, A);
+  double d_top = o.x * nT.x + o.y * nT.y + o.z * nT.z + dT;
+  double d_base = o.x * nB.x + o.y * nB.y + o.z * nB.z + dB;
+  if (isPos(d_top)) {
+    if (isPosOrZero(dv)) return false;
+    if (ray_plane_t(o, R, nT, dT, cap_t1) && isPos(cap_t1 - cyl_t2)) return false;
+    else if (ray_plane_t(o, R, -nB, -dB, cap_t2) && isNeg(cap_t2 - cyl_t1)) return false;
+    else if (isPos(cap_t1 - cyl_t1)) {
+      t_out = cap_t1;
+      p_out = o + R * cap_t1;
+      n_out = nT;
+      return true;
+    }
+  } else if (isPos(d_base)) {
+    if (isNegOrZero(dv)) return false;
+    if (ray_plane_t(o, R, nB, dB, cap_t1) && isPos(cap_t1 - cyl_t2)) return false;
+    else if (ray_plane_t(o, R, -nT, -dT, cap_t2) && isNeg(cap_t2 - cyl_t1)) return false;
+    else if (isPos(cap_t1 - cyl_t1)) {
+      t_out = cap_t1;
+      p_out = o + R * cap_t1;
+      n_out = nB;
+      return true;
+    }
+  } else {
+    if (isPos(dv)) {
+      if (ray_plane_t(o, R, -nT, -dT, cap_t1) && isNeg(cap_t1 - cyl_t1)) return false;
+    } else if (isNeg(dv)) {
+      if (ray_plane_t(o, R, -nB, -dB, cap_t1) && isNeg(cap_t1 - cyl_t1)) return false;
+    }
+  }
+  t_out = cyl_t1;
+  p_out = o + R * cyl_t1;
+  V HB = p_out - p1;
+  n_out = (HB - dot(HB, A) * A) / radius;
+  return true;
+}
+
 // R3Shape::Intersects dispatch (R3Shape.cpp:328-329); SK_MESH is R3Intersects(ray,
 // R3TriangleArray) (R3Isect.cpp:800-833): min t over ALL triangles, t >= -1e-6 allowed (Q2).
 __device__ __forceinline__ bool shape_intersect(const SceneView &S, const DShape &sh, V o, V d,
@@ -271,6 +363,8 @@ __device__ __forceinline__ bool shape_intersect(const SceneView &S, const DShape
       if (!ray_circle(o, d, ld3(sh.c), ld3(sh.n), sh.r, t, p)) return false;
       n = ld3(sh.n);
       return true;
+    case SK_CYLINDER:  // c = p1, n = p2
+      return ray_cylinder(o, d, ld3(sh.c), ld3(sh.n), sh.r, t, p, n);
     default:
       return false;
   }

@@ -734,7 +734,7 @@ int check_ready(gi_ctx *c) {
     return fail(c, GI_ERR_UNSUPPORTED, "scene graph deeper than 16 levels");
   if (c->scene.unsupported_shapes)
     return fail(c, GI_ERR_UNSUPPORTED,
-                "scene contains cylinder/cone/line shapes: not yet on the device path");
+                "scene contains cone shapes: not yet on the device path");
   return GI_OK;
 }
 

@@ -329,9 +329,8 @@ static bool parse(Graph &G, int root, const std::string &file, bool real, std::s
       for (int i = 0; i < 3; i++) {
         s.s.c[i] = v[i];
         s.s.n[i] = n.v[i];
-        double ext = v[6] * sqrt(std::max(0.0, 1.0 - n.v[i] * n.v[i]));
-        s.s.bmin[i] = v[i] - ext;
-        s.s.bmax[i] = v[i] + ext;
+        s.s.bmin[i] = v[i] - v[6];  // R3Circle::BBox: centre +- radius (R3Circle.cpp:179-184)
+        s.s.bmax[i] = v[i] + v[6];
       }
       s.s.r = v[6];
       if (!add_shape(m, std::move(s))) return bad("material id");
@@ -342,17 +341,26 @@ static bool parse(Graph &G, int root, const std::string &file, bool real, std::s
       GShape s;
       memset(&s.s, 0, sizeof s.s);
       s.s.kind = !strcmp(cmd, "cone") ? SK_CONE : SK_CYLINDER;
-      Bx bx;
+      // cylinder/cone (R3Scene.cpp:1589-1636): p1/p2 = c -/+ 0.5*h*(0,1,0);
+      // line (:1667-1687): R3Cylinder(p1, p2, RN_BIG_EPSILON = 1e-3)
+      double p1[3], p2[3], rad;
       if (line) {
-        bx.add(v);
-        bx.add(v + 3);
+        for (int i = 0; i < 3; i++) { p1[i] = v[i]; p2[i] = v[3 + i]; }
+        rad = 1e-3;
       } else {
-        double lo[3] = {v[0] - v[3], v[1] - 0.5 * v[4], v[2] - v[3]};
-        double hi[3] = {v[0] + v[3], v[1] + 0.5 * v[4], v[2] + v[3]};
-        bx.add(lo);
-        bx.add(hi);
+        for (int i = 0; i < 3; i++) p1[i] = p2[i] = v[i];
+        p1[1] = v[1] - 0.5 * v[4];
+        p2[1] = v[1] + 0.5 * v[4];
+        rad = v[3];
       }
-      for (int i = 0; i < 3; i++) { s.s.bmin[i] = bx.mn[i]; s.s.bmax[i] = bx.mx[i]; }
+      s.s.r = rad;
+      for (int i = 0; i < 3; i++) {
+        s.s.c[i] = p1[i];
+        s.s.n[i] = p2[i];
+        // R3Cylinder::BBox: union of the cap circles' centre +- radius cubes
+        s.s.bmin[i] = std::min(p1[i] - rad, p2[i] - rad);
+        s.s.bmax[i] = std::max(p1[i] + rad, p2[i] + rad);
+      }
       if (!add_shape(m, std::move(s))) return bad("material id");
     } else if (!strcmp(cmd, "mesh")) {
       char name[256];
@@ -528,7 +536,7 @@ static Bx flatten(Graph &G, int gi_idx, int parent, HostScene &S) {
         ds.tri_count = (int)s.tris.size();
         S.tris.insert(S.tris.end(), s.tris.begin(), s.tris.end());
       }
-      if (s.s.kind == SK_CYLINDER || s.s.kind == SK_CONE) S.unsupported_shapes = true;
+      if (s.s.kind == SK_CONE) S.unsupported_shapes = true;
       S.shapes.push_back(ds);
       eb.add(s.s.bmin);
       eb.add(s.s.bmax);

@@ -19,7 +19,7 @@ struct HostScene {
   double ambient[3] = {0, 0, 0}, background[3] = {0, 0, 0};
   double bmin[3], bmax[3];
   double radius = 0, centroid[3] = {0, 0, 0};
-  bool unsupported_shapes = false;  // cylinder / cone present
+  bool unsupported_shapes = false;  // cone present
   bool unsupported_depth = false;   // scene graph deeper than GI_MAX_DEPTH
 };
 

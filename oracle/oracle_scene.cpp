@@ -154,6 +154,109 @@ static bool ray_circle(V3 org, V3 dir, V3 c, V3 n, double r, double &t, V3 &poin
   return true;
 }
 
+// R3Cylinder::BBox (R3Cylinder.cpp:175-181): union of the cap circles' boxes, each the cube
+// centre +- radius (R3Circle.cpp:179-184)
+static void cap_cubes_box(Shape &sh) {
+  for (int i = 0; i < 3; i++) {
+    sh.box.mn[i] = fmin(sh.c[i] - sh.r, sh.axis[i] - sh.r);
+    sh.box.mx[i] = fmax(sh.c[i] + sh.r, sh.axis[i] + sh.r);
+  }
+}
+
+// R3Intersects(ray, plane, NULL, &t), R3Isect.cpp:700-732. A ray lying in the plane counts as
+// an intersection and leaves t unchanged (the caller's cap_t stays at its initial 0).
+static bool ray_plane_t(V3 o, V3 d, V3 n, double pd, double &t) {
+  double denom = dot(n, d);
+  double sd = o.x * n.x + o.y * n.y + o.z * n.z + pd;  // R3SignedDistance, R3Dist.cpp:603-607
+  if (isZero(denom)) return isZero(sd);
+  double s = -(sd) / denom;
+  if (isNeg(s)) return false;
+  t = s;
+  return true;
+}
+
+// R3Intersects(ray, R3Cylinder), R3Isect.cpp:1025-1200 (Graphics Gems IV p.356) for the
+// cylinder p1 -> p2 (axis R3Span: unit vector, R3Span.cpp:63-70), radius r; caps are the
+// planes through p1 (normal -A) and p2 (normal +A) (R3Cylinder.cpp constructors,
+// R3Circle.cpp:78-83, R3Plane.cpp:85-90).
+static bool ray_cylinder(V3 o, V3 R, V3 p1, V3 p2, double radius, double &t_out, V3 &p_out,
+                         V3 &n_out) {
+  const double INF = 1.0e6;  // RN_INFINITY
+  V3 A = p2 - p1;
+  double alen = length(A);
+  if (!isZero(alen)) A = A / alen;
+  V3 nT = A, nB = -A;
+  double dT = -(nT.x * p2.x + nT.y * p2.y + nT.z * p2.z);
+  double dB = -(nB.x * p1.x + nB.y * p1.y + nB.z * p1.z);
+  double cyl_t1, cyl_t2;
+  V3 D = cross(R, A);
+  double a = length(D);
+  if (isZero(a)) {
+    // parallel: R3Distance(point, line), R3Dist.cpp:59-65
+    double d = length(cross(A, p1 - o));
+    if (!isNegOrZero(d - radius)) return false;
+    cyl_t1 = 0.0;
+    cyl_t2 = INF;
+  } else {
+    D = D / a;
+    V3 RC = o - p1;
+    double d = dot(RC, D);
+    if (d < 0.0) d = -d;
+    if (isPos(d - radius)) return false;
+    double t = dot(cross(RC, A), D) / -a;
+    double s;
+    V3 O = normalize(cross(D, A));
+    double b = radius * radius - d * d;
+    if (isPos(b)) {
+      double e = dot(R, O);
+      s = sqrt(b) / e;
+      if (s < 0.0) s = -s;
+    } else {
+      s = 0.0;
+    }
+    cyl_t2 = t + s;
+    if (isNeg(cyl_t2)) return false;
+    cyl_t1 = t - s;
+    if (cyl_t1 < 0.0) cyl_t1 = 0.0;
+  }
+  double cap_t1 = 0, cap_t2 = 0;
+  double dv = dot(R, A);
+  double d_top = o.x * nT.x + o.y * nT.y + o.z * nT.z + dT;
+  double d_base = o.x * nB.x + o.y * nB.y + o.z * nB.z + dB;
+  if (isPos(d_top)) {
+    if (isPosOrZero(dv)) return false;
+    if (ray_plane_t(o, R, nT, dT, cap_t1) && isPos(cap_t1 - cyl_t2)) return false;
+    else if (ray_plane_t(o, R, -nB, -dB, cap_t2) && isNeg(cap_t2 - cyl_t1)) return false;
+    else if (isPos(cap_t1 - cyl_t1)) {
+      t_out = cap_t1;
+      p_out = o + R * cap_t1;
+      n_out = nT;
+      return true;
+    }
+  } else if (isPos(d_base)) {
+    if (isNegOrZero(dv)) return false;
+    if (ray_plane_t(o, R, nB, dB, cap_t1) && isPos(cap_t1 - cyl_t2)) return false;
+    else if (ray_plane_t(o, R, -nT, -dT, cap_t2) && isNeg(cap_t2 - cyl_t1)) return false;
+    else if (isPos(cap_t1 - cyl_t1)) {
+      t_out = cap_t1;
+      p_out = o + R * cap_t1;
+      n_out = nB;
+      return true;
+    }
+  } else {
+    if (isPos(dv)) {
+      if (ray_plane_t(o, R, -nT, -dT, cap_t1) && isNeg(cap_t1 - cyl_t1)) return false;
+    } else if (isNeg(dv)) {
+      if (ray_plane_t(o, R, -nB, -dB, cap_t1) && isNeg(cap_t1 - cyl_t1)) return false;
+    }
+  }
+  t_out = cyl_t1;
+  p_out = o + R * cyl_t1;
+  V3 HB = p_out - p1;
+  n_out = (HB - dot(HB, A) * A) / radius;
+  return true;
+}
+
 // R3Shape::Intersects virtual dispatch (R3Shape.cpp:328-329 -> R3Isect.cpp)
 static bool shape_intersect(const Shape &sh, V3 org, V3 dir, double &t, V3 &point, V3 &normal) {
   switch (sh.type) {
@@ -198,8 +301,10 @@ static bool shape_intersect(const Shape &sh, V3 org, V3 dir, double &t, V3 &poin
       if (!ray_circle(org, dir, sh.c, sh.axis, sh.r, t, point)) return false;
       normal = sh.axis;
       return true;
+    case SH_CYLINDER:
+      return ray_cylinder(org, dir, sh.c, sh.axis, sh.r, t, point, normal);
     default:
-      return false;  // cylinder / cone: not on the config path
+      return false;  // cone: used by no input scene
   }
 }
 
@@ -505,11 +610,10 @@ static bool read_princeton(Scene &s, int root_node, const std::string &filename,
       sh.c = V3(c[0], c[1], c[2]);
       sh.axis = normalize(V3(d[0], d[1], d[2]));
       sh.r = r;
-      // R3Circle::BBox: conservative square around the disk
+      // R3Circle::BBox (R3Circle.cpp:179-184): the cube centre +- radius
       for (int i = 0; i < 3; i++) {
-        double ext = r * sqrt(fmax(0.0, 1.0 - sh.axis[i] * sh.axis[i]));
-        sh.box.mn[i] = c[i] - ext;
-        sh.box.mx[i] = c[i] + ext;
+        sh.box.mn[i] = c[i] - r;
+        sh.box.mx[i] = c[i] + r;
       }
       if (!resolve(m, el)) return fail("material id");
       el->shapes.push_back(sh);
@@ -519,12 +623,12 @@ static bool read_princeton(Scene &s, int root_node, const std::string &filename,
       if (fscanf(fp, "%d%lf%lf%lf%lf%lf", &m, &c[0], &c[1], &c[2], &r, &h) != 6)
         return fail(cmd);
       Shape sh;
+      // R3Scene.cpp:1589-1636: p1/p2 = c -/+ 0.5*h*(0,1,0)
       sh.type = !strcmp(cmd, "cylinder") ? SH_CYLINDER : SH_CONE;
       sh.c = V3(c[0], c[1] - 0.5 * h, c[2]);
       sh.axis = V3(c[0], c[1] + 0.5 * h, c[2]);
       sh.r = r;
-      sh.box.mn = V3(c[0] - r, c[1] - 0.5 * h, c[2] - r);
-      sh.box.mx = V3(c[0] + r, c[1] + 0.5 * h, c[2] + r);
+      cap_cubes_box(sh);
       if (!resolve(m, el)) return fail("material id");
       el->shapes.push_back(sh);
     } else if (!strcmp(cmd, "line")) {
@@ -533,11 +637,12 @@ static bool read_princeton(Scene &s, int root_node, const std::string &filename,
       if (fscanf(fp, "%d%lf%lf%lf%lf%lf%lf", &m, &v[0], &v[1], &v[2], &v[3], &v[4], &v[5]) != 7)
         return fail("line");
       Shape sh;
+      // R3Scene.cpp:1667-1687: a line is R3Cylinder(p1, p2, RN_BIG_EPSILON)
       sh.type = SH_CYLINDER;
       sh.c = V3(v[0], v[1], v[2]);
       sh.axis = V3(v[3], v[4], v[5]);
-      sh.r = 1e-3;  // RN_BIG_EPSILON
-      sh.box.add(sh.c); sh.box.add(sh.axis);
+      sh.r = 1e-3;  // RN_BIG_EPSILON (RNScalar.cpp:22)
+      cap_cubes_box(sh);
       if (!resolve(m, el)) return fail("material id");
       el->shapes.push_back(sh);
     } else if (!strcmp(cmd, "mesh")) {

@@ -40,7 +40,8 @@ def compare(a, b, exact_frac, le1_frac, mean_tol):
 
 @pytest.mark.parametrize("name,extra", [
     ("cornell.scn", []), ("jensen.scn", ["-lt", "8", "-ss", "8"]), ("stilllife.scn", []),
-    ("pointlight1.scn", []), ("spotlight1.scn", []), ("dirlight1.scn", [])])
+    ("pointlight1.scn", []), ("spotlight1.scn", []), ("dirlight1.scn", []),
+    ("cylinder.scn", []), ("lines.scn", [])])
 def test_direct_only_matches_oracle(renderer, name, extra):
     args = [scene(name), "/tmp/x.png", "-resolution", "48", "48", "-aa", "0", "-no_indirect",
             "-no_caustic", "-tt", "8", "-st", "8", "-seed", "3"] + extra
@@ -79,7 +80,8 @@ def test_photon_maps_match_oracle(renderer):
         assert (a["dir"] == b["dir"]).mean() > 0.999
 
 
-@pytest.mark.parametrize("name", ["cornell.scn", "stilllife.scn", "teapot.scn", "jensen.scn"])
+@pytest.mark.parametrize("name", ["cornell.scn", "stilllife.scn", "teapot.scn", "jensen.scn",
+                                  "cylinder.scn"])
 def test_intersections_match_oracle(renderer, name):
     rng = np.random.default_rng(0)
     info = renderer.ReadScene(scene(name))
@@ -134,3 +136,36 @@ def test_full_gi_configs_match_oracle(renderer, name, extra, exact):
         assert gp["caustic_stored"] == ost["caustic_stored"]
     assert gst["screen_rays"] == ost["screen_rays"]
     compare(g, o, exact, 0.99, 0.5)
+
+
+def test_cylinder_and_line_cases_match_oracle(renderer):
+    """R3Intersects(ray, R3Cylinder) (R3Isect.cpp:1025-1200) branch coverage: rays aimed at the
+    side and caps from outside, from inside the cylinder, from above/below the caps, parallel to
+    the axis (inside and outside), and rays aimed at the radius-1e-3 `line` cylinders."""
+    rng = np.random.default_rng(5)
+    renderer.ReadScene(scene("cylinder.scn"))
+    n = 3000
+    # targets on the unit cylinder (axis y, y in [-0.5, 0.5]) and on the cube-edge lines
+    phi = rng.random(n) * 2 * np.pi
+    side = np.stack([np.cos(phi), rng.random(n) - 0.5, np.sin(phi)], 1)
+    cap = np.stack([np.sqrt(rng.random(n)) * np.cos(phi), np.sign(rng.random(n) - 0.5) * 0.5,
+                    np.sqrt(rng.random(n)) * np.sin(phi)], 1)
+    a, b = np.array([-1.0, -1.0, -1.0]), np.array([1.0, -1.0, -1.0])
+    on_line = a + rng.random((n, 1)) * (b - a)
+    targets = np.concatenate([side, cap, on_line])
+    org = targets + rng.normal(size=targets.shape) * 3.0
+    d = targets - org
+    inside = np.stack([rng.random(n) * 0.5 - 0.25, rng.random(n) - 0.5, rng.random(n) * 0.5 - 0.25], 1)
+    d_in = rng.normal(size=(n, 3))
+    par_o = np.stack([rng.random(n) * 3 - 1.5, np.full(n, 2.0), rng.random(n) * 3 - 1.5], 1)
+    par_d = np.tile([0.0, -1.0, 0.0], (n, 1))
+    org = np.concatenate([org, inside, par_o])
+    d = np.concatenate([d, d_in, par_d])
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    gh, gt, gp, gn, gm = renderer.Intersects(org, d)
+    oh, ot, op, on, om = oracle_lib.intersect(scene("cylinder.scn"), org, d)
+    assert gh.sum() > 0.3 * len(gh)
+    assert (gh == oh).mean() > 0.9995
+    both = (gh == 1) & (oh == 1)
+    np.testing.assert_allclose(gt[both], ot[both], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(gn[both], on[both], atol=1e-9)

@@ -1,8 +1,10 @@
 """Device render / photon tracing / ray casting vs the oracle restatement on the same inputs
 and RNG streams. Images are compared on the 8-bit output (R2Image::SetPixelRGB truncation):
-direct-only renders must match exactly except for rare 1-LSB truncation flips (fp64
-reassociation), full-GI renders must agree per pixel within 1 LSB on >= 99% of pixels and in
-mean within 0.5 LSB (path divergence from last-ulp transcendental differences is allowed)."""
+the device code is compiled without FP contraction (like the reference's x86 build) and is
+bit-exact with the oracle in practice (tools/exactness.py: 100% on cornell/jensen direct and
+cornell/teapot full GI). The thresholds leave room only for rare last-ulp differences between
+device and host transcendentals (pow/acos/sin/cos), which can fork a Monte Carlo path:
+direct-only >= 99.9% exact, full GI >= 99% exact and >= 99.5% within 1 LSB."""
 import os
 
 import numpy as np
@@ -47,7 +49,7 @@ def test_direct_only_matches_oracle(renderer, name, extra):
             "-no_caustic", "-tt", "8", "-st", "8", "-seed", "3"] + extra
     g, gst, _ = run_gpu(renderer, args)
     o, ost = oracle_lib.render(args, 48, 48)
-    compare(g, o, 0.995, 0.999, 0.05)
+    compare(g, o, 0.999, 0.999, 0.05)
     assert gst["screen_rays"] == ost["screen_rays"]
 
 
@@ -59,7 +61,7 @@ def test_full_gi_cornell_matches_oracle(renderer):
     o, ost = oracle_lib.render(args, 24, 24)
     assert gp["global_stored"] == ost["global_stored"]
     assert gp["caustic_stored"] == ost["caustic_stored"]
-    compare(g, o, 0.97, 0.99, 0.5)
+    compare(g, o, 0.99, 0.995, 0.5)
     assert abs(gst["knn_queries"] - ost["knn_queries"]) <= 0.01 * ost["knn_queries"]
 
 
@@ -121,10 +123,10 @@ def test_tiles_compose_full_image(renderer):
 # translate nodes, 4 point lights), C5 teapot (1,452-triangle mesh, depth of field).
 @pytest.mark.parametrize("name,extra,exact", [
     ("jensen.scn", ["-global", "4000", "-caustic", "20000", "-lt", "4", "-ss", "4", "-it", "16"],
-     0.95),
-    ("stilllife.scn", ["-global", "20000", "-no_caustic", "-it", "16"], 0.95),
+     0.99),
+    ("stilllife.scn", ["-global", "20000", "-no_caustic", "-it", "16"], 0.99),
     ("teapot.scn", ["-global", "20000", "-no_caustic", "-it", "8", "-dof", "2", "8.0", "0.05"],
-     0.95),
+     0.99),
 ])
 def test_full_gi_configs_match_oracle(renderer, name, extra, exact):
     args = [scene(name), "/tmp/x.png", "-resolution", "20", "20", "-aa", "0", "-tt", "8",

@@ -217,7 +217,8 @@ struct gi_ctx {
   // render scratch
   DBuf spawn, npaths, path_off, nmc, mc_off, nind, ind_off, base, pixels, rgbf, rgb8, gheap_d2, gheap_idx, qcount, stats_bak;
   DBuf qpos[2], qshade[2], qkey[2], qout[2];
-  DBuf list_idx, list_d2, list_n;  // K-best lists of the query-per-wave k-NN path
+  DBuf list_idx, list_d2, list_n;
+  DBuf qseg[2];  // K-best lists of the query-per-wave k-NN path
   size_t qcap_hint[2] = {0, 0};
   KeySortScratch keysort[2];
   int knn_kernel_kind = -1;  // -1 auto, 0 per-lane heap, 1 query per wave, 2 packet
@@ -692,7 +693,12 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     // photon-map estimates, then a deterministic (key) order of each list for the reduction
     for (int l = 0; l < 2; l++) {
       a.nq[l] = nq[l];
-      if (!nq[l]) continue;
+      if (!nq[l]) {  // no queries: empty segments for every primary
+        HIPCHK(c, c->qseg[l].ensure((size_t)(nprim + 1) * 4));
+        HIPCHK(c, hipMemsetAsync(c->qseg[l].p, 0, (size_t)(nprim + 1) * 4, c->stream));
+        a.qseg[l] = c->qseg[l].as<uint32_t>();
+        continue;
+      }
       HIPCHK(c, c->qout[l].ensure((size_t)nq[l] * 24));
       if (!c->map_valid[l]) {
         HIPCHK(c, hipMemsetAsync(c->qout[l].p, 0, (size_t)nq[l] * 24, c->stream));
@@ -704,11 +710,17 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
       }
       uint64_t *sk = nullptr;
       uint32_t *ss = nullptr;
-      int bits = 20;
-      while (bits < 64 && ((uint64_t)total_paths >> (bits - 20)) != 0) bits++;
+      // keys: primary << 32 | slot in primary << 16 | query in path (empty slots: ~0)
+      int bits = 32;
+      while (bits < 64 && ((uint64_t)nprim >> (bits - 32)) != 0) bits++;
+      if (bits < 64) bits++;  // room for the empty-slot key's top bits
       HIPCHK(c, key_order(a.qkey[l], nq[l], bits, c->keysort[l], &sk, &ss, c->stream));
       a.skey[l] = sk;
       a.sslot[l] = ss;
+      HIPCHK(c, c->qseg[l].ensure((size_t)(nprim + 1) * 4));
+      a.qseg[l] = c->qseg[l].as<uint32_t>();
+      launch_segments(sk, nq[l], (uint32_t)nprim, a.qseg[l], c->stream);
+      HIPCHK(c, hipGetLastError());
       a.qout[l] = c->qout[l].as<double>();
     }
     a.rgbf = c->rgbf.as<float>();

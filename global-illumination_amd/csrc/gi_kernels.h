@@ -77,6 +77,7 @@ struct RenderArgs {
   uint32_t qcap[2];
   const uint64_t *skey[2];    // sorted keys
   const uint32_t *sslot[2];   // slot of each sorted key
+  uint32_t *qseg[2];          // [nprim + 1]: sorted queries of primary b are [qseg[b], qseg[b+1])
   uint32_t nq[2];
   double *base;         // [total_paths * 3]
   const double *qout[2];       // k-NN contributions per slot
@@ -188,6 +189,8 @@ hipError_t launch_scan(const uint32_t *in, uint32_t *out, int64_t n, ScanTemp &t
 void launch_primary(const RenderArgs &a, hipStream_t st);
 void launch_path(const RenderArgs &a, hipStream_t st);  // slot0 + indirect + Monte Carlo
 void launch_reduce(const RenderArgs &a, hipStream_t st);
+void launch_segments(const uint64_t *skeys, uint32_t n, uint32_t nprim, uint32_t *seg,
+                     hipStream_t st);
 void launch_knn(const KnnArgs &a, bool lds_heap, hipStream_t st);
 bool launch_knn_wave(const KnnArgs &a, int cap_mul, hipStream_t st);
 bool launch_knn_packet(const KnnArgs &a, hipStream_t st);

@@ -62,9 +62,10 @@ __global__ void scan_add_kernel(uint32_t *out, const uint32_t *block_off, int64_
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ void decode_primary(const RenderArgs &a, int64_t b, int &pix, int &i,
                                                int &j, int &k, uint64_t &psample) {
-  int af2 = a.af * a.af;
-  k = (int)(b % a.dof_test);
-  int64_t r = b / a.dof_test;
+  // b < nprim <= 2^31 per batch: 32-bit division (64-bit integer division is a long routine)
+  uint32_t af2 = (uint32_t)(a.af * a.af), dof = (uint32_t)a.dof_test, ub = (uint32_t)b;
+  k = (int)(ub % dof);
+  uint32_t r = ub / dof;
   int sub = (int)(r % af2);
   pix = (int)(r / af2);
   int2 pc = a.pixels[pix];
@@ -163,6 +164,8 @@ struct PathCtx {
   const Flags *F;
   const RenderArgs *A;
   uint64_t g;       // path slot
+  uint32_t prim;    // primary sample of the path (within the batch)
+  uint32_t pslot;   // slot of the path within its primary sample (0 = the primary's own)
   uint32_t j;       // queries issued so far by this path
   C3 base;
   Counts cnt;
@@ -195,7 +198,10 @@ __device__ __forceinline__ void put_query(PathCtx &P, int list, V p, V n, V ex, 
     base = (uint32_t)__shfl((int)base, leader, 64);
     slot = base + rank;
   }
-  uint64_t key = (P.g << 20) | (uint64_t)(P.j++);
+  // order key: (primary, slot in primary, query in path) -- the per-pixel reduction sums each
+  // primary's queries in this order; segments per primary come from one boundary pass
+  uint64_t key = ((uint64_t)P.prim << 32) | ((uint64_t)(P.pslot & 0xffffu) << 16) |
+                 (uint64_t)(P.j++ & 0xffffu);
   if (slot >= a.qcap[list]) return;  // overflow: the host grows the lists and re-runs
   uint32_t sign = (ct > 0) ? 1u : ((ct < 0) ? 2u : 0u);
   uint32_t meta = sign | ((uint32_t)mat << 2);
@@ -348,11 +354,25 @@ __device__ __forceinline__ int64_t scan_owner(const uint32_t *off, int64_t n, in
   return lo;
 }
 
-__device__ __forceinline__ void path_init(PathCtx &P, const RenderArgs &a, int64_t g) {
+// scan_owner for a whole wave: one binary search for the wave's first path, then each lane
+// steps forward (a wave's 64 consecutive paths span only a few primary samples)
+__device__ __forceinline__ int64_t wave_owner(const uint32_t *off, int64_t n, int64_t t,
+                                              int64_t total) {
+  int64_t t0 = (int64_t)__builtin_amdgcn_readfirstlane((int)t);
+  if (t0 > t) t0 = t;
+  int64_t p = scan_owner(off, n, t0 < total ? t0 : total - 1);
+  while (p + 1 < n && (int64_t)off[p + 1] <= t) p++;
+  return p;
+}
+
+__device__ __forceinline__ void path_init(PathCtx &P, const RenderArgs &a, int64_t g, int64_t prim,
+                                          int pslot) {
   P.S = &a.S;
   P.F = &a.F;
   P.A = &a;
   P.g = (uint64_t)g;
+  P.prim = (uint32_t)prim;
+  P.pslot = (uint32_t)pslot;
   P.j = 0;
   P.base = rgb(0, 0, 0);
   Counts z = {0, 0, 0, 0, 0, 0};
@@ -382,7 +402,7 @@ __global__ __launch_bounds__(256) void slot0_kernel(RenderArgs a) {
     int64_t g = a.path_off[b];
     const Spawn &sp = a.spawn[b];
     PathCtx P;
-    path_init(P, a, g);
+    path_init(P, a, g, b, 0);
     P.fixed[0] = P.fixed[1] = b;
     P.base = ldc(sp.base);
     if (sp.hit) {
@@ -410,16 +430,17 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void i
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   Counts cnt = {0, 0, 0, 0, 0, 0};
   if (t < a.total_ind) {
-    int64_t pb = scan_owner(a.ind_off, a.nprim, t);
+    int64_t pb = wave_owner(a.ind_off, a.nprim, t, a.total_ind);
     int s = (int)(t - a.ind_off[pb]);
     const Spawn &sp = a.spawn[pb];
-    int64_t g = (int64_t)a.path_off[pb] + 1 + sp.n_t + sp.n_s + s;
+    int pslot = 1 + sp.n_t + sp.n_s + s;
+    int64_t g = (int64_t)a.path_off[pb] + pslot;
     int pix, i, j, k;
     uint64_t psample;
     decode_primary(a, pb, pix, i, j, k, psample);
     const DMaterial &m = a.S.mats[sp.mat];
     PathCtx P;
-    path_init(P, a, g);
+    path_init(P, a, g, pb, pslot);
     P.fixed[0] = a.qind_base + t;  // at most one (global) query per indirect path
     Rng rng;
     rng.init(a.F.seed, KIND_IND, psample, (uint64_t)s);
@@ -442,7 +463,7 @@ __global__ __launch_bounds__(128) void mc_kernel(RenderArgs a) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   Counts cnt = {0, 0, 0, 0, 0, 0};
   if (t < a.total_mc) {
-    int64_t pb = scan_owner(a.mc_off, a.nprim, t);
+    int64_t pb = wave_owner(a.mc_off, a.nprim, t, a.total_mc);
     int s = (int)(t - a.mc_off[pb]);
     const Spawn &sp = a.spawn[pb];
     int64_t g = (int64_t)a.path_off[pb] + 1 + s;
@@ -455,7 +476,7 @@ __global__ __launch_bounds__(128) void mc_kernel(RenderArgs a) {
     V p = ld3(sp.p), n = ld3(sp.n), view = ld3(sp.v);
     double ct = sp.ct, R = sp.R;
     PathCtx P;
-    path_init(P, a, g);
+    path_init(P, a, g, pb, 1 + s);
     Rng rng;
     if (s < sp.n_t) {
       rng.init(F.seed, KIND_TRANS, psample, (uint64_t)s);
@@ -842,6 +863,27 @@ __global__ __launch_bounds__(64) void cached_kernel(KnnArgs a) {
   if (a.stats) wave_add(&a.stats[ST_KNN + a.stat_off], nq_done);
 }
 
+// CSR offsets of the key-sorted query list by primary sample: thread i fills seg[b] = i for
+// every primary b in (b(i-1), b(i)]; empty slots (key ~0) and i = n close the array.
+__global__ void segments_kernel(const uint64_t *skeys, uint32_t n, uint32_t nprim, uint32_t *seg) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > (int64_t)n) return;
+  auto prim_of = [&](int64_t k) -> int64_t {
+    uint64_t key = skeys[k];
+    if (key == ~0ull) return nprim;
+    uint64_t b = key >> 32;
+    return b < nprim ? (int64_t)b : (int64_t)nprim;
+  };
+  int64_t bi = (i < (int64_t)n) ? prim_of(i) : (int64_t)nprim;
+  int64_t bp = (i == 0) ? -1 : prim_of(i - 1);
+  for (int64_t b = bp + 1; b <= bi; b++) seg[b] = (uint32_t)i;
+}
+
+void launch_segments(const uint64_t *skeys, uint32_t n, uint32_t nprim, uint32_t *seg,
+                     hipStream_t st) {
+  segments_kernel<<<(unsigned)(((int64_t)n + 1 + 255) / 256), 256, 0, st>>>(skeys, n, nprim, seg);
+}
+
 // ---------------------------------------------------------------------------------------
 // Per-pixel reduction: RenderImage's DOF average + ClampColor + box filter + SetPixelRGB
 // (render.cpp:130-135, 205-221; R2Image.cpp:205-208)
@@ -864,15 +906,8 @@ __global__ __launch_bounds__(64) void reduce_kernel(RenderArgs a) {
         c2 += a.base[3 * (int64_t)g + 2];
       }
       for (int l = 0; l < 2; l++) {
-        const uint64_t *K = a.skey[l];
-        uint32_t n = a.nq[l];
-        uint64_t k0 = (uint64_t)p0 << 20, k1 = (uint64_t)p1 << 20;
-        uint32_t lo = 0, hi = n;
-        while (lo < hi) {
-          uint32_t mid = (lo + hi) >> 1;
-          if (K[mid] < k0) lo = mid + 1; else hi = mid;
-        }
-        for (uint32_t q = lo; q < n && K[q] < k1; q++) {
+        uint32_t q0 = a.qseg[l][b], q1 = a.qseg[l][b + 1];
+        for (uint32_t q = q0; q < q1; q++) {
           uint32_t sl = a.sslot[l][q];
           c0 += a.qout[l][3 * (int64_t)sl];
           c1 += a.qout[l][3 * (int64_t)sl + 1];

@@ -131,7 +131,8 @@ def main():
         step()
     barrier()
     t0 = time.perf_counter()
-    keys = ("q0", "q1", "ph0", "ph1", "vis0", "vis1", "ms0", "ms1", "n0", "n1")
+    keys = ("q0", "q1", "ph0", "ph1", "vis0", "vis1", "ms0", "ms1", "n0", "n1", "fb0", "fb1",
+            "fbq0", "fbq1")
     agg = dict.fromkeys(keys, 0.0)
     for _ in range(a.steps):
         st = step()
@@ -141,6 +142,8 @@ def main():
             agg[f"vis{m}"] += st["knn_map_visited"][m]
             agg[f"ms{m}"] += st["knn_map_kernel_ms"][m]
             agg[f"n{m}"] += st["knn_map_launches"][m]
+            agg[f"fb{m}"] += st["knn_map_fallback_ms"][m]
+            agg[f"fbq{m}"] += st["knn_map_fallback_queries"][m]
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -158,7 +161,8 @@ def main():
 
     if rank == 0:
         # roofline of the dominant kernel: the global-map k-NN radiance estimate
-        # (knn_lane_kernel, K=50), HIP-event timed in-library on the render stream
+        # (knn_chunk_kernel + per-lane fallback, K=50), HIP-event timed in-library on the
+        # render stream
         def kstats(m):
             ms = agg[f"ms{m}"]
             launches = max(1.0, agg[f"n{m}"])
@@ -171,13 +175,16 @@ def main():
                     "queries_per_launch": agg[f"q{m}"] / launches,
                     "photons_per_query": photons / max(1.0, agg[f"q{m}"]),
                     "visited_per_query": agg[f"vis{m}"] / max(1.0, agg[f"q{m}"]),
+                    "fallback_avg_ms": round(agg[f"fb{m}"] / launches, 3),
+                    "fallback_query_frac": round(agg[f"fbq{m}"] / max(1.0, agg[f"q{m}"]), 4),
                     "ms_per_frame": ms / a.steps / max(1, world)}
         g, c = kstats(0), kstats(1)
         traffic = load_traffic(a)
         roofline = {"bound": "hbm", "achieved": g["achieved_GBps"], "peak": HBM_PEAK_GBPS,
                     "unit": "GB/s", "frac": round(g["achieved_GBps"] / HBM_PEAK_GBPS, 5),
                     "traffic": traffic,
-                    "kernel": "gi::knn_lane_kernel<8,4> (global map k-NN + EstimateRadiance)",
+                    "kernel": "gi::knn_chunk_kernel<256> + gi::knn_lane_kernel<8,4> fallback "
+                              "(global map k-NN + EstimateRadiance; avg_launch_ms = their sum)",
                     "bytes_per_unit": "16 B per photon returned (SURVEY.md 8(d))",
                     "global": g, "caustic_kernel": dict(c, kernel="gi::knn_wave_kernel<512> + knn_list_estimate_kernel")}
         cpu = None

@@ -207,6 +207,10 @@ struct gi_ctx {
   bool map_valid[2] = {false, false};
   int leaf_size[2] = {64, 512};  // photons per kd leaf, per map (global, caustic)
   int wave_cap_mul = 1;
+  int chunk_cap = 256;            // chunk kernel: LDS candidate capacity per 64-query chunk
+  hipEvent_t ev2 = nullptr;       // chunk kernel / fallback split
+  double fb_ms[2] = {0, 0};       // fallback time and queries per map (since the last reset)
+  uint64_t fb_q[2] = {0, 0};
   int sel_slack = 64;
   bool force_gheap = false;
   int knn_qpl = 1;
@@ -218,6 +222,8 @@ struct gi_ctx {
   DBuf spawn, npaths, path_off, nmc, mc_off, nind, ind_off, base, pixels, rgbf, rgb8, gheap_d2, gheap_idx, qcount, stats_bak;
   DBuf qpos[2], qshade[2], qkey[2], qout[2];
   DBuf list_idx, list_d2, list_n;
+  DBuf fb_list, fb_count;          // chunk k-NN fallback queries
+  uint64_t fb_total = 0;
   DBuf qseg[2];  // K-best lists of the query-per-wave k-NN path
   size_t qcap_hint[2] = {0, 0};
   KeySortScratch keysort[2];
@@ -481,6 +487,7 @@ KnnArgs knn_args(gi_ctx *c, int mi) {
   k.stat_off = mi == GI_MAP_GLOBAL ? 0 : ST_KNN_MAP;
   k.sel_slack = c->sel_slack;
   k.qpl = c->knn_qpl;
+  if (const char *s = getenv("GI_KNN_DBG")) k.dbg = atoi(s);
   return k;
 }
 
@@ -489,8 +496,53 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
   // auto (-1): per-lane 4-ary LDS heaps while they fit (K <= 64), else one query per wave
   // (measured with tools/knn_micro.py on cornell 1M+1M maps)
   int kind = c->knn_kernel_kind;
-  if (kind < 0) kind = (k.K <= 64) ? 3 : 1;
+  // auto: chunk kernel (+ per-lane fallback) for K <= 64, per-lane kernel for list mode,
+  // query-per-wave beyond (measured)
+  int auto_kind = (k.K <= 64) ? (k.mode == KNN_MODE_LIST ? 3 : 5) : 1;
+  if (kind < 0) kind = auto_kind;
+  // an override that cannot serve this map's K (or list mode) falls back to the automatic one
+  if (((kind == 5 || kind == 6) && (k.K > 64 || k.mode == KNN_MODE_LIST)) || (kind == 3 && k.K > 128) ||
+      (kind == 0 && k.K > 64))
+    kind = auto_kind;
   if (kind == 2 && (int64_t)k.K * 64 * 8 > 80 * 1024) kind = 1;
+  if ((kind == 5 || kind == 6) && k.K <= 64 && k.mode != KNN_MODE_LIST) {
+    // chunk kernel, then the per-lane kernel on the chunks that overflowed its LDS gather
+    HIPCHK(c, c->fb_list.ensure((size_t)nq * 4));
+    HIPCHK(c, c->fb_count.ensure(4));
+    HIPCHK(c, hipMemsetAsync(c->fb_count.p, 0, 4, c->stream));
+    k.nq = nq;
+    k.q0 = 0;
+    k.fb_list = c->fb_list.as<uint32_t>();
+    k.fb_count = c->fb_count.as<uint32_t>();
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    launch_knn_chunk(k, c->chunk_cap, kind == 6, c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->ev2, c->stream));
+    uint32_t nfb = 0;
+    HIPCHK(c, hipMemcpyAsync(&nfb, c->fb_count.p, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->fb_total += nfb;
+    if (nfb) {
+      KnnArgs f = k;
+      f.perm = c->fb_list.as<uint32_t>();
+      f.nq = nfb;
+      f.q0 = 0;
+      launch_knn_lane(f, c->lane_chunk, c->heap_arity, c->stream);
+      HIPCHK(c, hipGetLastError());
+    }
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    if (ms) {
+      HIPCHK(c, hipEventSynchronize(c->ev1));
+      float t = 0, tf = 0;
+      HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+      HIPCHK(c, hipEventElapsedTime(&tf, c->ev2, c->ev1));
+      *ms += t;
+      int mi = k.stat_off ? 1 : 0;
+      c->fb_ms[mi] += tf;
+      c->fb_q[mi] += nfb;
+    }
+    return GI_OK;
+  }
   if (kind == 3 && (size_t)k.K * 512 <= 64 * 1024) {
     k.nq = nq;
     k.q0 = 0;
@@ -766,6 +818,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return GI_ERR_HIP; }
   hipEventCreate(&c->ev0);
   hipEventCreate(&c->ev1);
+  hipEventCreate(&c->ev2);
   std::vector<double> lut;
   build_lut(lut);
   if (upload(c->d_lut, lut.data(), lut.size() * 8, c->stream) != hipSuccess ||
@@ -780,6 +833,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_LEAF_SIZE_C")) c->leaf_size[1] = std::max(1, atoi(s));
   if (const char *s = getenv("GI_WAVE_CAP_MUL")) c->wave_cap_mul = std::max(1, atoi(s));
   if (const char *s = getenv("GI_SEL_SLACK")) c->sel_slack = std::max(1, atoi(s));
+  if (const char *s = getenv("GI_CHUNK_CAP")) c->chunk_cap = std::max(64, atoi(s));
   if (const char *s = getenv("GI_KNN_GHEAP")) c->force_gheap = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_QPL")) c->knn_qpl = std::max(1, atoi(s));
   if (const char *s = getenv("GI_LANE_CHUNK")) c->lane_chunk = std::max(1, atoi(s));
@@ -813,6 +867,7 @@ void gi_destroy(gi_ctx *c) {
   sort_scratch_release(c->sorter);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
+  if (c->ev2) hipEventDestroy(c->ev2);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -998,6 +1053,8 @@ static int render_common(gi_ctx *c, int aa, int w, int h, const std::vector<int3
   }
   HIPCHK(c, hipMemsetAsync(c->rgb8.p, 0, npx, c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_stats.p, 0, ST_COUNT * 8, c->stream));
+  c->fb_ms[0] = c->fb_ms[1] = 0;
+  c->fb_q[0] = c->fb_q[1] = 0;
   gi_render_stats local;
   memset(&local, 0, sizeof local);
   rc = render_pixels(c, aa, w, h, pix, &local);
@@ -1021,6 +1078,8 @@ static int render_common(gi_ctx *c, int aa, int w, int h, const std::vector<int3
       st->knn_map_visited[m] = s[ST_KNN_VISITED + m * ST_KNN_MAP];
       st->knn_map_kernel_ms[m] = local.knn_map_kernel_ms[m];
       st->knn_map_launches[m] = local.knn_map_launches[m];
+      st->knn_map_fallback_ms[m] = c->fb_ms[m];
+      st->knn_map_fallback_queries[m] = c->fb_q[m];
     }
     st->knn_queries = st->knn_map_queries[0] + st->knn_map_queries[1];
     st->knn_photons = st->knn_map_photons[0] + st->knn_map_photons[1];

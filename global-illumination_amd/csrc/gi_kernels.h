@@ -123,6 +123,50 @@ __device__ __forceinline__ bool kd_next(const KdNode *nodes, int &node, float qx
   return true;
 }
 
+// d-ary max-heap of u64 keys in LDS laid out [slot][lane] (stride 64): sift-down, Floyd build,
+// and accept (append unordered until K, heapify once, then replace the root)
+template <int ARY>
+__device__ __forceinline__ void heapn_sift(uint64_t *h, int n, int c, uint64_t key) {
+  while (true) {
+    int f = ARY * c + 1;
+    if (f >= n) break;
+    uint64_t kk[ARY];
+#pragma unroll
+    for (int j = 0; j < ARY; j++) kk[j] = (f + j < n) ? h[(f + j) * 64] : 0ull;
+    int m = f;
+    uint64_t mk = kk[0];
+#pragma unroll
+    for (int j = 1; j < ARY; j++)
+      if (kk[j] > mk) { mk = kk[j]; m = f + j; }
+    if (key >= mk) break;
+    h[c * 64] = mk;
+    c = m;
+  }
+  h[c * 64] = key;
+}
+
+template <int ARY>
+__device__ __forceinline__ void heapn_build(uint64_t *h, int n) {
+  for (int i = (n - 2) / ARY; i >= 0; i--) heapn_sift<ARY>(h, n, i, h[i * 64]);
+}
+
+// accept one candidate (key < lim already checked)
+template <int ARY>
+__device__ __forceinline__ void heapn_accept(uint64_t *h, int &size, int K, uint64_t key,
+                                             uint64_t &lim) {
+  if (size < K) {
+    h[size * 64] = key;
+    size++;
+    if (size == K) {
+      heapn_build<ARY>(h, K);
+      lim = h[0];
+    }
+  } else {
+    heapn_sift<ARY>(h, K, 0, key);
+    lim = h[0];
+  }
+}
+
 // wave-level counter reduction (one atomic per wave)
 __device__ __forceinline__ void wave_add(unsigned long long *dst, uint64_t v) {
 #pragma unroll
@@ -150,6 +194,8 @@ struct KnnArgs {
   int32_t stat_off;        // 0 (global map) or ST_KNN_MAP (caustic map)
   int32_t sel_slack;       // query-per-wave kernel: re-select once K + slack candidates held
   int32_t qpl;             // per-lane kernel: consecutive (sorted) queries per lane
+  int32_t dbg;             // diagnostics: chunk kernel phase skips (timing only)
+  int32_t pad4;
   float r2f;               // (float)(r*r) accept radius
   double rmax;
   double fa, fb, fk;       // FILTER_CONST_A/B/K
@@ -161,6 +207,8 @@ struct KnnArgs {
   int32_t *list_idx;       // query-per-wave kernel: K-best lists [nq][K] (kd-order index)
   float *list_d2;          //   and their d2; -1 past list_n[q]
   int32_t *list_n;
+  uint32_t *fb_list;       // chunk kernel: queries (original slots) handed to the fallback
+  uint32_t *fb_count;
   float *gheap_d2;         // global heap scratch (K > 64)
   int32_t *gheap_idx;
   unsigned long long *stats;
@@ -196,6 +244,7 @@ bool launch_knn_wave(const KnnArgs &a, int cap_mul, hipStream_t st);
 bool launch_knn_packet(const KnnArgs &a, hipStream_t st);
 bool launch_knn_lane(const KnnArgs &a, int chunk, int arity, hipStream_t st);
 bool launch_knn_group(const KnnArgs &a, int lanes, hipStream_t st);
+bool launch_knn_chunk(const KnnArgs &a, int cap, bool lane_heaps, hipStream_t st);
 void launch_list_estimate(const KnnArgs &a, hipStream_t st);
 void launch_cached(const KnnArgs &a, hipStream_t st);
 void launch_photons(const PhotonArgs &a, bool emit, hipStream_t st);

@@ -388,48 +388,6 @@ __device__ __forceinline__ void kheap_replace_top(uint64_t *h, int size, uint64_
 //     then the wave runs the leaf loop together, CH photon loads in flight per lane.
 // Result set: the K smallest (d2, index) keys with d2 <= r2 (R3Kdtree.cpp:688-784 semantics).
 // ---------------------------------------------------------------------------------------
-template <int ARY>
-__device__ __forceinline__ void heapn_sift(uint64_t *h, int n, int c, uint64_t key) {
-  while (true) {
-    int f = ARY * c + 1;
-    if (f >= n) break;
-    uint64_t kk[ARY];
-#pragma unroll
-    for (int j = 0; j < ARY; j++) kk[j] = (f + j < n) ? h[(f + j) * 64] : 0ull;
-    int m = f;
-    uint64_t mk = kk[0];
-#pragma unroll
-    for (int j = 1; j < ARY; j++)
-      if (kk[j] > mk) { mk = kk[j]; m = f + j; }
-    if (key >= mk) break;
-    h[c * 64] = mk;
-    c = m;
-  }
-  h[c * 64] = key;
-}
-
-template <int ARY>
-__device__ __forceinline__ void heapn_build(uint64_t *h, int n) {
-  for (int i = (n - 2) / ARY; i >= 0; i--) heapn_sift<ARY>(h, n, i, h[i * 64]);
-}
-
-// accept one candidate (key < lim already checked)
-template <int ARY>
-__device__ __forceinline__ void heapn_accept(uint64_t *h, int &size, int K, uint64_t key,
-                                             uint64_t &lim) {
-  if (size < K) {
-    h[size * 64] = key;
-    size++;
-    if (size == K) {
-      heapn_build<ARY>(h, K);
-      lim = h[0];
-    }
-  } else {
-    heapn_sift<ARY>(h, K, 0, key);
-    lim = h[0];
-  }
-}
-
 template <int CH, int ARY>
 __global__ __launch_bounds__(64) void knn_lane_kernel(KnnArgs a) {
   extern __shared__ uint64_t lsm[];

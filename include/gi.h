@@ -139,6 +139,9 @@ typedef struct gi_render_stats {
   /* the same split per photon map (0 = global, 1 = caustic) */
   uint64_t knn_map_queries[2], knn_map_photons[2], knn_map_visited[2];
   double knn_map_kernel_ms[2], knn_map_launches[2];
+  /* chunk k-NN path: time and queries of the per-lane fallback within knn_map_kernel_ms */
+  double knn_map_fallback_ms[2];
+  uint64_t knn_map_fallback_queries[2];
 } gi_render_stats;
 
 typedef struct gi_ctx gi_ctx;

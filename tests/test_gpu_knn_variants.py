@@ -28,6 +28,10 @@ VARIANTS = [
     {"GI_KNN_KERNEL": "4", "GI_GROUP_LANES": "8"},
     {"GI_KNN_KERNEL": "4", "GI_GROUP_LANES": "16", "GI_SEL_SLACK": "1"},
     {"GI_KNN_KERNEL": "4", "GI_GROUP_LANES": "32", "GI_LEAF_SIZE": "128"},
+    {"GI_KNN_KERNEL": "5"},
+    {"GI_KNN_KERNEL": "5", "GI_CHUNK_CAP": "256", "GI_LEAF_SIZE": "50"},
+    {"GI_KNN_KERNEL": "6"},
+    {"GI_KNN_KERNEL": "6", "GI_CHUNK_CAP": "256"},
 ]
 
 
@@ -74,6 +78,41 @@ def test_variant_estimate(env, filt, k, r):
     try:
         ph = synth.photon_map(30000, seed=11)
         q = synth.queries(900, seed=5, k=k, r=r, filt=filt, spec=True)
+        fk = 1.25 if filt == CONE else 1.0
+        p = gi_amd.default_params()
+        p.filter_const_k = fk
+        r_.set_params(p)
+        r_.set_photon_map(GLOBAL, ph)
+        g, gn, gm = r_.EstimateRadiance(GLOBAL, q)
+    finally:
+        r_.close()
+    o, on, om = oracle_lib.estimate_radiance(ph, q, filter_k=fk)
+    np.testing.assert_array_equal(gn, on)
+    np.testing.assert_array_equal(gm, om)
+    np.testing.assert_allclose(g, o, rtol=1e-10, atol=1e-300)
+
+
+def clustered_queries(n, seed, k, r, filt):
+    """Dense queries on one face (the regime the chunk kernel is built for): 64 consecutive
+    Morton-sorted queries span much less than a K-neighbourhood."""
+    q = synth.queries(n, seed=seed, k=k, r=r, filt=filt, spec=True)
+    rng = np.random.default_rng(seed)
+    pts = np.zeros((n, 3))
+    pts[:, 0] = 0.4 + rng.random(n) * 0.2
+    pts[:, 1] = 0.0
+    pts[:, 2] = 0.5 + rng.random(n) * 0.2
+    q["point"] = pts
+    q["normal"] = np.tile([0.0, 1.0, 0.0], (n, 1))
+    return q
+
+
+@pytest.mark.parametrize("env", VARIANTS, ids=lambda e: "-".join(f"{k[3:]}{v}" for k, v in e.items()))
+@pytest.mark.parametrize("filt,k,r", [(DISK, 50, 2.5), (CONE, 32, 0.05)])
+def test_variant_dense_queries(env, filt, k, r):
+    r_ = make_renderer(env)
+    try:
+        ph = synth.photon_map(200000, seed=13)
+        q = clustered_queries(8192, 17, k, r, filt)
         fk = 1.25 if filt == CONE else 1.0
         p = gi_amd.default_params()
         p.filter_const_k = fk

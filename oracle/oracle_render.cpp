@@ -1653,7 +1653,20 @@ void oracle_direction_lut(double *out) {
   memcpy(out, l.data(), l.size() * sizeof(double));
 }
 
-int oracle_main(int argc, char **argv) { return oracle_run(argc, argv, nullptr, 0, nullptr, 1); }
+// CLI exit behaviour of photonmap main: a bad flag prints "Invalid program argument: %s"
+// (no newline) and exit(1) (io_utils.cpp:192-199); missing names print the usage line and
+// ParseArgs returns 0, so main exit(-1) (io_utils.cpp:206, photonmap.cpp:446); scene or
+// image failures exit(-1) (photonmap.cpp:450,491).
+int oracle_main(int argc, char **argv) {
+  gi_params P;
+  params_default(P);
+  std::string scene, out, err;
+  int w, h, aa, real;
+  int rc = parse_args(argc, argv, P, scene, out, w, h, aa, real, err);
+  if (rc == 1) { fprintf(stderr, "%s", err.c_str()); return 1; }
+  if (rc == 2) { fprintf(stderr, "%s\n", err.c_str()); return -1; }
+  return oracle_run(argc, argv, nullptr, 0, nullptr, 1) ? -1 : 0;
+}
 
 // ParseArgs restatement (returns 0 ok, 1 bad flag, 2 usage) for flag-parity tests
 int oracle_parse_args(int argc, char **argv, gi_params *P, int *w, int *h, int *aa, int *real) {

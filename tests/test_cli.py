@@ -1,0 +1,105 @@
+"""The drop-in CLI `photonmap src.scn out.png [-FLAGS]` (photonmap.cpp:442-499) against the
+oracle's CLI restatement (oracle/oracle_main.cpp).
+
+Argument errors never reach the device, so they run on CPU:
+- A bad flag or an extra positional prints "Invalid program argument: %s" with no newline
+  and exits 1 (io_utils.cpp:192-199).
+- Missing file names print the usage line; ParseArgs returns 0 and main then exits -1
+  (io_utils.cpp:204-207, photonmap.cpp:445-446).
+
+The GPU test runs the whole CLI on a small cornell render and checks two things:
+- The written PNG matches the oracle CLI's PNG.
+- The `-v` report's counters match the oracle's (render.cpp:224-255,
+  photonmap.cpp:416-435).
+"""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_lib
+import pngio
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "global-illumination_amd", "photonmap")
+ORACLE_CLI = os.path.join(ROOT, "oracle", "oracle_photonmap")
+SCENES = os.path.join(ROOT, "tests", "scenes")
+
+USAGE = "Usage: photonmap inputscenefile outputimagefile [-FLAGS]\n"
+
+
+def run(binary, args, timeout=120):
+    if not os.path.exists(binary):
+        pytest.skip(f"{binary} not built (run __graft_entry__.build())")
+    return subprocess.run([binary] + args, capture_output=True, text=True, timeout=timeout)
+
+
+ARG_CASES = [
+    ([], 255, USAGE),
+    (["only_scene.scn"], 255, USAGE),
+    (["a.scn", "b.png", "-bogus"], 1, "Invalid program argument: -bogus"),
+    (["a.scn", "b.png", "extra"], 1, "Invalid program argument: extra"),
+    (["a.scn", "-v", "b.png", "-no_shadow", "-nonsense", "3"], 1,
+     "Invalid program argument: -nonsense"),
+]
+
+
+@pytest.mark.parametrize("args,rc,stderr", ARG_CASES)
+@pytest.mark.parametrize("binary", [CLI, ORACLE_CLI], ids=["device_cli", "oracle_cli"])
+def test_argument_errors(binary, args, rc, stderr):
+    r = run(binary, args)
+    assert r.returncode == rc, (r.returncode, r.stderr)
+    assert r.stderr == stderr
+    assert r.stdout == ""
+
+
+def test_missing_scene_fails_like_reference(tmp_path):
+    # ReadScene failure -> exit(-1) (photonmap.cpp:450); the oracle prints the loader message
+    r = run(ORACLE_CLI, [str(tmp_path / "missing.scn"), str(tmp_path / "o.png")])
+    assert r.returncode == 255
+    assert "Unable to open file" in r.stderr
+    assert not (tmp_path / "o.png").exists()
+
+
+def _verbose_counts(text):
+    out = {}
+    for key, val in re.findall(r"^\s*(# [A-Za-z ]+|Total Rays:|Total Photons Stored:)\s*=?\s*(\d+)\s*$",
+                               text, flags=re.M):
+        out[key.strip(" :")] = int(val)
+    return out
+
+
+@pytest.mark.gpu
+def test_cli_render_matches_oracle_cli(tmp_path):
+    flags = ["-resolution", "32", "24", "-aa", "1", "-global", "20000", "-caustic", "20000",
+             "-it", "8", "-tt", "8", "-st", "8"]
+    scn = os.path.join(SCENES, "cornell.scn")
+    dev_png, ora_png = str(tmp_path / "dev.png"), str(tmp_path / "ora.png")
+    r = run(CLI, [scn, dev_png] + flags + ["-v"], timeout=300)
+    assert r.returncode == 0, r.stderr
+    o = run(ORACLE_CLI, [scn, ora_png] + flags, timeout=300)
+    assert o.returncode == 0, o.stderr
+
+    a, b = pngio.read_png(dev_png), pngio.read_png(ora_png)
+    assert a.shape == b.shape == (24, 32, 3)
+    d = np.abs(a.astype(int) - b.astype(int)).max(-1)
+    assert (d == 0).mean() >= 0.99 and (d <= 1).mean() >= 0.995
+
+    # -v report: section headers in reference order and counters equal to the oracle's
+    for head in ("Read scene from", "Built photon map", "Rendering image", "Rendered image",
+                 "Wrote image to"):
+        assert head in r.stdout, r.stdout
+    assert r.stdout.index("Built photon map") < r.stdout.index("Rendered image") \
+        < r.stdout.index("Wrote image to")
+    got = _verbose_counts(r.stdout)
+    _rgb, st = oracle_lib.render([scn, ora_png] + flags, 32, 24)
+    assert got["# Global Photons Stored"] == st["global_stored"]
+    assert got["# Caustic Photons Stored"] == st["caustic_stored"]
+    assert got["Total Photons Stored"] == st["global_stored"] + st["caustic_stored"]
+    assert got["# Screen Rays"] == st["screen_rays"]
+    assert got["# Shadow Rays"] == st["shadow_rays"]
+    assert got["# Indirect Samples"] == st["indirect_samples"]
+    assert got["# Caustic Samples"] == st["caustic_samples"]
+    assert "Width = 32" in r.stdout and "Height = 24" in r.stdout

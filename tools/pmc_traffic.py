@@ -6,7 +6,10 @@ section): on gfx950 FETCH_SIZE reports 1/2 of the bytes actually read -> bytes =
 Writes profiles/knn_traffic.json, read by bench.py for roofline.traffic when the workload
 matches.
 
-usage: pmc_traffic.py <counter_collection.csv> <kernel-substring> <res> <aa> <global> <caustic>
+usage: pmc_traffic.py <counter_collection.csv> <kernel-substring[,substring...]> <res> <aa>
+                     <global> <caustic>
+Several substrings: the roofline "launch" is that sequence of kernels (e.g. the chunk kernel and
+its per-lane fallback); their per-dispatch averages are summed.
 """
 import csv
 import json
@@ -15,17 +18,21 @@ import sys
 
 
 def main():
-    path, kname = sys.argv[1], sys.argv[2]
+    path, knames = sys.argv[1], sys.argv[2].split(",")
     res, aa, glob, caus = (int(x) for x in sys.argv[3:7])
-    per = {}
-    for r in csv.DictReader(open(path)):
-        if kname not in r["Kernel_Name"] or r["Counter_Name"] != "FETCH_SIZE":
-            continue
-        per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
-    if not per:
-        sys.exit(f"no FETCH_SIZE rows for {kname!r} in {path}")
-    kib = sum(per.values()) / len(per)
-    out = {"kernel": kname, "dispatches": len(per), "fetch_size_kib_per_launch": kib,
+    rows = list(csv.DictReader(open(path)))
+    kib, ndisp = 0.0, {}
+    for kname in knames:
+        per = {}
+        for r in rows:
+            if kname not in r["Kernel_Name"] or r["Counter_Name"] != "FETCH_SIZE":
+                continue
+            per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+        if not per:
+            sys.exit(f"no FETCH_SIZE rows for {kname!r} in {path}")
+        kib += sum(per.values()) / len(per)
+        ndisp[kname] = len(per)
+    out = {"kernel": " + ".join(knames), "dispatches": ndisp, "fetch_size_kib_per_launch": kib,
            "correction": "x2 (gfx950 FETCH_SIZE = 1/2 of bytes read, MI355X_MICROARCH.md) x1024",
            "bytes_per_launch": kib * 1024 * 2,
            "workload": {"res": res, "aa": aa, "global": glob, "caustic": caus},

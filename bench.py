@@ -48,6 +48,10 @@ def parse():
     return ap.parse_args()
 
 
+# the roofline "launch": the chunk k-NN kernel and its per-lane fallback on the global map
+ROOFLINE_KERNELS = ["knn_chunk_lane_kernel", "knn_lane_kernel"]
+
+
 def load_traffic(a):
     """HBM bytes per launch of the roofline kernel from a committed PMC pass
     (tools/pmc_traffic.py -> profiles/knn_traffic.json), if it was taken on this workload."""
@@ -61,6 +65,8 @@ def load_traffic(a):
     if (wl.get("res"), wl.get("aa"), wl.get("global"), wl.get("caustic")) != (
             a.res, a.aa, a.global_photons, a.caustic_photons):
         return None
+    if t.get("kernel") != " + ".join(ROOFLINE_KERNELS):
+        return None  # measured on an earlier kernel
     return t.get("bytes_per_launch")
 
 
@@ -183,7 +189,7 @@ def main():
         roofline = {"bound": "hbm", "achieved": g["achieved_GBps"], "peak": HBM_PEAK_GBPS,
                     "unit": "GB/s", "frac": round(g["achieved_GBps"] / HBM_PEAK_GBPS, 5),
                     "traffic": traffic,
-                    "kernel": "gi::knn_chunk_kernel<256> + gi::knn_lane_kernel<8,4> fallback "
+                    "kernel": "gi::knn_chunk_lane_kernel<3> + gi::knn_lane_kernel<8,4> fallback "
                               "(global map k-NN + EstimateRadiance; avg_launch_ms = their sum)",
                     "bytes_per_unit": "16 B per photon returned (SURVEY.md 8(d))",
                     "global": g, "caustic_kernel": dict(c, kernel="gi::knn_wave_kernel<512> + knn_list_estimate_kernel")}

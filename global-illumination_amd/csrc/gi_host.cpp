@@ -493,19 +493,17 @@ KnnArgs knn_args(gi_ctx *c, int mi) {
 
 // run a k-NN launch over nq queries (chunked when the heap lives in global scratch)
 int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
-  // auto (-1): per-lane 4-ary LDS heaps while they fit (K <= 64), else one query per wave
-  // (measured with tools/knn_micro.py on cornell 1M+1M maps)
+  // auto (-1): chunk kernel with lane select (+ per-lane fallback) for K <= 64, the per-lane
+  // kernel for list mode, one query per wave beyond (measured)
   int kind = c->knn_kernel_kind;
-  // auto: chunk kernel (+ per-lane fallback) for K <= 64, per-lane kernel for list mode,
-  // query-per-wave beyond (measured)
-  int auto_kind = (k.K <= 64) ? (k.mode == KNN_MODE_LIST ? 3 : 5) : 1;
+  int auto_kind = (k.K <= 64) ? (k.mode == KNN_MODE_LIST ? 3 : 7) : 1;
   if (kind < 0) kind = auto_kind;
   // an override that cannot serve this map's K (or list mode) falls back to the automatic one
-  if (((kind == 5 || kind == 6) && (k.K > 64 || k.mode == KNN_MODE_LIST)) || (kind == 3 && k.K > 128) ||
+  if (((kind >= 5 && kind <= 7) && (k.K > 64 || k.mode == KNN_MODE_LIST)) || (kind == 3 && k.K > 128) ||
       (kind == 0 && k.K > 64))
     kind = auto_kind;
   if (kind == 2 && (int64_t)k.K * 64 * 8 > 80 * 1024) kind = 1;
-  if ((kind == 5 || kind == 6) && k.K <= 64 && k.mode != KNN_MODE_LIST) {
+  if ((kind >= 5 && kind <= 7) && k.K <= 64 && k.mode != KNN_MODE_LIST) {
     // chunk kernel, then the per-lane kernel on the chunks that overflowed its LDS gather
     HIPCHK(c, c->fb_list.ensure((size_t)nq * 4));
     HIPCHK(c, c->fb_count.ensure(4));
@@ -515,7 +513,7 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
     k.fb_list = c->fb_list.as<uint32_t>();
     k.fb_count = c->fb_count.as<uint32_t>();
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    launch_knn_chunk(k, c->chunk_cap, kind == 6, c->stream);
+    launch_knn_chunk(k, c->chunk_cap, kind - 5, c->stream);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->ev2, c->stream));
     uint32_t nfb = 0;
@@ -1064,6 +1062,11 @@ static int render_common(gi_ctx *c, int aa, int w, int h, const std::vector<int3
   unsigned long long s[ST_COUNT];
   HIPCHK(c, hipMemcpyAsync(s, c->d_stats.p, sizeof s, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (const char *kd = getenv("GI_KNN_DBG"); kd && (atoi(kd) & 16)) {
+    fprintf(stderr, "[gi] k-NN phase cycles (sum over waves):");
+    for (int i = 0; i < 16; i++) fprintf(stderr, " %llu", s[ST_PHASE + i]);
+    fprintf(stderr, "\n");
+  }
   if (st) {
     st->screen_rays = s[ST_RAY];
     st->shadow_rays = s[ST_SHADOW];

@@ -37,7 +37,8 @@ enum {
   ST_RAY = 0, ST_SHADOW, ST_MONTE, ST_TRANS, ST_SPEC, ST_INDIRECT, ST_CAUSTIC,
   ST_KNN, ST_KNN_PHOTONS, ST_KNN_VISITED,        // global map (caustic map: + ST_KNN_MAP)
   ST_KNN_C, ST_KNN_C_PHOTONS, ST_KNN_C_VISITED,
-  ST_COUNT = 16
+  ST_PHASE = 16,                                 // 16 diagnostic counters (GI_KNN_DBG & 16)
+  ST_COUNT = 32
 };
 enum { ST_KNN_MAP = ST_KNN_C - ST_KNN
 };
@@ -244,7 +245,7 @@ bool launch_knn_wave(const KnnArgs &a, int cap_mul, hipStream_t st);
 bool launch_knn_packet(const KnnArgs &a, hipStream_t st);
 bool launch_knn_lane(const KnnArgs &a, int chunk, int arity, hipStream_t st);
 bool launch_knn_group(const KnnArgs &a, int lanes, hipStream_t st);
-bool launch_knn_chunk(const KnnArgs &a, int cap, bool lane_heaps, hipStream_t st);
+bool launch_knn_chunk(const KnnArgs &a, int cap, int variant, hipStream_t st);  // 0 wave, 1 heaps, 2 lane select
 void launch_list_estimate(const KnnArgs &a, hipStream_t st);
 void launch_cached(const KnnArgs &a, hipStream_t st);
 void launch_photons(const PhotonArgs &a, bool emit, hipStream_t st);

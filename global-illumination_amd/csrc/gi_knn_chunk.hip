@@ -4,31 +4,33 @@
 // (photon_utils.cpp:72-162) per query: the K smallest (d2, kd-order index) keys with d2 <= r2.
 // The work is reorganised around the density of the queries. A frame issues ~150 M of them, and
 // 64 consecutive sorted queries span far less than one K-neighbourhood. One wave per chunk:
-//   1. bound: c = centre of the chunk's box B, rho = max |q - c|. Photons are on surfaces, so
-//      the kd leaf reached from c holds >= K photons; the K-th smallest metric d2 among them
-//      bounds d_K(c). Every query then has d_K(q) <= U = d_K(c) + rho (triangle inequality),
-//      and every photon of its K-NN lies within U of B.
+//   1. bound: c = centre of the chunk's box B, rho = max |q - c|. The exact d_K(c) is found from
+//      the photons near c (c's leaf gives a first radius, a gather within it the exact K-th).
+//      Every query then has d_K(q) <= d_K(c) + |q - c| <= U = d_K(c) + rho (triangle
+//      inequality), and every photon of its K-NN lies within U of B.
 //   2. gather: one wave-uniform kd traversal (box-to-box pruning) copies every photon within U
 //      of B into LDS (position, dir bits, rgbe, index), ballot-compacted.
-//   3. per query: each lane computes the keys of its LDS candidates into registers. A wave
-//      radix select (four 256-bin LDS histogram passes over the d2 bits, index bits only on
-//      exact ties) finds the K-th key. The kept photons' estimate terms are reduced across the
-//      wave in a fixed order.
+//   3. select, two variants:
+//      - lane select (knn_chunk_lane_kernel, default): lane j owns query j. Counting passes
+//        over the LDS candidates (every read is an LDS broadcast) narrow a d2 bracket with 16
+//        value-range bins each, until the K-th key's bracket holds <= 4 photons; a collect
+//        pass then keeps everything below the bracket and sorts the bracket by (d2, index).
+//        No cross-lane operations, no LDS atomics, all 64 queries advance together.
+//      - wave select (knn_chunk_kernel): one query at a time, 64 lanes compute its candidate
+//        keys and a wave-wide value-range bucket select keeps the K best.
+//   4. estimate: each lane estimates its own query from the LDS-staged photons it kept.
 // There is no per-query traversal and no per-query heap. The only global traffic per query is
 // its record and the LUT rows of the photons it keeps. Chunks whose gather exceeds the LDS
 // capacity (Morton jumps, sparse regions) go to a fallback list, and the per-lane kernel
 // (gi_knn.hip) answers those queries.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
+#include <type_traits>
 #include "gi_device.h"
 #include "gi_kernels.h"
 
 namespace gi {
 
-__device__ __forceinline__ double wsum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
 __device__ __forceinline__ float wmaxf(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
@@ -60,6 +62,12 @@ __device__ __forceinline__ float wave_sort(float v, int lane) {
   return v;
 }
 
+// photon metric: the reference's squared distance in fp32, one fixed operation order
+__device__ __forceinline__ float metric(float qx, float qy, float qz, const float4 &p) {
+  float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
+  return __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
+}
+
 // squared gap between a point/box and box B, same fp32 operation order as the photon metric
 __device__ __forceinline__ float gap2(float lx, float ly, float lz, float hx, float hy, float hz,
                                       const float *bl, const float *bh) {
@@ -67,49 +75,6 @@ __device__ __forceinline__ float gap2(float lx, float ly, float lz, float hx, fl
   float gy = fmaxf(fmaxf(ly - bh[1], bl[1] - hy), 0.0f);
   float gz = fmaxf(fmaxf(lz - bh[2], bl[2] - hz), 0.0f);
   return __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, __fmul_rn(gx, gx)));
-}
-
-// one radix digit over the register keys (PER per lane); returns the digit, updates need
-template <int PER>
-__device__ __forceinline__ uint32_t chunk_digit(uint32_t *hist, int lane, const uint64_t (&key)[PER],
-                                                bool low, int shift, uint32_t prefix,
-                                                uint32_t dprefix, uint32_t &need) {
-  hist[4 * lane] = hist[4 * lane + 1] = hist[4 * lane + 2] = hist[4 * lane + 3] = 0u;
-  __syncthreads();
-  uint32_t hm = (shift == 24) ? 0u : (0xffffffffu << (shift + 8));
-#pragma unroll
-  for (int u = 0; u < PER; u++) {
-    if (key[u] == ~0ull) continue;
-    uint32_t hi = (uint32_t)(key[u] >> 32), lo = (uint32_t)key[u];
-    uint32_t part = low ? lo : hi;
-    bool m = ((part ^ prefix) & hm) == 0u;
-    if (low) m = m && hi == dprefix;
-    if (m) atomicAdd(&hist[(part >> shift) & 255u], 1u);
-  }
-  __syncthreads();
-  uint32_t c0 = hist[4 * lane], c1 = hist[4 * lane + 1], c2 = hist[4 * lane + 2],
-           c3 = hist[4 * lane + 3];
-  uint32_t sum = c0 + c1 + c2 + c3, inc = sum;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t t = (uint32_t)__shfl_up((int)inc, o, 64);
-    if (lane >= o) inc += t;
-  }
-  uint32_t exc = inc - sum;
-  uint64_t hit = __ballot(exc < need && need <= inc);
-  int L = __ffsll((long long)hit) - 1;
-  uint32_t d = 0, before = exc;
-  if (lane == L) {
-    if (need <= before + c0) d = 0;
-    else if (need <= before + c0 + c1) { d = 1; before += c0; }
-    else if (need <= before + c0 + c1 + c2) { d = 2; before += c0 + c1; }
-    else { d = 3; before += c0 + c1 + c2; }
-    d = 4 * (uint32_t)lane + d;
-  }
-  need -= (uint32_t)__shfl((int)before, L, 64);
-  uint32_t digit = (uint32_t)__shfl((int)d, L, 64);
-  __syncthreads();
-  return digit;
 }
 
 // Keep exactly the K smallest (d2, kd index) of the wave's register keys (key = d2 bits << 32 |
@@ -121,298 +86,674 @@ __device__ __forceinline__ uint32_t chunk_digit(uint32_t *hist, int lane, const 
 template <int PER>
 __device__ __forceinline__ void wave_select_k(uint64_t (&key)[PER], int K, float mn, float mx,
                                               uint32_t *hist, const uint32_t *cidx, int lane) {
-        // value-range buckets: b(d2) = (d2 - min) * 255/(max - min) is monotone in d2, so the
-      // K-th key lies in the first bucket whose cumulative count reaches K
-      mn = wminf(mn);
-      mx = wmaxf(mx);
-      float scale = (mx > mn) ? 255.0f / (mx - mn) : 0.0f;
-      hist[4 * lane] = hist[4 * lane + 1] = hist[4 * lane + 2] = hist[4 * lane + 3] = 0u;
-      __syncthreads();
-      uint32_t bk[PER];
+  mn = wminf(mn);
+  mx = wmaxf(mx);
+  float scale = (mx > mn) ? 255.0f / (mx - mn) : 0.0f;
+  hist[4 * lane] = hist[4 * lane + 1] = hist[4 * lane + 2] = hist[4 * lane + 3] = 0u;
+  __syncthreads();
+  uint32_t bk[PER];
+#pragma unroll
+  for (int u = 0; u < PER; u++) {
+    bk[u] = 256u;
+    if (key[u] != ~0ull) {
+      float d2 = __uint_as_float((uint32_t)(key[u] >> 32));
+      bk[u] = min(255u, (uint32_t)((d2 - mn) * scale));
+      atomicAdd(&hist[bk[u]], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t c0 = hist[4 * lane], c1 = hist[4 * lane + 1], c2 = hist[4 * lane + 2],
+           c3 = hist[4 * lane + 3];
+  uint32_t sum = c0 + c1 + c2 + c3, inc = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t tt = (uint32_t)__shfl_up((int)inc, o, 64);
+    if (lane >= o) inc += tt;
+  }
+  uint32_t exc = inc - sum, need = (uint32_t)K;
+  uint64_t hit = __ballot(exc < need && need <= inc);
+  int Lh = __ffsll((long long)hit) - 1;
+  uint32_t d = 0, before = exc, cb = 0;
+  if (lane == Lh) {
+    if (need <= before + c0) { d = 0; cb = c0; }
+    else if (need <= before + c0 + c1) { d = 1; before += c0; cb = c1; }
+    else if (need <= before + c0 + c1 + c2) { d = 2; before += c0 + c1; cb = c2; }
+    else { d = 3; before += c0 + c1 + c2; cb = c3; }
+    d = 4 * (uint32_t)lane + d;
+  }
+  uint32_t B = (uint32_t)__shfl((int)d, Lh, 64);
+  uint32_t m = need - (uint32_t)__shfl((int)before, Lh, 64);  // keys needed from bucket B
+  cb = (uint32_t)__shfl((int)cb, Lh, 64);
+  __syncthreads();
+  // keep buckets < B, drop buckets > B; in B keep the m smallest (d2, kd index)
+  uint32_t take = 0;  // bit u: key u of this lane is in B and kept
+  if (m < cb) {
+    uint32_t cand = 0;
+#pragma unroll
+    for (int u = 0; u < PER; u++) cand |= (bk[u] == B) ? (1u << u) : 0u;
+    for (uint32_t it = 0; it < m; it++) {
+      uint64_t best = ~0ull;
+      int bu = -1;
 #pragma unroll
       for (int u = 0; u < PER; u++) {
-        bk[u] = 256u;
-        if (key[u] != ~0ull) {
-          float d2 = __uint_as_float((uint32_t)(key[u] >> 32));
-          bk[u] = min(255u, (uint32_t)((d2 - mn) * scale));
-          atomicAdd(&hist[bk[u]], 1u);
-        }
+        if (!((cand >> u) & 1u)) continue;
+        uint64_t rk = (key[u] & 0xffffffff00000000ull) | (uint64_t)cidx[(uint32_t)key[u]];
+        if (rk < best) { best = rk; bu = u; }
       }
-      __syncthreads();
-      uint32_t c0 = hist[4 * lane], c1 = hist[4 * lane + 1], c2 = hist[4 * lane + 2],
-               c3 = hist[4 * lane + 3];
-      uint32_t sum = c0 + c1 + c2 + c3, inc = sum;
+      uint64_t wbest = best;
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        uint32_t tt = (uint32_t)__shfl_up((int)inc, o, 64);
-        if (lane >= o) inc += tt;
+      for (int o = 32; o > 0; o >>= 1) {
+        uint64_t ob = (uint64_t)__shfl_xor((long long)wbest, o, 64);
+        wbest = ob < wbest ? ob : wbest;
       }
-      uint32_t exc = inc - sum, need = (uint32_t)K;
-      uint64_t hit = __ballot(exc < need && need <= inc);
-      int Lh = __ffsll((long long)hit) - 1;
-      uint32_t d = 0, before = exc, cb = 0;
-      if (lane == Lh) {
-        if (need <= before + c0) { d = 0; cb = c0; }
-        else if (need <= before + c0 + c1) { d = 1; before += c0; cb = c1; }
-        else if (need <= before + c0 + c1 + c2) { d = 2; before += c0 + c1; cb = c2; }
-        else { d = 3; before += c0 + c1 + c2; cb = c3; }
-        d = 4 * (uint32_t)lane + d;
-      }
-      uint32_t B = (uint32_t)__shfl((int)d, Lh, 64);
-      uint32_t m = need - (uint32_t)__shfl((int)before, Lh, 64);  // keys needed from bucket B
-      cb = (uint32_t)__shfl((int)cb, Lh, 64);
-      __syncthreads();
-      // keep buckets < B, drop buckets > B; in B keep the m smallest (d2, kd index)
-      uint32_t take = 0;  // bit u: key u of this lane is in B and kept
-      if (m < cb) {
-        uint32_t cand = 0;
-#pragma unroll
-        for (int u = 0; u < PER; u++) cand |= (bk[u] == B) ? (1u << u) : 0u;
-        for (uint32_t it = 0; it < m; it++) {
-          uint64_t best = ~0ull;
-          int bu = -1;
-#pragma unroll
-          for (int u = 0; u < PER; u++) {
-            if (!((cand >> u) & 1u)) continue;
-            uint64_t rk = (key[u] & 0xffffffff00000000ull) | (uint64_t)cidx[(uint32_t)key[u]];
-            if (rk < best) { best = rk; bu = u; }
-          }
-          uint64_t wbest = best;
-#pragma unroll
-          for (int o = 32; o > 0; o >>= 1) {
-            uint64_t ob = (uint64_t)__shfl_xor((long long)wbest, o, 64);
-            wbest = ob < wbest ? ob : wbest;
-          }
-          if (bu >= 0 && best == wbest) {
-            take |= 1u << bu;
-            cand &= ~(1u << bu);
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < PER; u++) {
-        if (key[u] == ~0ull) continue;
-        bool keep = bk[u] < B || (bk[u] == B && (m >= cb || ((take >> u) & 1u)));
-        if (!keep) key[u] = ~0ull;
+      if (bu >= 0 && best == wbest) {
+        take |= 1u << bu;
+        cand &= ~(1u << bu);
       }
     }
+  }
+#pragma unroll
+  for (int u = 0; u < PER; u++) {
+    if (key[u] == ~0ull) continue;
+    bool keep = bk[u] < B || (bk[u] == B && (m >= cb || ((take >> u) & 1u)));
+    if (!keep) key[u] = ~0ull;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// phases 1-2, shared by the chunk kernels
+// ---------------------------------------------------------------------------------------------
+struct ChunkGeom {
+  float bl[3], bh[3];  // the chunk's query box B
+  float cx, cy, cz;    // its centre c
+  double dkc;          // exact d_K(c) as a true-distance upper bound; -1 when not found
+  uint32_t count;      // candidates gathered into LDS
+  bool overflow;       // more than `cap` candidates: the chunk goes to the fallback
+};
+
+// Diagnostic counters of GI_KNN_DBG & 16 (ST_PHASE + i, summed over waves):
+//   0 bound cycles, 1 gather cycles, 2 select cycles, 3 estimate cycles, 4 bound+gather cycles
+//   of overflowing chunks, 5 kd nodes read by the bound, 6 by the gather, 7 chunks,
+//   8 counting passes (lane select), 9 queries handed to the fallback by the lane select
+struct ChunkProf {
+  bool on;
+  uint64_t t;
+  uint64_t c[10];
+  __device__ __forceinline__ void lap(int i) {
+    if (on) {
+      uint64_t n = clock64();
+      c[i] += n - t;
+      t = n;
+    }
+  }
+};
 
 template <int CAPC>
-__global__ __launch_bounds__(64) void knn_chunk_kernel(KnnArgs a) {
+__device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, bool valid, float4 qp,
+                                                   uint32_t cap, float4 *cpos, uint32_t *cidx,
+                                                   uint32_t *crgbe, uint32_t *hist, ChunkGeom &G,
+                                                   ChunkProf &P) {
   constexpr int PER = CAPC / 64;
-  __shared__ float4 cpos[CAPC];
-  __shared__ uint32_t cidx[CAPC];
-  __shared__ uint32_t crgbe[CAPC];
-  __shared__ uint32_t hist[256];
-  __shared__ uint16_t sel[64 * 64];   // kept LDS slots per query of the chunk (K <= 64)
-  __shared__ float smax[64];          // per query: K-th d2 (or -1 when fewer than K kept)
-  __shared__ int snum[64];
-  const int lane = threadIdx.x;
   const KdNode *nodes = reinterpret_cast<const KdNode *>(a.map.nodes);
   const float4 *pos = reinterpret_cast<const float4 *>(a.map.pos4);
   const int L = a.map.nleaves;
   const int64_t N = a.map.n;
   const int K = a.K;
-  uint64_t st_q = 0, st_found = 0, st_vis = 0;
-  for (int64_t chunk = blockIdx.x; chunk * 64 < a.nq; chunk += gridDim.x) {
-    // ---- 1. the chunk's queries, their box and the K-th distance bound
-    int64_t qs = chunk * 64 + lane;
-    bool valid = qs < a.nq;
-    int64_t qi = 0;
-    float4 qp = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (valid) {
-      qi = a.perm ? (int64_t)a.perm[a.q0 + qs] : a.q0 + qs;
-      qp = a.qpos[qi];
-      valid = __float_as_uint(qp.w) != QMETA_NONE;
+  float *bl = G.bl, *bh = G.bh;
+  bl[0] = wminf(valid ? qp.x : INFINITY); bh[0] = wmaxf(valid ? qp.x : -INFINITY);
+  bl[1] = wminf(valid ? qp.y : INFINITY); bh[1] = wmaxf(valid ? qp.y : -INFINITY);
+  bl[2] = wminf(valid ? qp.z : INFINITY); bh[2] = wmaxf(valid ? qp.z : -INFINITY);
+  const float cx = 0.5f * (bl[0] + bh[0]), cy = 0.5f * (bl[1] + bh[1]), cz = 0.5f * (bl[2] + bh[2]);
+  G.cx = cx; G.cy = cy; G.cz = cz;
+  double rho = 0.0;
+  if (valid) {
+    double dx = (double)qp.x - cx, dy = (double)qp.y - cy, dz = (double)qp.z - cz;
+    rho = sqrt(dx * dx + dy * dy + dz * dz);
+  }
+  rho = wmax(rho);
+  // ---- 1. U: r_max, tightened by the exact d_K(c)
+  double U = a.rmax;
+  G.dkc = -1.0;
+  if (N > 0 && K > 0) {
+    int node = 1;
+    while (node < L) {
+      KdNode nd = nodes[node];
+      float qa = kd_axis_q(__float_as_int(nd.hi.w), cx, cy, cz);
+      node = 2 * node + ((qa - nd.lo.w >= 0.0f) ? 1 : 0);
+      if (P.on) P.c[5]++;
     }
-    uint64_t vmask = __ballot(valid);
-    if (vmask == 0) continue;
-    float bl[3], bh[3];
-    bl[0] = wminf(valid ? qp.x : INFINITY); bh[0] = wmaxf(valid ? qp.x : -INFINITY);
-    bl[1] = wminf(valid ? qp.y : INFINITY); bh[1] = wmaxf(valid ? qp.y : -INFINITY);
-    bl[2] = wminf(valid ? qp.z : INFINITY); bh[2] = wmaxf(valid ? qp.z : -INFINITY);
-    float cx = 0.5f * (bl[0] + bh[0]), cy = 0.5f * (bl[1] + bh[1]), cz = 0.5f * (bl[2] + bh[2]);
-    double rho = 0.0;
-    if (valid) {
-      double dx = (double)qp.x - cx, dy = (double)qp.y - cy, dz = (double)qp.z - cz;
-      rho = sqrt(dx * dx + dy * dy + dz * dz);
-    }
-    rho = wmax(rho);
-    // U: r_max, tightened by the K-th metric d2 from c among the photons of c's leaf
-    double U = a.rmax;
-    double dkc = -1.0;  // exact d_K(c) (true-distance upper bound), when found
-    if (N > 0 && K > 0) {
-      int node = 1;
-      while (node < L) {
-        KdNode nd = nodes[node];
-        float qa = kd_axis_q(__float_as_int(nd.hi.w), cx, cy, cz);
-        node = 2 * node + ((qa - nd.lo.w >= 0.0f) ? 1 : 0);
-      }
-      int leaf = node - L;
-      int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
-      if (s1 - s0 >= K && K <= 64) {
-        float d2 = INFINITY;
-        if (s0 + lane < s1) {
-          float4 p = pos[s0 + lane];
-          float dx = cx - p.x, dy = cy - p.y, dz = cz - p.z;
-          d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
-        }
-        float sorted = wave_sort(d2, lane);
-        float dk2 = __shfl(sorted, K - 1, 64);  // >= d_K(c): K-th over a subset of photons
-        // exact d_K(c): gather the photons within that radius of c and select the K-th
-        float RA2 = __double2float_ru((double)dk2 * (1.0 + 1e-5));
-        uint32_t na = 0;
-        bool ovf = false;
-        int nd = 1;
-        while (true) {
-          KdNode b = nodes[nd];
-          if (kd_box_d2(b.lo, b.hi, cx, cy, cz) <= RA2) {
-            if (nd < L) {
-              float qa = kd_axis_q(__float_as_int(b.hi.w), cx, cy, cz);
-              nd = 2 * nd + ((qa - b.lo.w >= 0.0f) ? 1 : 0);
-              continue;
-            }
-            int lf = nd - L;
-            int64_t a0 = ((int64_t)lf * N) / L, a1 = ((int64_t)(lf + 1) * N) / L;
-            for (int64_t bb = a0; bb < a1; bb += 64) {
-              int64_t ii = bb + lane;
-              bool take = false;
-              float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-              if (ii < a1) {
-                p = pos[ii];
-                float dx = cx - p.x, dy = cy - p.y, dz = cz - p.z;
-                take = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx))) <= RA2;
-              }
-              uint64_t m = __ballot(take);
-              uint32_t nn = (uint32_t)__popcll(m);
-              if (na + nn > (uint32_t)CAPC) { ovf = true; break; }
-              if (take) {
-                uint32_t off = na + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                cpos[off] = p;
-                cidx[off] = (uint32_t)ii;
-              }
-              na += nn;
-            }
-            if (ovf) break;
-          }
-          while (nd != 1) {
-            const KdNode &pn = nodes[nd >> 1];
-            float qa = kd_axis_q(__float_as_int(pn.hi.w), cx, cy, cz);
-            if ((nd & 1) == ((qa - pn.lo.w >= 0.0f) ? 1 : 0)) break;
-            nd >>= 1;
-          }
-          if (nd == 1) break;
-          nd ^= 1;
-        }
-        __syncthreads();
-        if (!ovf && na >= (uint32_t)K) {
-          uint64_t kc[PER];
-          float mn = INFINITY, mx = -INFINITY;
-#pragma unroll
-          for (int u = 0; u < PER; u++) {
-            uint32_t s = (uint32_t)(u * 64 + lane);
-            kc[u] = ~0ull;
-            if (s < na) {
-              float4 p = cpos[s];
-              float dx = cx - p.x, dy = cy - p.y, dz = cz - p.z;
-              float dd = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
-              kc[u] = ((uint64_t)__float_as_uint(dd) << 32) | (uint64_t)s;
-              mn = fminf(mn, dd);
-              mx = fmaxf(mx, dd);
-            }
-          }
-          if (na > (uint32_t)K) wave_select_k<PER>(kc, K, wminf(mn), wmaxf(mx), hist, cidx, lane);
-          float km = 0.0f;
-#pragma unroll
-          for (int u = 0; u < PER; u++)
-            if (kc[u] != ~0ull) km = fmaxf(km, __uint_as_float((uint32_t)(kc[u] >> 32)));
-          dk2 = wmaxf(km);
-        }
-        __syncthreads();
-        // metric -> true distance: 1e-5 relative margin covers the fp32 rounding
-        dkc = sqrt((double)dk2 * (1.0 + 1e-5));
-        double ub = dkc + rho * (1.0 + 1e-6) + 1e-12;
-        if (ub < U) U = ub;
-      }
-    }
-    float U2 = __double2float_ru(U * U * (1.0 + 1e-5));
-    // ---- 2. gather every photon within U of the chunk's box into LDS
-    uint32_t count = 0;
-    bool overflow = false;
-    if (N > 0 && K > 0) {
-      int node = 1;
+    int leaf = node - L;
+    int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
+    if (s1 - s0 >= K && K <= 64) {
+      float d2 = INFINITY;
+      if (s0 + lane < s1) d2 = metric(cx, cy, cz, pos[s0 + lane]);
+      float sorted = wave_sort(d2, lane);
+      float dk2 = __shfl(sorted, K - 1, 64);  // >= d_K(c): K-th over a subset of photons
+      // exact d_K(c): gather the photons within that radius of c and select the K-th
+      float RA2 = __double2float_ru((double)dk2 * (1.0 + 1e-5));
+      uint32_t na = 0;
+      bool ovf = false;
+      int nd = 1;
       while (true) {
-        KdNode nd = nodes[node];
-        if (gap2(nd.lo.x, nd.lo.y, nd.lo.z, nd.hi.x, nd.hi.y, nd.hi.z, bl, bh) <= U2) {
-          if (node < L) {
-            float qa = kd_axis_q(__float_as_int(nd.hi.w), cx, cy, cz);
-            node = 2 * node + ((qa - nd.lo.w >= 0.0f) ? 1 : 0);
+        KdNode b = nodes[nd];
+        if (P.on) P.c[5]++;
+        if (kd_box_d2(b.lo, b.hi, cx, cy, cz) <= RA2) {
+          if (nd < L) {
+            float qa = kd_axis_q(__float_as_int(b.hi.w), cx, cy, cz);
+            nd = 2 * nd + ((qa - b.lo.w >= 0.0f) ? 1 : 0);
             continue;
           }
-          int leaf = node - L;
-          int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
-          for (int64_t b = s0; b < s1; b += 64) {
-            int64_t ii = b + lane;
+          int lf = nd - L;
+          int64_t a0 = ((int64_t)lf * N) / L, a1 = ((int64_t)(lf + 1) * N) / L;
+          for (int64_t bb = a0; bb < a1; bb += 64) {
+            int64_t ii = bb + lane;
             bool take = false;
             float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (ii < s1) {
+            if (ii < a1) {
               p = pos[ii];
-              take = gap2(p.x, p.y, p.z, p.x, p.y, p.z, bl, bh) <= U2;
+              take = metric(cx, cy, cz, p) <= RA2;
             }
             uint64_t m = __ballot(take);
             uint32_t nn = (uint32_t)__popcll(m);
-            if (count + nn > (uint32_t)CAPC) {
-              overflow = true;
-              break;
-            }
+            if (na + nn > (uint32_t)CAPC) { ovf = true; break; }
             if (take) {
-              uint32_t off = count + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+              uint32_t off = na + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
               cpos[off] = p;
               cidx[off] = (uint32_t)ii;
-              crgbe[off] = a.map.rgbe[ii];
             }
-            count += nn;
+            na += nn;
           }
-          if (overflow) break;
+          if (ovf) break;
         }
-        // stackless backtrack (near side by c)
-        while (node != 1) {
-          const KdNode &pn = nodes[node >> 1];
+        while (nd != 1) {
+          const KdNode &pn = nodes[nd >> 1];
           float qa = kd_axis_q(__float_as_int(pn.hi.w), cx, cy, cz);
-          int near_is_right = (qa - pn.lo.w >= 0.0f) ? 1 : 0;
-          if ((node & 1) == near_is_right) break;
-          node >>= 1;
+          if ((nd & 1) == ((qa - pn.lo.w >= 0.0f) ? 1 : 0)) break;
+          nd >>= 1;
         }
-        if (node == 1) break;
-        node ^= 1;
+        if (nd == 1) break;
+        nd ^= 1;
+      }
+      __syncthreads();
+      if (!ovf && na >= (uint32_t)K) {
+        uint64_t kc[PER];
+        float mn = INFINITY, mx = -INFINITY;
+#pragma unroll
+        for (int u = 0; u < PER; u++) {
+          uint32_t s = (uint32_t)(u * 64 + lane);
+          kc[u] = ~0ull;
+          if (s < na) {
+            float dd = metric(cx, cy, cz, cpos[s]);
+            kc[u] = ((uint64_t)__float_as_uint(dd) << 32) | (uint64_t)s;
+            mn = fminf(mn, dd);
+            mx = fmaxf(mx, dd);
+          }
+        }
+        if (na > (uint32_t)K) wave_select_k<PER>(kc, K, mn, mx, hist, cidx, lane);
+        float km = 0.0f;
+#pragma unroll
+        for (int u = 0; u < PER; u++)
+          if (kc[u] != ~0ull) km = fmaxf(km, __uint_as_float((uint32_t)(kc[u] >> 32)));
+        dk2 = wmaxf(km);
+      }
+      __syncthreads();
+      // metric -> true distance: 1e-5 relative margin covers the fp32 rounding
+      G.dkc = sqrt((double)dk2 * (1.0 + 1e-5));
+      double ub = G.dkc + rho * (1.0 + 1e-6) + 1e-12;
+      if (ub < U) U = ub;
+    }
+  }
+  const float U2 = __double2float_ru(U * U * (1.0 + 1e-5));
+  P.lap(0);
+  // ---- 2. gather every photon within U of the chunk's box into LDS
+  uint32_t count = 0;
+  bool overflow = false;
+  if (N > 0 && K > 0) {
+    int node = 1;
+    while (true) {
+      KdNode nd = nodes[node];
+      if (P.on) P.c[6]++;
+      if (gap2(nd.lo.x, nd.lo.y, nd.lo.z, nd.hi.x, nd.hi.y, nd.hi.z, bl, bh) <= U2) {
+        if (node < L) {
+          float qa = kd_axis_q(__float_as_int(nd.hi.w), cx, cy, cz);
+          node = 2 * node + ((qa - nd.lo.w >= 0.0f) ? 1 : 0);
+          continue;
+        }
+        int leaf = node - L;
+        int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
+        for (int64_t b = s0; b < s1; b += 64) {
+          int64_t ii = b + lane;
+          bool take = false;
+          float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (ii < s1) {
+            p = pos[ii];
+            take = gap2(p.x, p.y, p.z, p.x, p.y, p.z, bl, bh) <= U2;
+          }
+          uint64_t m = __ballot(take);
+          uint32_t nn = (uint32_t)__popcll(m);
+          if (count + nn > cap) {
+            overflow = true;
+            break;
+          }
+          if (take) {
+            uint32_t off = count + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            cpos[off] = p;
+            cidx[off] = (uint32_t)ii;
+            crgbe[off] = a.map.rgbe[ii];
+          }
+          count += nn;
+        }
+        if (overflow) break;
+      }
+      // stackless backtrack (near side by c)
+      while (node != 1) {
+        const KdNode &pn = nodes[node >> 1];
+        float qa = kd_axis_q(__float_as_int(pn.hi.w), cx, cy, cz);
+        int near_is_right = (qa - pn.lo.w >= 0.0f) ? 1 : 0;
+        if ((node & 1) == near_is_right) break;
+        node >>= 1;
+      }
+      if (node == 1) break;
+      node ^= 1;
+    }
+  }
+  G.count = count;
+  G.overflow = overflow;
+  if (P.on) {
+    uint64_t n = clock64();
+    P.c[overflow ? 4 : 1] += n - P.t;
+    P.t = n;
+    P.c[7]++;
+  }
+}
+
+// this query's own bound d_K(q) <= d_K(c) + |q - c| (tighter than the chunk's U), as an fp32
+// metric bound, capped by the accept radius
+__device__ __forceinline__ float query_lim2(const KnnArgs &a, const ChunkGeom &G, float qx, float qy,
+                                            float qz) {
+  float lim2 = a.r2f;
+  if (G.dkc >= 0.0) {
+    double ex = (double)qx - G.cx, ey = (double)qy - G.cy, ez = (double)qz - G.cz;
+    double uq = G.dkc + sqrt(ex * ex + ey * ey + ez * ez) * (1.0 + 1e-6) + 1e-12;
+    float uq2 = __double2float_ru(uq * uq * (1.0 + 1e-5));
+    if (uq2 < lim2) lim2 = uq2;
+  }
+  return lim2;
+}
+
+// hand the wave's valid queries to the per-lane fallback kernel
+__device__ __forceinline__ void to_fallback(const KnnArgs &a, uint64_t vmask, bool valid, int64_t qi,
+                                            int lane) {
+  uint32_t nv = (uint32_t)__popcll(vmask);
+  uint32_t base = 0;
+  if (lane == 0) base = atomicAdd(a.fb_count, nv);
+  base = (uint32_t)__shfl((int)base, 0, 64);
+  if (valid) a.fb_list[base + (uint32_t)__popcll(vmask & ((1ull << lane) - 1ull))] = (uint32_t)qi;
+}
+
+// ---- 4. the estimate of one query from LDS-staged photons (slot_at(s) = s-th kept slot).
+//         EstimateRadiance photon_utils.cpp:72-162 / irradiance :209-246
+template <typename SlotAt>
+__device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, float4 qp, int num,
+                                               float km, const float4 *cpos, const uint32_t *crgbe,
+                                               SlotAt slot_at) {
+  const int K = a.K;
+  double maxd2 = kEps;
+  double o0 = 0, o1 = 0, o2 = 0, tw = 0;
+  if (num > 0) {
+    maxd2 = (num < K) ? a.rmax * a.rmax : (double)km;
+    if (num == K && maxd2 < kEps) maxd2 = kEps;
+    if (a.mode == KNN_MODE_IRRADIANCE) {
+      for (int s = 0; s < num; s++) {
+        uint32_t e = crgbe[slot_at(s)];
+        uint32_t ex = e >> 24;
+        if (ex) {
+          double inv = ldexp(1.0, (int)ex - 128 - 8);
+          o0 += (double)(e & 255u) * inv;
+          o1 += (double)((e >> 8) & 255u) * inv;
+          o2 += (double)((e >> 16) & 255u) * inv;
+        }
+      }
+      double den = kPi * maxd2;
+      o0 /= den; o1 /= den; o2 /= den;
+    } else {
+      const QShade &sh = a.qshade[qi];
+      uint32_t meta = __float_as_uint(qp.w);
+      uint32_t sign = meta & 3u;
+      const DMaterial &mt = a.mats[meta >> 2];
+      double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
+      double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
+      bool spec = (mt.flags & MF_SPECULAR) || (mt.n < 0);
+      double c1 = 1.0, c2 = 1.0;
+      if (a.filter == 1) c1 = 1.0 / (a.fk * sqrt(maxd2));
+      else if (a.filter == 2) {
+        c1 = pow(2.7182818284590452354, -a.fb);
+        c2 = 1.0 / (2.0 * maxd2);
+      }
+      for (int s = 0; s < num; s++) {
+        uint32_t slot = slot_at(s);
+        float4 p = cpos[slot];
+        double d2 = (double)metric(qp.x, qp.y, qp.z, p);
+        uint32_t dcode = __float_as_uint(p.w) & 0xffffu;
+        double ix = a.lut[3 * dcode], iy = a.lut[3 * dcode + 1], iz = a.lut[3 * dcode + 2];
+        double perp = N0 * ix + N1 * iy + N2 * iz;
+        if ((sign == 2u && perp < 0) || (sign == 1u && perp > 0)) continue;
+        uint32_t e = crgbe[slot];
+        uint32_t ee = e >> 24;
+        double inv = ee ? ldexp(1.0, (int)ee - 128 - 8) : 0.0;
+        double p0 = ee ? (double)(e & 255u) * inv : 0.0;
+        double p1 = ee ? (double)((e >> 8) & 255u) * inv : 0.0;
+        double p2 = ee ? (double)((e >> 16) & 255u) * inv : 0.0;
+        double ca = E0 * -ix + E1 * -iy + E2 * -iz;
+        if (ca < 0) ca = 0;
+        double ap = fabs(perp);
+        double pw = spec ? pow(ca, mt.n) : 0.0;
+        p0 *= ap * mt.kd[0] + pw * mt.ks[0];
+        p1 *= ap * mt.kd[1] + pw * mt.ks[1];
+        p2 *= ap * mt.kd[2] + pw * mt.ks[2];
+        if (a.filter == 1) {
+          double f = (1.0 - c1 * sqrt(d2));
+          p0 *= f; p1 *= f; p2 *= f;
+        } else if (a.filter == 2) {
+          double w = (1.0 - (1.0 - pow(c1, c2 * d2)) / (1.0 - c1));
+          p0 *= w; p1 *= w; p2 *= w;
+          tw += w;
+        }
+        o0 += p0; o1 += p1; o2 += p2;
+      }
+      bool ok = true;
+      if (a.filter == 0 && maxd2 > 0) {
+        double den = kPi * maxd2;
+        o0 /= den; o1 /= den; o2 /= den;
+      } else if (a.filter == 1 && maxd2 > 0) {
+        double den = (1.0 - 2.0 / 3.0 / a.fk) * kPi * maxd2;
+        o0 /= den; o1 /= den; o2 /= den;
+      } else if (a.filter == 2 && tw > 0 && maxd2 > 0) {
+        double scl = a.fa * (num / tw) / (kPi * maxd2);
+        o0 *= scl; o1 *= scl; o2 *= scl;
+      } else {
+        ok = false;
+      }
+      if (ok) {
+        o0 *= sh.w[0]; o1 *= sh.w[1]; o2 *= sh.w[2];
+      } else {
+        o0 = o1 = o2 = 0;
       }
     }
-    if (overflow) {
-      // hand the chunk's queries to the per-lane fallback kernel
-      uint32_t nv = (uint32_t)__popcll(vmask);
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(a.fb_count, nv);
-      base = (uint32_t)__shfl((int)base, 0, 64);
-      if (valid) a.fb_list[base + (uint32_t)__popcll(vmask & ((1ull << lane) - 1ull))] = (uint32_t)qi;
+  }
+  a.out[3 * qi] = o0;
+  a.out[3 * qi + 1] = o1;
+  a.out[3 * qi + 2] = o2;
+  if (a.out_n) a.out_n[qi] = num;
+  if (a.out_maxd2) a.out_maxd2[qi] = (num > 0) ? (float)maxd2 : 0.0f;
+}
+
+__device__ __forceinline__ void chunk_load_query(const KnnArgs &a, int64_t chunk, int lane, bool &valid,
+                                                 int64_t &qi, float4 &qp) {
+  int64_t qs = chunk * 64 + lane;
+  valid = qs < a.nq;
+  qi = 0;
+  qp = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (valid) {
+    qi = a.perm ? (int64_t)a.perm[a.q0 + qs] : a.q0 + qs;
+    qp = a.qpos[qi];
+    valid = __float_as_uint(qp.w) != QMETA_NONE;
+  }
+}
+
+__device__ __forceinline__ void chunk_flush_stats(const KnnArgs &a, const ChunkProf &P, uint64_t q,
+                                                  uint64_t found, uint64_t vis) {
+  if (P.on && a.stats)
+    for (int i = 0; i < 10; i++) wave_add(&a.stats[ST_PHASE + i], P.c[i]);
+  if (a.stats) {
+    wave_add(&a.stats[ST_KNN + a.stat_off], q);
+    wave_add(&a.stats[ST_KNN_PHOTONS + a.stat_off], found);
+    wave_add(&a.stats[ST_KNN_VISITED + a.stat_off], vis);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// lane select: one query per lane, counting passes over the LDS candidates
+// ---------------------------------------------------------------------------------------------
+constexpr int LS_BR = 4;       // bracket photons resolved by the collect pass
+constexpr int LS_PASSES = 10;  // counting passes before a query goes to the fallback
+
+// value-range bin of d2 in the bracket binning (lo, sc): monotone non-decreasing in d2, 0 at lo
+// (also for sc = inf), 15 at the bracket's top
+__device__ __forceinline__ uint32_t bin16(float d2, float lo, float sc) {
+  float t = (d2 - lo) * sc;
+  t = (t > 0.0f) ? t : 0.0f;
+  return (t >= 15.0f) ? 15u : (uint32_t)t;
+}
+
+// smallest float x in (lo, hi] with bin16(x) >= b, for 1 <= b <= 15, lo < hi, bin16(hi) == 15
+__device__ __forceinline__ float bin_floor(uint32_t b, float lo, float hi, float sc) {
+  uint32_t l = __float_as_uint(lo), h = __float_as_uint(hi);  // bin(l) < b <= bin(h)
+  float g = lo + (float)b / sc;
+  if (g > lo && g < hi) {
+    uint32_t gb = __float_as_uint(g);
+    uint32_t gl = (gb - l > 64u) ? gb - 64u : l;
+    uint32_t gh = (h - gb > 64u) ? gb + 64u : h;
+    if (bin16(__uint_as_float(gl), lo, sc) < b) l = gl;
+    if (bin16(__uint_as_float(gh), lo, sc) >= b) h = gh;
+  }
+  while (h - l > 1u) {
+    uint32_t m = l + ((h - l) >> 1);
+    if (bin16(__uint_as_float(m), lo, sc) >= b) h = m;
+    else l = m;
+  }
+  return __uint_as_float(h);
+}
+
+__device__ __forceinline__ float next_up(float x) { return __uint_as_float(__float_as_uint(x) + 1u); }
+__device__ __forceinline__ float next_down(float x) { return __uint_as_float(__float_as_uint(x) - 1u); }
+
+template <int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE)))
+void knn_chunk_lane_kernel(KnnArgs a) {
+  constexpr int CAPC = 256;
+  __shared__ float4 cpos[CAPC];
+  __shared__ uint32_t cidx[CAPC];
+  __shared__ uint32_t crgbe[CAPC];
+  __shared__ uint32_t hist[256];
+  __shared__ uint8_t sel[64 * 64];  // kept LDS slots, [s][lane] (K <= 64)
+  const int lane = threadIdx.x;
+  const int K = a.K;
+  uint64_t st_q = 0, st_found = 0, st_vis = 0;
+  ChunkProf P;
+  P.on = (a.dbg & 16) != 0;
+  P.t = 0;
+  for (int i = 0; i < 10; i++) P.c[i] = 0;
+  for (int64_t chunk = blockIdx.x; chunk * 64 < a.nq; chunk += gridDim.x) {
+    bool valid;
+    int64_t qi;
+    float4 qp;
+    chunk_load_query(a, chunk, lane, valid, qi, qp);
+    uint64_t vmask = __ballot(valid);
+    if (vmask == 0) continue;
+    if (P.on) P.t = clock64();
+    ChunkGeom G;
+    // byte counters below: at most 255 candidates per chunk
+    chunk_bound_gather<CAPC>(a, lane, valid, qp, CAPC - 1, cpos, cidx, crgbe, hist, G, P);
+    if (G.overflow) {
+      to_fallback(a, vmask, valid, qi, lane);
       __syncthreads();
       continue;
     }
     __syncthreads();
-    // ---- 3. each query of the chunk against the LDS candidates
-    for (int j = 0; j < 64 && !(a.dbg & 4); j++) {
-      if (!((vmask >> j) & 1ull)) continue;
-      float qx = __shfl(qp.x, j, 64), qy = __shfl(qp.y, j, 64), qz = __shfl(qp.z, j, 64);
-      int64_t qj = (int64_t)__shfl((int)(qi & 0xffffffff), j, 64) |
-                   ((int64_t)__shfl((int)(qi >> 32), j, 64) << 32);
-      uint32_t meta = __float_as_uint(__shfl(qp.w, j, 64));
-      // this query's own bound d_K(q) <= d_K(c) + |q - c| (tighter than the chunk's U)
-      float lim2 = a.r2f;
-      if (dkc >= 0.0) {
-        double ex = (double)qx - cx, ey = (double)qy - cy, ez = (double)qz - cz;
-        double uq = dkc + sqrt(ex * ex + ey * ey + ez * ez) * (1.0 + 1e-6) + 1e-12;
-        float uq2 = __double2float_ru(uq * uq * (1.0 + 1e-5));
-        if (uq2 < lim2) lim2 = uq2;
+    const uint32_t count = G.count;
+    const float qx = qp.x, qy = qp.y, qz = qp.z;
+    // ---- 3. lane select. State: every valid candidate with d2 < A is kept; `need` more come
+    //         from the bracket [A, B] (smallest (d2, kd index) first); above B nothing is kept.
+    float A = 0.0f, B = query_lim2(a, G, qx, qy, qz);
+    int need = (valid && K > 0) ? K : 0;
+    int mode = need > 0 ? 1 : 0;  // 1 counting, 2 bracket resolved by the collect pass, 0 done
+    if (!(a.dbg & 4)) {
+      for (int pass = 0; pass < LS_PASSES && __ballot(mode == 1); pass++) {
+        if (P.on) P.c[8]++;
+        const bool on = mode == 1;
+        const float sc = 16.0f / (B - A);
+        uint64_t w0 = 0, w1 = 0;  // 16 bins x 8-bit counters
+#pragma unroll 4
+        for (uint32_t s = 0; s < count; s++) {
+          float d2 = metric(qx, qy, qz, cpos[s]);
+          bool mem = on && d2 >= A && d2 <= B;
+          uint32_t b = bin16(d2, A, sc);
+          uint64_t inc = mem ? (1ull << ((b & 7u) << 3)) : 0ull;
+          if (b & 8u) w1 += inc;
+          else w0 += inc;
+        }
+        if (on) {
+          uint32_t before = 0, bs = 16, cb = 0;
+#pragma unroll
+          for (int b = 0; b < 16; b++) {
+            uint32_t c = (uint32_t)(((b < 8) ? (w0 >> (8 * b)) : (w1 >> (8 * (b - 8)))) & 255ull);
+            if (bs == 16) {
+              if (before + c >= (uint32_t)need) { bs = (uint32_t)b; cb = c; }
+              else before += c;
+            }
+          }
+          if (bs == 16) {
+            // fewer members than needed (first pass: fewer than K within the bound): keep all
+            A = next_up(B);
+            need = 0;
+            mode = 0;
+          } else {
+            need -= (int)before;
+            float nA = (bs == 0) ? A : bin_floor(bs, A, B, sc);
+            float nB = (bs == 15) ? B : next_down(bin_floor(bs + 1, A, B, sc));
+            if (cb == (uint32_t)need) {
+              A = next_up(nB);
+              need = 0;
+              mode = 0;
+            } else {
+              A = nA;
+              B = nB;
+              if (cb <= (uint32_t)LS_BR) mode = 2;
+              else if (!(B > A)) mode = 3;  // more than LS_BR photons tied at one d2
+            }
+          }
+        }
       }
+    }
+    // queries the counting passes did not resolve go to the exact per-lane kernel
+    const bool fb = mode == 1 || mode == 3;
+    uint64_t fbm = __ballot(fb);
+    if (fbm) {
+      if (fb) a.fb_list[atomicAdd(a.fb_count, 1u)] = (uint32_t)qi;
+      if (P.on) P.c[9] += (uint64_t)__popcll(fbm);
+    }
+    const bool col = valid && !fb && !(a.dbg & 4);
+    // collect: everything below A, and the bracket's photons into a small register buffer
+    int n = 0;
+    float km = 0.0f;
+    uint64_t br[LS_BR];
+#pragma unroll
+    for (int i = 0; i < LS_BR; i++) br[i] = ~0ull;
+    const bool inb_on = col && need > 0;
+#pragma unroll 4
+    for (uint32_t s = 0; s < count; s++) {
+      float d2 = metric(qx, qy, qz, cpos[s]);
+      if (col && d2 < A) {
+        sel[n * 64 + lane] = (uint8_t)s;
+        n++;
+        km = fmaxf(km, d2);
+      }
+      if (inb_on && d2 >= A && d2 <= B) {
+#pragma unroll
+        for (int i = LS_BR - 1; i > 0; i--) br[i] = br[i - 1];
+        br[0] = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)s;
+      }
+    }
+    if (inb_on) {
+      // sort the bracket by (d2, kd index) and keep `need` of it
+      uint64_t fk[LS_BR];
+      uint32_t sl[LS_BR];
+#pragma unroll
+      for (int i = 0; i < LS_BR; i++) {
+        sl[i] = (uint32_t)br[i];
+        fk[i] = (br[i] == ~0ull) ? ~0ull : ((br[i] & 0xffffffff00000000ull) | (uint64_t)cidx[sl[i] & 255u]);
+      }
+#pragma unroll
+      for (int i = 0; i < LS_BR; i++)
+#pragma unroll
+        for (int j = 0; j + 1 < LS_BR - i; j++)
+          if (fk[j + 1] < fk[j]) {
+            uint64_t t = fk[j]; fk[j] = fk[j + 1]; fk[j + 1] = t;
+            uint32_t u = sl[j]; sl[j] = sl[j + 1]; sl[j + 1] = u;
+          }
+#pragma unroll
+      for (int i = 0; i < LS_BR; i++)
+        if (i < need) {
+          sel[n * 64 + lane] = (uint8_t)sl[i];
+          n++;
+          km = fmaxf(km, __uint_as_float((uint32_t)(fk[i] >> 32)));
+        }
+    }
+    P.lap(2);
+    // ---- 4. estimate
+    if (col && !(a.dbg & 2))
+      chunk_estimate(a, qi, qp, n, km, cpos, crgbe,
+                     [&](int s) { return (uint32_t)sel[s * 64 + lane]; });
+    if (col) {
+      st_q += 1;
+      st_found += (uint64_t)n;
+      st_vis += count;
+    }
+    __syncthreads();
+    P.lap(3);
+  }
+  chunk_flush_stats(a, P, st_q, st_found, st_vis);
+}
+
+// ---------------------------------------------------------------------------------------------
+// wave select: one query at a time across the wave
+// ---------------------------------------------------------------------------------------------
+template <int CAPC, int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE)))
+void knn_chunk_kernel(KnnArgs a) {
+  constexpr int PER = CAPC / 64;
+  using SlotT = typename std::conditional<(CAPC <= 256), uint8_t, uint16_t>::type;
+  __shared__ float4 cpos[CAPC];
+  __shared__ uint32_t cidx[CAPC];
+  __shared__ uint32_t crgbe[CAPC];
+  __shared__ uint32_t hist[256];
+  __shared__ SlotT sel[64 * 64];      // kept LDS slots per query of the chunk (K <= 64)
+  __shared__ float smax[64];          // per query: K-th d2
+  __shared__ int snum[64];
+  const int lane = threadIdx.x;
+  const int K = a.K;
+  uint64_t st_q = 0, st_found = 0, st_vis = 0;
+  ChunkProf P;
+  P.on = (a.dbg & 16) != 0;
+  P.t = 0;
+  for (int i = 0; i < 10; i++) P.c[i] = 0;
+  for (int64_t chunk = blockIdx.x; chunk * 64 < a.nq; chunk += gridDim.x) {
+    bool valid;
+    int64_t qi;
+    float4 qp;
+    chunk_load_query(a, chunk, lane, valid, qi, qp);
+    uint64_t vmask = __ballot(valid);
+    if (vmask == 0) continue;
+    if (P.on) P.t = clock64();
+    ChunkGeom G;
+    chunk_bound_gather<CAPC>(a, lane, valid, qp, CAPC, cpos, cidx, crgbe, hist, G, P);
+    if (G.overflow) {
+      to_fallback(a, vmask, valid, qi, lane);
+      __syncthreads();
+      continue;
+    }
+    __syncthreads();
+    const uint32_t count = G.count;
+    // ---- 3. each query of the chunk against the LDS candidates
+    for (int j = 0; j < 64; j++) {
+      if (!((vmask >> j) & 1ull)) continue;
+      if (a.dbg & 4) {
+        if (lane == 0) { snum[j] = 0; smax[j] = 0.0f; }
+        continue;
+      }
+      float qx = __shfl(qp.x, j, 64), qy = __shfl(qp.y, j, 64), qz = __shfl(qp.z, j, 64);
+      float lim2 = query_lim2(a, G, qx, qy, qz);
       // key = d2 bits << 32 | LDS slot; ~0 = not a candidate (beyond the bound or past count)
       uint64_t key[PER];
       uint32_t nvalid = 0;
@@ -422,9 +763,7 @@ __global__ __launch_bounds__(64) void knn_chunk_kernel(KnnArgs a) {
         uint32_t s = (uint32_t)(u * 64 + lane);
         key[u] = ~0ull;
         if (s < count) {
-          float4 p = cpos[s];
-          float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
-          float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
+          float d2 = metric(qx, qy, qz, cpos[s]);
           if (d2 <= lim2) {
             key[u] = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)s;
             mn = fminf(mn, d2);
@@ -444,7 +783,7 @@ __global__ __launch_bounds__(64) void knn_chunk_kernel(KnnArgs a) {
         uint64_t bm = __ballot(kp);
         if (kp) {
           sel[j * 64 + base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull))] =
-              (uint16_t)(uint32_t)key[u];
+              (SlotT)(uint32_t)key[u];
           km = fmaxf(km, __uint_as_float((uint32_t)(key[u] >> 32)));
         }
         base += (uint32_t)__popcll(bm);
@@ -453,115 +792,28 @@ __global__ __launch_bounds__(64) void knn_chunk_kernel(KnnArgs a) {
       if (lane == 0) {
         snum[j] = num;
         smax[j] = km;
-        st_q += 1;
-        st_found += (uint64_t)num;
-        st_vis += count;
       }
     }
     __syncthreads();
-    // ---- 4. estimates, one query per lane (photon data from LDS; latencies overlap across
-    //         the 64 lanes). EstimateRadiance photon_utils.cpp:72-162 / Irradiance :209-246
-    if (valid && !(a.dbg & 2)) {
+    P.lap(2);
+    if (valid) {
       int num = snum[lane];
-      double maxd2 = kEps;
-      double o0 = 0, o1 = 0, o2 = 0, tw = 0;
-      if (num > 0) {
-        maxd2 = (num < K) ? a.rmax * a.rmax : (double)smax[lane];
-        if (num == K && maxd2 < kEps) maxd2 = kEps;
-        if (a.mode == KNN_MODE_IRRADIANCE) {
-          for (int s = 0; s < num; s++) {
-            uint32_t e = crgbe[sel[lane * 64 + s]];
-            uint32_t ex = e >> 24;
-            if (ex) {
-              double inv = ldexp(1.0, (int)ex - 128 - 8);
-              o0 += (double)(e & 255u) * inv;
-              o1 += (double)((e >> 8) & 255u) * inv;
-              o2 += (double)((e >> 16) & 255u) * inv;
-            }
-          }
-          double den = kPi * maxd2;
-          o0 /= den; o1 /= den; o2 /= den;
-        } else {
-          const QShade &sh = a.qshade[qi];
-          uint32_t meta = __float_as_uint(qp.w);
-          uint32_t sign = meta & 3u;
-          const DMaterial &mt = a.mats[meta >> 2];
-          double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
-          double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
-          bool spec = (mt.flags & MF_SPECULAR) || (mt.n < 0);
-          double c1 = 1.0, c2 = 1.0;
-          if (a.filter == 1) c1 = 1.0 / (a.fk * sqrt(maxd2));
-          else if (a.filter == 2) {
-            c1 = pow(2.7182818284590452354, -a.fb);
-            c2 = 1.0 / (2.0 * maxd2);
-          }
-          for (int s = 0; s < num; s++) {
-            uint32_t slot = sel[lane * 64 + s];
-            float4 p = cpos[slot];
-            float dx = qp.x - p.x, dy = qp.y - p.y, dz = qp.z - p.z;
-            double d2 = (double)__builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
-            uint32_t dcode = __float_as_uint(p.w) & 0xffffu;
-            double ix = a.lut[3 * dcode], iy = a.lut[3 * dcode + 1], iz = a.lut[3 * dcode + 2];
-            double perp = N0 * ix + N1 * iy + N2 * iz;
-            if ((sign == 2u && perp < 0) || (sign == 1u && perp > 0)) continue;
-            uint32_t e = crgbe[slot];
-            uint32_t ee = e >> 24;
-            double inv = ee ? ldexp(1.0, (int)ee - 128 - 8) : 0.0;
-            double p0 = ee ? (double)(e & 255u) * inv : 0.0;
-            double p1 = ee ? (double)((e >> 8) & 255u) * inv : 0.0;
-            double p2 = ee ? (double)((e >> 16) & 255u) * inv : 0.0;
-            double ca = E0 * -ix + E1 * -iy + E2 * -iz;
-            if (ca < 0) ca = 0;
-            double ap = fabs(perp);
-            double pw = spec ? pow(ca, mt.n) : 0.0;
-            p0 *= ap * mt.kd[0] + pw * mt.ks[0];
-            p1 *= ap * mt.kd[1] + pw * mt.ks[1];
-            p2 *= ap * mt.kd[2] + pw * mt.ks[2];
-            if (a.filter == 1) {
-              double f = (1.0 - c1 * sqrt(d2));
-              p0 *= f; p1 *= f; p2 *= f;
-            } else if (a.filter == 2) {
-              double w = (1.0 - (1.0 - pow(c1, c2 * d2)) / (1.0 - c1));
-              p0 *= w; p1 *= w; p2 *= w;
-              tw += w;
-            }
-            o0 += p0; o1 += p1; o2 += p2;
-          }
-          bool ok = true;
-          if (a.filter == 0 && maxd2 > 0) {
-            double den = kPi * maxd2;
-            o0 /= den; o1 /= den; o2 /= den;
-          } else if (a.filter == 1 && maxd2 > 0) {
-            double den = (1.0 - 2.0 / 3.0 / a.fk) * kPi * maxd2;
-            o0 /= den; o1 /= den; o2 /= den;
-          } else if (a.filter == 2 && tw > 0 && maxd2 > 0) {
-            double scl = a.fa * (num / tw) / (kPi * maxd2);
-            o0 *= scl; o1 *= scl; o2 *= scl;
-          } else {
-            ok = false;
-          }
-          if (ok) {
-            o0 *= sh.w[0]; o1 *= sh.w[1]; o2 *= sh.w[2];
-          } else {
-            o0 = o1 = o2 = 0;
-          }
-        }
-      }
-      a.out[3 * qi] = o0;
-      a.out[3 * qi + 1] = o1;
-      a.out[3 * qi + 2] = o2;
-      if (a.out_n) a.out_n[qi] = num;
-      if (a.out_maxd2) a.out_maxd2[qi] = (num > 0) ? (float)maxd2 : 0.0f;
+      if (!(a.dbg & 2))
+        chunk_estimate(a, qi, qp, num, smax[lane], cpos, crgbe,
+                       [&](int s) { return (uint32_t)sel[lane * 64 + s]; });
+      st_q += 1;
+      st_found += (uint64_t)num;
+      st_vis += count;
     }
     __syncthreads();
+    P.lap(3);
   }
-  if (a.stats && lane == 0) {
-    if (st_q) atomicAdd(&a.stats[ST_KNN + a.stat_off], (unsigned long long)st_q);
-    if (st_found) atomicAdd(&a.stats[ST_KNN_PHOTONS + a.stat_off], (unsigned long long)st_found);
-    if (st_vis) atomicAdd(&a.stats[ST_KNN_VISITED + a.stat_off], (unsigned long long)st_vis);
-  }
+  chunk_flush_stats(a, P, st_q, st_found, st_vis);
 }
 
+// ---------------------------------------------------------------------------------------------
+// per-lane heaps over centre-sorted candidates (experiment, slower; kept for comparison)
+// ---------------------------------------------------------------------------------------------
 // ascending bitonic sort of PER*64 u64 keys held as key[u] at index u*64 + lane
 template <int PER>
 __device__ __forceinline__ void wave_bitonic_sort(uint64_t (&k)[PER], int lane) {
@@ -604,196 +856,28 @@ __global__ __launch_bounds__(64) void knn_chunk_heap_kernel(KnnArgs a) {
   extern __shared__ uint64_t hsm[];   // per-lane 4-ary heaps [K][64]
   uint64_t *h = hsm + threadIdx.x;
   const int lane = threadIdx.x;
-  const KdNode *nodes = reinterpret_cast<const KdNode *>(a.map.nodes);
-  const float4 *pos = reinterpret_cast<const float4 *>(a.map.pos4);
-  const int L = a.map.nleaves;
-  const int64_t N = a.map.n;
   const int K = a.K;
   uint64_t st_q = 0, st_found = 0, st_vis = 0;
+  ChunkProf P;
+  P.on = false;
+  P.t = 0;
+  for (int i = 0; i < 10; i++) P.c[i] = 0;
   for (int64_t chunk = blockIdx.x; chunk * 64 < a.nq; chunk += gridDim.x) {
-    // ---- 1. the chunk's queries, their box and the K-th distance bound
-    int64_t qs = chunk * 64 + lane;
-    bool valid = qs < a.nq;
-    int64_t qi = 0;
-    float4 qp = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (valid) {
-      qi = a.perm ? (int64_t)a.perm[a.q0 + qs] : a.q0 + qs;
-      qp = a.qpos[qi];
-      valid = __float_as_uint(qp.w) != QMETA_NONE;
-    }
+    bool valid;
+    int64_t qi;
+    float4 qp;
+    chunk_load_query(a, chunk, lane, valid, qi, qp);
     uint64_t vmask = __ballot(valid);
     if (vmask == 0) continue;
-    float bl[3], bh[3];
-    bl[0] = wminf(valid ? qp.x : INFINITY); bh[0] = wmaxf(valid ? qp.x : -INFINITY);
-    bl[1] = wminf(valid ? qp.y : INFINITY); bh[1] = wmaxf(valid ? qp.y : -INFINITY);
-    bl[2] = wminf(valid ? qp.z : INFINITY); bh[2] = wmaxf(valid ? qp.z : -INFINITY);
-    float cx = 0.5f * (bl[0] + bh[0]), cy = 0.5f * (bl[1] + bh[1]), cz = 0.5f * (bl[2] + bh[2]);
-    double rho = 0.0;
-    if (valid) {
-      double dx = (double)qp.x - cx, dy = (double)qp.y - cy, dz = (double)qp.z - cz;
-      rho = sqrt(dx * dx + dy * dy + dz * dz);
-    }
-    rho = wmax(rho);
-    // U: r_max, tightened by the K-th metric d2 from c among the photons of c's leaf
-    double U = a.rmax;
-    double dkc = -1.0;  // exact d_K(c) (true-distance upper bound), when found
-    if (N > 0 && K > 0) {
-      int node = 1;
-      while (node < L) {
-        KdNode nd = nodes[node];
-        float qa = kd_axis_q(__float_as_int(nd.hi.w), cx, cy, cz);
-        node = 2 * node + ((qa - nd.lo.w >= 0.0f) ? 1 : 0);
-      }
-      int leaf = node - L;
-      int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
-      if (s1 - s0 >= K && K <= 64) {
-        float d2 = INFINITY;
-        if (s0 + lane < s1) {
-          float4 p = pos[s0 + lane];
-          float dx = cx - p.x, dy = cy - p.y, dz = cz - p.z;
-          d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
-        }
-        float sorted = wave_sort(d2, lane);
-        float dk2 = __shfl(sorted, K - 1, 64);  // >= d_K(c): K-th over a subset of photons
-        // exact d_K(c): gather the photons within that radius of c and select the K-th
-        float RA2 = __double2float_ru((double)dk2 * (1.0 + 1e-5));
-        uint32_t na = 0;
-        bool ovf = false;
-        int nd = 1;
-        while (true) {
-          KdNode b = nodes[nd];
-          if (kd_box_d2(b.lo, b.hi, cx, cy, cz) <= RA2) {
-            if (nd < L) {
-              float qa = kd_axis_q(__float_as_int(b.hi.w), cx, cy, cz);
-              nd = 2 * nd + ((qa - b.lo.w >= 0.0f) ? 1 : 0);
-              continue;
-            }
-            int lf = nd - L;
-            int64_t a0 = ((int64_t)lf * N) / L, a1 = ((int64_t)(lf + 1) * N) / L;
-            for (int64_t bb = a0; bb < a1; bb += 64) {
-              int64_t ii = bb + lane;
-              bool take = false;
-              float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-              if (ii < a1) {
-                p = pos[ii];
-                float dx = cx - p.x, dy = cy - p.y, dz = cz - p.z;
-                take = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx))) <= RA2;
-              }
-              uint64_t m = __ballot(take);
-              uint32_t nn = (uint32_t)__popcll(m);
-              if (na + nn > (uint32_t)CAPC) { ovf = true; break; }
-              if (take) {
-                uint32_t off = na + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                cpos[off] = p;
-                cidx[off] = (uint32_t)ii;
-              }
-              na += nn;
-            }
-            if (ovf) break;
-          }
-          while (nd != 1) {
-            const KdNode &pn = nodes[nd >> 1];
-            float qa = kd_axis_q(__float_as_int(pn.hi.w), cx, cy, cz);
-            if ((nd & 1) == ((qa - pn.lo.w >= 0.0f) ? 1 : 0)) break;
-            nd >>= 1;
-          }
-          if (nd == 1) break;
-          nd ^= 1;
-        }
-        __syncthreads();
-        if (!ovf && na >= (uint32_t)K) {
-          uint64_t kc[PER];
-          float mn = INFINITY, mx = -INFINITY;
-#pragma unroll
-          for (int u = 0; u < PER; u++) {
-            uint32_t s = (uint32_t)(u * 64 + lane);
-            kc[u] = ~0ull;
-            if (s < na) {
-              float4 p = cpos[s];
-              float dx = cx - p.x, dy = cy - p.y, dz = cz - p.z;
-              float dd = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
-              kc[u] = ((uint64_t)__float_as_uint(dd) << 32) | (uint64_t)s;
-              mn = fminf(mn, dd);
-              mx = fmaxf(mx, dd);
-            }
-          }
-          if (na > (uint32_t)K) wave_select_k<PER>(kc, K, wminf(mn), wmaxf(mx), hist, cidx, lane);
-          float km = 0.0f;
-#pragma unroll
-          for (int u = 0; u < PER; u++)
-            if (kc[u] != ~0ull) km = fmaxf(km, __uint_as_float((uint32_t)(kc[u] >> 32)));
-          dk2 = wmaxf(km);
-        }
-        __syncthreads();
-        // metric -> true distance: 1e-5 relative margin covers the fp32 rounding
-        dkc = sqrt((double)dk2 * (1.0 + 1e-5));
-        double ub = dkc + rho * (1.0 + 1e-6) + 1e-12;
-        if (ub < U) U = ub;
-      }
-    }
-    float U2 = __double2float_ru(U * U * (1.0 + 1e-5));
-    // ---- 2. gather every photon within U of the chunk's box into LDS
-    uint32_t count = 0;
-    bool overflow = false;
-    if (N > 0 && K > 0) {
-      int node = 1;
-      while (true) {
-        KdNode nd = nodes[node];
-        if (gap2(nd.lo.x, nd.lo.y, nd.lo.z, nd.hi.x, nd.hi.y, nd.hi.z, bl, bh) <= U2) {
-          if (node < L) {
-            float qa = kd_axis_q(__float_as_int(nd.hi.w), cx, cy, cz);
-            node = 2 * node + ((qa - nd.lo.w >= 0.0f) ? 1 : 0);
-            continue;
-          }
-          int leaf = node - L;
-          int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
-          for (int64_t b = s0; b < s1; b += 64) {
-            int64_t ii = b + lane;
-            bool take = false;
-            float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (ii < s1) {
-              p = pos[ii];
-              take = gap2(p.x, p.y, p.z, p.x, p.y, p.z, bl, bh) <= U2;
-            }
-            uint64_t m = __ballot(take);
-            uint32_t nn = (uint32_t)__popcll(m);
-            if (count + nn > (uint32_t)CAPC) {
-              overflow = true;
-              break;
-            }
-            if (take) {
-              uint32_t off = count + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-              cpos[off] = p;
-              cidx[off] = (uint32_t)ii;
-              crgbe[off] = a.map.rgbe[ii];
-            }
-            count += nn;
-          }
-          if (overflow) break;
-        }
-        // stackless backtrack (near side by c)
-        while (node != 1) {
-          const KdNode &pn = nodes[node >> 1];
-          float qa = kd_axis_q(__float_as_int(pn.hi.w), cx, cy, cz);
-          int near_is_right = (qa - pn.lo.w >= 0.0f) ? 1 : 0;
-          if ((node & 1) == near_is_right) break;
-          node >>= 1;
-        }
-        if (node == 1) break;
-        node ^= 1;
-      }
-    }
-    if (overflow) {
-      // hand the chunk's queries to the per-lane fallback kernel
-      uint32_t nv = (uint32_t)__popcll(vmask);
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(a.fb_count, nv);
-      base = (uint32_t)__shfl((int)base, 0, 64);
-      if (valid) a.fb_list[base + (uint32_t)__popcll(vmask & ((1ull << lane) - 1ull))] = (uint32_t)qi;
+    ChunkGeom G;
+    chunk_bound_gather<CAPC>(a, lane, valid, qp, CAPC, cpos, cidx, crgbe, hist, G, P);
+    if (G.overflow) {
+      to_fallback(a, vmask, valid, qi, lane);
       __syncthreads();
       continue;
     }
     __syncthreads();
+    const uint32_t count = G.count;
     // ---- 3. sort the candidates by distance to c, then every lane scans them for its own
     //         query into its LDS heap: all lanes read the same candidate (LDS broadcast), and
     //         near-first order keeps replacements rare after the Floyd-built fill
@@ -804,9 +888,7 @@ __global__ __launch_bounds__(64) void knn_chunk_heap_kernel(KnnArgs a) {
         uint32_t s = (uint32_t)(u * 64 + lane);
         kc[u] = ~0ull;
         if (s < count) {
-          float4 p = cpos[s];
-          float dx = cx - p.x, dy = cy - p.y, dz = cz - p.z;
-          float dd = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
+          float dd = metric(G.cx, G.cy, G.cz, cpos[s]);
           kc[u] = ((uint64_t)__float_as_uint(dd) << 32) | (uint64_t)s;
         }
       }
@@ -820,114 +902,25 @@ __global__ __launch_bounds__(64) void knn_chunk_heap_kernel(KnnArgs a) {
     __syncthreads();
     int size = 0;
     if (!(a.dbg & 4)) {
-      float lim2 = a.r2f;
-      if (valid && dkc >= 0.0) {
-        double ex = (double)qp.x - cx, ey = (double)qp.y - cy, ez = (double)qp.z - cz;
-        double uq = dkc + sqrt(ex * ex + ey * ey + ez * ez) * (1.0 + 1e-6) + 1e-12;
-        float uq2 = __double2float_ru(uq * uq * (1.0 + 1e-5));
-        if (uq2 < lim2) lim2 = uq2;
-      }
+      float lim2 = valid ? query_lim2(a, G, qp.x, qp.y, qp.z) : 0.0f;
       uint64_t lim = valid ? (((uint64_t)__float_as_uint(lim2) + 1ull) << 32) : 0ull;
       for (uint32_t i = 0; i < count; i++) {
         uint32_t slot = ord[i];
-        float4 p = cpos[slot];
-        float dx = qp.x - p.x, dy = qp.y - p.y, dz = qp.z - p.z;
-        float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
+        float d2 = metric(qp.x, qp.y, qp.z, cpos[slot]);
         uint64_t key = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)cidx[slot];
         if (key < lim) heapn_accept<4>(h, size, K, key, lim);
       }
     }
-    // ---- 4. estimate from the lane's heap (EstimateRadiance photon_utils.cpp:72-162)
+    // ---- 4. estimate from the lane's heap (kd indices mapped back to their LDS slots)
     if (valid && !(a.dbg & 2)) {
-      int num = size;
-      double maxd2 = kEps;
-      double o0 = 0, o1 = 0, o2 = 0, tw = 0;
-      if (num > 0) {
-        maxd2 = (num < K) ? a.rmax * a.rmax : (double)__uint_as_float((uint32_t)(h[0] >> 32));
-        if (num == K && maxd2 < kEps) maxd2 = kEps;
-        if (a.mode == KNN_MODE_IRRADIANCE) {
-          for (int s = 0; s < num; s++) {
-            uint32_t e = a.map.rgbe[(uint32_t)h[s * 64]];
-            uint32_t ex = e >> 24;
-            if (ex) {
-              double inv = ldexp(1.0, (int)ex - 128 - 8);
-              o0 += (double)(e & 255u) * inv;
-              o1 += (double)((e >> 8) & 255u) * inv;
-              o2 += (double)((e >> 16) & 255u) * inv;
-            }
-          }
-          double den = kPi * maxd2;
-          o0 /= den; o1 /= den; o2 /= den;
-        } else {
-          const QShade &sh = a.qshade[qi];
-          uint32_t meta = __float_as_uint(qp.w);
-          uint32_t sign = meta & 3u;
-          const DMaterial &mt = a.mats[meta >> 2];
-          double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
-          double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
-          bool spec = (mt.flags & MF_SPECULAR) || (mt.n < 0);
-          double c1 = 1.0, c2 = 1.0;
-          if (a.filter == 1) c1 = 1.0 / (a.fk * sqrt(maxd2));
-          else if (a.filter == 2) {
-            c1 = pow(2.7182818284590452354, -a.fb);
-            c2 = 1.0 / (2.0 * maxd2);
-          }
-          for (int s = 0; s < num; s++) {
-            uint64_t key = h[s * 64];
-            uint32_t id = (uint32_t)key;
-            double d2 = (double)__uint_as_float((uint32_t)(key >> 32));
-            uint32_t dcode = __float_as_uint(a.map.pos4[4 * (int64_t)id + 3]) & 0xffffu;
-            double ix = a.lut[3 * dcode], iy = a.lut[3 * dcode + 1], iz = a.lut[3 * dcode + 2];
-            double perp = N0 * ix + N1 * iy + N2 * iz;
-            if ((sign == 2u && perp < 0) || (sign == 1u && perp > 0)) continue;
-            uint32_t e = a.map.rgbe[id];
-            uint32_t ee = e >> 24;
-            double inv = ee ? ldexp(1.0, (int)ee - 128 - 8) : 0.0;
-            double p0 = ee ? (double)(e & 255u) * inv : 0.0;
-            double p1 = ee ? (double)((e >> 8) & 255u) * inv : 0.0;
-            double p2 = ee ? (double)((e >> 16) & 255u) * inv : 0.0;
-            double ca = E0 * -ix + E1 * -iy + E2 * -iz;
-            if (ca < 0) ca = 0;
-            double ap = fabs(perp);
-            double pw = spec ? pow(ca, mt.n) : 0.0;
-            p0 *= ap * mt.kd[0] + pw * mt.ks[0];
-            p1 *= ap * mt.kd[1] + pw * mt.ks[1];
-            p2 *= ap * mt.kd[2] + pw * mt.ks[2];
-            if (a.filter == 1) {
-              double f = (1.0 - c1 * sqrt(d2));
-              p0 *= f; p1 *= f; p2 *= f;
-            } else if (a.filter == 2) {
-              double w = (1.0 - (1.0 - pow(c1, c2 * d2)) / (1.0 - c1));
-              p0 *= w; p1 *= w; p2 *= w;
-              tw += w;
-            }
-            o0 += p0; o1 += p1; o2 += p2;
-          }
-          bool ok = true;
-          if (a.filter == 0 && maxd2 > 0) {
-            double den = kPi * maxd2;
-            o0 /= den; o1 /= den; o2 /= den;
-          } else if (a.filter == 1 && maxd2 > 0) {
-            double den = (1.0 - 2.0 / 3.0 / a.fk) * kPi * maxd2;
-            o0 /= den; o1 /= den; o2 /= den;
-          } else if (a.filter == 2 && tw > 0 && maxd2 > 0) {
-            double scl = a.fa * (num / tw) / (kPi * maxd2);
-            o0 *= scl; o1 *= scl; o2 *= scl;
-          } else {
-            ok = false;
-          }
-          if (ok) {
-            o0 *= sh.w[0]; o1 *= sh.w[1]; o2 *= sh.w[2];
-          } else {
-            o0 = o1 = o2 = 0;
-          }
-        }
-      }
-      a.out[3 * qi] = o0;
-      a.out[3 * qi + 1] = o1;
-      a.out[3 * qi + 2] = o2;
-      if (a.out_n) a.out_n[qi] = num;
-      if (a.out_maxd2) a.out_maxd2[qi] = (num > 0) ? (float)maxd2 : 0.0f;
+      float km = size ? __uint_as_float((uint32_t)(h[0] >> 32)) : 0.0f;
+      chunk_estimate(a, qi, qp, size, km, cpos, crgbe, [&](int s) {
+        uint32_t id = (uint32_t)h[s * 64];
+        uint32_t slot = 0;
+        for (uint32_t t = 0; t < count; t++)
+          if (cidx[t] == id) { slot = t; break; }
+        return slot;
+      });
     }
     if (valid) {
       st_q += 1;
@@ -936,27 +929,34 @@ __global__ __launch_bounds__(64) void knn_chunk_heap_kernel(KnnArgs a) {
     }
     __syncthreads();
   }
-  if (a.stats) {
-    wave_add(&a.stats[ST_KNN + a.stat_off], st_q);
-    wave_add(&a.stats[ST_KNN_PHOTONS + a.stat_off], st_found);
-    wave_add(&a.stats[ST_KNN_VISITED + a.stat_off], st_vis);
-  }
+  chunk_flush_stats(a, P, st_q, st_found, st_vis);
 }
 
-bool launch_knn_chunk(const KnnArgs &a, int cap, bool lane_heaps, hipStream_t st) {
+// variant: 0 wave select, 1 per-lane heaps, 2 lane select
+bool launch_knn_chunk(const KnnArgs &a, int cap, int variant, hipStream_t st) {
   if (a.nq == 0) return true;
   if (a.mode == KNN_MODE_LIST || a.K > 64) return false;
   int64_t chunks = (a.nq + 63) / 64;
   unsigned grid = (unsigned)(chunks < (1 << 17) ? chunks : (1 << 17));
-  if (lane_heaps) {
+  static const int wpe = getenv("GI_CHUNK_WPE") ? atoi(getenv("GI_CHUNK_WPE")) : 3;
+  if (variant == 1) {
     size_t lds = (size_t)a.K * 64 * sizeof(uint64_t);
     if (cap <= 256) knn_chunk_heap_kernel<256><<<grid, 64, lds, st>>>(a);
     else knn_chunk_heap_kernel<512><<<grid, 64, lds, st>>>(a);
     return true;
   }
-  if (cap <= 256) knn_chunk_kernel<256><<<grid, 64, 0, st>>>(a);
-  else if (cap <= 512) knn_chunk_kernel<512><<<grid, 64, 0, st>>>(a);
-  else knn_chunk_kernel<1024><<<grid, 64, 0, st>>>(a);
+  if (variant == 2) {
+    if (wpe >= 4) knn_chunk_lane_kernel<4><<<grid, 64, 0, st>>>(a);
+    else if (wpe == 3) knn_chunk_lane_kernel<3><<<grid, 64, 0, st>>>(a);
+    else knn_chunk_lane_kernel<2><<<grid, 64, 0, st>>>(a);
+    return true;
+  }
+  if (cap <= 256) {
+    if (wpe >= 4) knn_chunk_kernel<256, 4><<<grid, 64, 0, st>>>(a);
+    else if (wpe == 3) knn_chunk_kernel<256, 3><<<grid, 64, 0, st>>>(a);
+    else knn_chunk_kernel<256, 2><<<grid, 64, 0, st>>>(a);
+  } else if (cap <= 512) knn_chunk_kernel<512, 2><<<grid, 64, 0, st>>>(a);
+  else knn_chunk_kernel<1024, 1><<<grid, 64, 0, st>>>(a);
   return true;
 }
 

@@ -32,6 +32,8 @@ VARIANTS = [
     {"GI_KNN_KERNEL": "5", "GI_CHUNK_CAP": "256", "GI_LEAF_SIZE": "50"},
     {"GI_KNN_KERNEL": "6"},
     {"GI_KNN_KERNEL": "6", "GI_CHUNK_CAP": "256"},
+    {"GI_KNN_KERNEL": "7"},
+    {"GI_KNN_KERNEL": "7", "GI_LEAF_SIZE": "50"},
 ]
 
 
@@ -113,6 +115,42 @@ def test_variant_dense_queries(env, filt, k, r):
     try:
         ph = synth.photon_map(200000, seed=13)
         q = clustered_queries(8192, 17, k, r, filt)
+        fk = 1.25 if filt == CONE else 1.0
+        p = gi_amd.default_params()
+        p.filter_const_k = fk
+        r_.set_params(p)
+        r_.set_photon_map(GLOBAL, ph)
+        g, gn, gm = r_.EstimateRadiance(GLOBAL, q)
+    finally:
+        r_.close()
+    o, on, om = oracle_lib.estimate_radiance(ph, q, filter_k=fk)
+    np.testing.assert_array_equal(gn, on)
+    np.testing.assert_array_equal(gm, om)
+    np.testing.assert_allclose(g, o, rtol=1e-10, atol=1e-300)
+
+
+@pytest.mark.parametrize("env", VARIANTS, ids=lambda e: "-".join(f"{k[3:]}{v}" for k, v in e.items()))
+@pytest.mark.parametrize("k,filt", [(50, DISK), (8, CONE), (50, CONE)])
+def test_variant_tied_distances(env, k, filt):
+    """Photons and queries snapped to a coarse grid on one face: ~40 photons share each
+    position and many keys share one d2, so the K-th distance is tied across many photons
+    (the lane select's bracket cannot split them and hands such queries to the fallback).
+    Which tied photon is kept follows the kd order, and the GPU and oracle kd builds order
+    photons with equal coordinates differently, so every photon carries the same power and
+    direction: the estimate then depends only on the multiset of the K smallest d2, which is
+    unique, and must match exactly."""
+    r_ = make_renderer(env)
+    try:
+        ph = synth.photon_map(40000, seed=23)
+        rng = np.random.default_rng(29)
+        pts = np.zeros((len(ph), 3), dtype=np.float32)
+        pts[:, 0] = np.round(0.3 + rng.random(len(ph)) * 0.3, 2)
+        pts[:, 2] = np.round(0.4 + rng.random(len(ph)) * 0.3, 2)
+        ph["pos"] = pts
+        ph["rgbe"][:] = ph["rgbe"][0]
+        ph["dir"][:] = ph["dir"][0]
+        q = clustered_queries(4096, 31, k, 0.2, filt)
+        q["point"] = np.round(q["point"], 2)
         fk = 1.25 if filt == CONE else 1.0
         p = gi_amd.default_params()
         p.filter_const_k = fk

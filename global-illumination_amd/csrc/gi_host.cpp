@@ -217,7 +217,9 @@ struct gi_ctx {
   int lane_chunk = 8;             // per-lane kernel: photon loads in flight per lane
   int group_lanes = 16;           // group kernel: lanes per query
   int heap_arity = 4;             // per-lane kernel: d-ary heap
-  int ind_waves = 2;              // indirect-path kernel occupancy target                // per-lane kernel: sorted queries per lane (bound reuse)       // per-lane kernel: heap in global memory even for K <= 64           // query-per-wave kernel: candidate buffer = mul * pow2(K+64)
+  int ind_waves = 3;              // indirect-path kernel occupancy target (waves per SIMD)
+  DBuf ind_cont, ind_ncont;       // indirect paths that continue past their first bounce
+  bool split_ind = true;          // continuation queue for indirect paths (else one loop per lane)
   // render scratch
   DBuf spawn, npaths, path_off, nmc, mc_off, nind, ind_off, base, pixels, rgbf, rgb8, gheap_d2, gheap_idx, qcount, stats_bak;
   DBuf qpos[2], qshade[2], qkey[2], qout[2];
@@ -672,6 +674,7 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     a.nprim = nprim;
     a.stats = c->d_stats.as<unsigned long long>();
     a.ind_waves = c->ind_waves;
+    a.split_ind = c->split_ind;
     if (const char *s = getenv("GI_DBG")) a.dbg = atoi(s);
     HIPCHK(c, c->spawn.ensure((size_t)nprim * sizeof(Spawn)));
     HIPCHK(c, c->npaths.ensure((size_t)nprim * 4));
@@ -707,6 +710,12 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     a.total_ind = totals[2];
     HIPCHK(c, c->base.ensure((size_t)total_paths * 24));
     a.base = c->base.as<double>();
+    if (a.split_ind && a.total_ind > 0) {
+      HIPCHK(c, c->ind_cont.ensure((size_t)a.total_ind * sizeof(IndCont)));
+      HIPCHK(c, c->ind_ncont.ensure(4));
+      a.ind_cont = c->ind_cont.as<IndCont>();
+      a.ind_ncont = c->ind_ncont.as<uint32_t>();
+    }
     // single Monte Carlo pass; grow the query lists and re-run on overflow
     uint32_t nq[2] = {0, 0};
     HIPCHK(c, hipMemcpyAsync(c->stats_bak.p, c->d_stats.p, ST_COUNT * 8,
@@ -838,6 +847,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_GROUP_LANES")) c->group_lanes = std::max(1, atoi(s));
   if (const char *s = getenv("GI_HEAP_ARITY")) c->heap_arity = std::max(2, atoi(s));
   if (const char *s = getenv("GI_IND_WAVES")) c->ind_waves = std::max(1, atoi(s));
+  if (const char *s = getenv("GI_SPLIT_IND")) c->split_ind = atoi(s) != 0;
   if (const char *s = getenv("GI_SORT_QUERIES")) c->sort_queries = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_KERNEL")) c->knn_kernel_kind = atoi(s);
   *out = c;
@@ -850,7 +860,7 @@ void gi_destroy(gi_ctx *c) {
   DBuf *bufs[] = {&c->d_nodes, &c->d_elems, &c->d_shapes, &c->d_tris, &c->d_mats, &c->d_lights,
                   &c->d_lut, &c->d_stats, &c->spawn, &c->npaths, &c->path_off, &c->base,
                   &c->pixels, &c->rgbf, &c->rgb8, &c->gheap_d2, &c->gheap_idx, &c->qcount,
-                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf};
+                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont};
   for (DBuf *b : bufs) b->release();
   for (int l = 0; l < 2; l++) {
     c->qpos[l].release(); c->qshade[l].release(); c->qkey[l].release(); c->qout[l].release();

@@ -27,6 +27,19 @@ struct Spawn {
 };
 
 // shading half of a photon-map query (search half is float4 {x, y, z, meta})
+// an indirect sample path whose first bounce hit a material with a specular or transmissive
+// term: the state of MonteCarlo_IndirectSample's loop (montecarlo.cpp:177-305) at that hit,
+// queued so the shading and the rest of the path run compacted in ind_cont_kernel
+struct IndCont {
+  double org[3];          // origin of the traced ray (the loop's ray_start)
+  double hp[3], hn[3];    // hit point and normal
+  double w[3];            // outer weight W (throughput is still 1)
+  uint64_t rkey, rctr;    // RNG stream position
+  uint32_t g, prim;       // path slot, primary sample
+  uint32_t pslot, qslot;  // slot within the primary, deterministic global-query slot
+  int32_t mat, pad;
+};
+
 struct QShade {
   double n[3];   // surface normal
   double ex[3];  // exact reflection direction (Phong lobe term)
@@ -64,6 +77,9 @@ struct RenderArgs {
   int64_t total_mc, total_ind;
   int32_t ind_waves;    // occupancy target of the indirect-path kernel (waves per SIMD)
   int32_t dbg;          // diagnostics: 1 = skip the indirect trace, 2 = skip diffuse sampling too
+  int32_t split_ind;    // 1: indirect paths trace their first bounce, continuations are queued
+  IndCont *ind_cont;    // [total_ind] continuation queue
+  uint32_t *ind_ncont;  // its length (device counter)
   int64_t qind_base;    // global list: indirect path t owns slot qind_base + t
   // query lists (0 = global map, 1 = caustic map). Deterministic slots first: list l slot p
   // = primary sample p's own query (slot-0 path), then (global list only) slot

@@ -219,53 +219,74 @@ __device__ __forceinline__ void global_query(PathCtx &P, V p, V n, V ex, double 
   put_query(P, 0, p, n, ex, ct, mat, w);
 }
 
-// MonteCarlo_IndirectSample, montecarlo.cpp:177-305 (W = outer weight of this path)
-__device__ __forceinline__ void mc_indirect_body(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
+// The shading half of one iteration of MonteCarlo_IndirectSample's loop, montecarlo.cpp:
+// 177-305, at hit h of the ray from org (W = outer weight of the path, tw = throughput so far;
+// org is also the loop's ray_start). Returns true when the path continues with the bounced ray
+// in (org, dir). DIFFUSE_ONLY: the material has no specular/transmissive term (kt = ks = 0,
+// opaque): R = pt = ps = 0 exactly, so only the query/absorb outcomes remain and the branches
+// with pow/acos/asin/tan are not compiled in.
+template <bool DIFFUSE_ONLY>
+__device__ __forceinline__ bool ind_shade(PathCtx &P, const Hit &h, V &org, V &dir, Rng &rng, C3 W,
+                                          C3 &tw) {
   const SceneView &S = *P.S;
   const Flags &F = *P.F;
-  C3 tw = rgb(1, 1, 1);
-  V ray_start = org;
-  for (int iter = 0; iter < F.max_monte_depth; iter++) {
-    Hit h;
-    if (!scene_intersect(S, org, dir, h)) {
-      P.base += W * (tw * ldc(S.background));
-      break;
-    }
-    P.cnt.monte++;
-    const DMaterial &m = S.mats[h.mat];
-    V view = normalize(h.p - ray_start);
-    double ct = dot(h.n, -view);
-    double R = 0;
-    if (F.fresnel && (m.flags & MF_TRANSPARENT)) R = reflection_coeff(F.ir_air, ct, m.ir);
-    double pd = m.max_kd, pt = m.max_kt;
-    double ps = m.max_ks + R * pt;
-    pt *= (1.0 - R);
-    double pterm = m.max_e + F.prob_absorb;
-    double ptot = pd + pt + ps + pterm;
-    double rnd = rng.next();
-    if (ptot > 1.0) rnd *= ptot;
-    V sb;
-    if (rnd < pd) {
-      V ex = reflective_bounce(h.n, view, ct);
-      global_query(P, h.p, h.n, ex, ct, h.mat, W * (ldc(m.kd) * tw / pd));
-      break;
-    } else if (rnd < pd + pt) {
-      V ex = transmissive_bounce(F.ir_air, h.n, view, ct, m.ir);
-      sb = F.distrib_trans ? specular_sample(ex, m.n, ct, rng) : ex;
-      P.cnt.trans++;
-      tw *= (1.0 - R) * ldc(m.kt) / pt;
-    } else if (rnd < pd + pt + ps) {
-      V ex = reflective_bounce(h.n, view, ct);
-      sb = F.distrib_spec ? specular_sample(ex, m.n, ct, rng) : ex;
-      P.cnt.spec++;
-      tw *= (ldc(m.ks) + R * ldc(m.kt)) / ps;
-    } else {
-      break;
-    }
-    ray_start = h.p + sb * kEps;
-    org = ray_start;
-    dir = sb;
+  const DMaterial &m = S.mats[h.mat];
+  V view = normalize(h.p - org);
+  double ct = dot(h.n, -view);
+  double R = 0;
+  if (!DIFFUSE_ONLY && F.fresnel && (m.flags & MF_TRANSPARENT)) R = reflection_coeff(F.ir_air, ct, m.ir);
+  double pd = m.max_kd, pt = m.max_kt;
+  double ps = m.max_ks + R * pt;
+  pt *= (1.0 - R);
+  double pterm = m.max_e + F.prob_absorb;
+  double ptot = pd + pt + ps + pterm;
+  double rnd = rng.next();
+  if (ptot > 1.0) rnd *= ptot;
+  if (rnd < pd) {
+    V ex = reflective_bounce(h.n, view, ct);
+    global_query(P, h.p, h.n, ex, ct, h.mat, W * (ldc(m.kd) * tw / pd));
+    return false;
   }
+  if (DIFFUSE_ONLY) return false;
+  V sb;
+  if (rnd < pd + pt) {
+    V ex = transmissive_bounce(F.ir_air, h.n, view, ct, m.ir);
+    sb = F.distrib_trans ? specular_sample(ex, m.n, ct, rng) : ex;
+    P.cnt.trans++;
+    tw *= (1.0 - R) * ldc(m.kt) / pt;
+  } else if (rnd < pd + pt + ps) {
+    V ex = reflective_bounce(h.n, view, ct);
+    sb = F.distrib_spec ? specular_sample(ex, m.n, ct, rng) : ex;
+    P.cnt.spec++;
+    tw *= (ldc(m.ks) + R * ldc(m.kt)) / ps;
+  } else {
+    return false;
+  }
+  org = h.p + sb * kEps;
+  dir = sb;
+  return true;
+}
+
+__device__ __forceinline__ bool diffuse_only(const DMaterial &m) {
+  return !(m.flags & MF_TRANSPARENT) && m.max_kt == 0.0 && m.max_ks == 0.0;
+}
+
+// one full iteration: trace, then shade (background on a miss)
+__device__ __forceinline__ bool ind_bounce(PathCtx &P, V &org, V &dir, Rng &rng, C3 W, C3 &tw) {
+  Hit h;
+  if (!scene_intersect(*P.S, org, dir, h)) {
+    P.base += W * (tw * ldc(P.S->background));
+    return false;
+  }
+  P.cnt.monte++;
+  return ind_shade<false>(P, h, org, dir, rng, W, tw);
+}
+
+// MonteCarlo_IndirectSample, montecarlo.cpp:177-305 (W = outer weight of this path)
+__device__ __forceinline__ void mc_indirect_body(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
+  C3 tw = rgb(1, 1, 1);
+  for (int iter = 0; iter < P.F->max_monte_depth; iter++)
+    if (!ind_bounce(P, org, dir, rng, W, tw)) break;
 }
 
 __device__ __noinline__ void mc_indirect(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
@@ -424,11 +445,17 @@ __global__ __launch_bounds__(256) void slot0_kernel(RenderArgs a) {
   path_stats(a, cnt);
 }
 
-// IndirectIllumination sample s of primary pb (raytracer.cpp:112-135)
-template <int W>
+// IndirectIllumination sample s of primary pb (raytracer.cpp:112-135). With split_ind the
+// kernel traces the first bounce and shades it only when the hit material is diffuse-only.
+// Nearly every wave has a lane or two whose ray hits the glass, and shading that inline would
+// make all 64 lanes execute the Fresnel pow, refraction trig and Phong-lobe sampling (and hold
+// them idle through the glass bounces). Such paths are queued at the hit (wave-aggregated
+// append) and finish compacted in ind_cont_kernel; the arithmetic and RNG stream are unchanged.
+template <int W, bool SPLIT>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void ind_kernel(RenderArgs a) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   Counts cnt = {0, 0, 0, 0, 0, 0};
+  bool queue = false;
   if (t < a.total_ind) {
     int64_t pb = wave_owner(a.ind_off, a.nprim, t, a.total_ind);
     int s = (int)(t - a.ind_off[pb]);
@@ -446,16 +473,91 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void i
     rng.init(a.F.seed, KIND_IND, psample, (uint64_t)s);
     V p = ld3(sp.p), n = ld3(sp.n);
     V sb = (a.dbg >= 2) ? n : diffuse_sample(n, sp.ct, rng);
-    if (a.dbg == 0) mc_indirect_body(P, p + sb * kEps, sb, rng, ldc(m.kd) / (double)sp.n_i);
-    else P.base = rgb(sb.x, sb.y, sb.z);
-    if (P.fixed[0] >= 0) put_none(a, 0, P.fixed[0]);
+    C3 Wt = ldc(m.kd) / (double)sp.n_i;
+    if (a.dbg != 0) {
+      P.base = rgb(sb.x, sb.y, sb.z);
+    } else if (!SPLIT) {
+      mc_indirect_body(P, p + sb * kEps, sb, rng, Wt);
+    } else if (a.F.max_monte_depth > 0) {
+      V org = p + sb * kEps, dir = sb;
+      C3 tw = rgb(1, 1, 1);
+      Hit h;
+      if (!scene_intersect(a.S, org, dir, h)) {
+        P.base += Wt * (tw * ldc(a.S.background));
+      } else {
+        P.cnt.monte++;
+        if (diffuse_only(a.S.mats[h.mat])) {
+          ind_shade<true>(P, h, org, dir, rng, Wt, tw);
+        } else {
+          // glass / mirror hit: shaded in ind_cont_kernel (wave-aggregated append)
+          queue = true;
+          uint64_t act = __ballot(1);
+          int lane = (int)(threadIdx.x & 63);
+          int leader = __ffsll((long long)act) - 1;
+          uint32_t base = 0;
+          if (lane == leader) base = atomicAdd(a.ind_ncont, (uint32_t)__popcll(act));
+          base = (uint32_t)__shfl((int)base, leader, 64);
+          IndCont &q = a.ind_cont[base + (uint32_t)__popcll(act & ((1ull << lane) - 1ull))];
+          q.org[0] = org.x; q.org[1] = org.y; q.org[2] = org.z;
+          q.hp[0] = h.p.x; q.hp[1] = h.p.y; q.hp[2] = h.p.z;
+          q.hn[0] = h.n.x; q.hn[1] = h.n.y; q.hn[2] = h.n.z;
+          q.w[0] = Wt.r; q.w[1] = Wt.g; q.w[2] = Wt.b;
+          q.rkey = rng.key;
+          q.rctr = rng.ctr;
+          q.g = (uint32_t)g;
+          q.prim = (uint32_t)pb;
+          q.pslot = (uint32_t)pslot;
+          q.qslot = (uint32_t)P.fixed[0];
+          q.mat = h.mat;
+        }
+      }
+    }
     P.cnt.indirect++;
-    a.base[3 * g] = P.base.r;
-    a.base[3 * g + 1] = P.base.g;
-    a.base[3 * g + 2] = P.base.b;
+    if (!queue) {
+      if (P.fixed[0] >= 0) put_none(a, 0, P.fixed[0]);
+      a.base[3 * g] = P.base.r;
+      a.base[3 * g + 1] = P.base.g;
+      a.base[3 * g + 2] = P.base.b;
+    }
     cnt = P.cnt;
   }
   path_stats(a, cnt);
+}
+
+// the queued indirect paths from iteration 1 on (MonteCarlo_IndirectSample's loop), one per
+// thread over a grid-stride loop: the queue length is known only on the device
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void ind_cont_kernel(RenderArgs a) {
+  const uint32_t n = *a.ind_ncont;
+  Counts tot = {0, 0, 0, 0, 0, 0};
+  const int64_t rounds = ((int64_t)n + (int64_t)gridDim.x * blockDim.x - 1) / ((int64_t)gridDim.x * blockDim.x);
+  for (int64_t r = 0; r < rounds; r++) {
+    int64_t t = (r * gridDim.x + blockIdx.x) * (int64_t)blockDim.x + threadIdx.x;
+    if (t >= (int64_t)n) continue;
+    const IndCont &q = a.ind_cont[t];
+    PathCtx P;
+    path_init(P, a, q.g, q.prim, (int)q.pslot);
+    P.fixed[0] = q.qslot;
+    Rng rng;
+    rng.key = q.rkey;
+    rng.ctr = q.rctr;
+    V org = ld3(q.org), dir = org;
+    C3 tw = rgb(1, 1, 1), W = ldc(q.w);
+    Hit h;
+    h.p = ld3(q.hp);
+    h.n = ld3(q.hn);
+    h.t = 0.0;
+    h.mat = q.mat;
+    if (ind_shade<false>(P, h, org, dir, rng, W, tw))
+      for (int iter = 1; iter < a.F.max_monte_depth; iter++)
+        if (!ind_bounce(P, org, dir, rng, W, tw)) break;
+    if (P.fixed[0] >= 0) put_none(a, 0, P.fixed[0]);
+    a.base[3 * (int64_t)q.g] = P.base.r;
+    a.base[3 * (int64_t)q.g + 1] = P.base.g;
+    a.base[3 * (int64_t)q.g + 2] = P.base.b;
+    tot.shadow += P.cnt.shadow; tot.monte += P.cnt.monte; tot.trans += P.cnt.trans;
+    tot.spec += P.cnt.spec; tot.indirect += P.cnt.indirect; tot.caustic += P.cnt.caustic;
+  }
+  path_stats(a, tot);
 }
 
 // TransmissiveIllumination / SpecularIllumination sample (raytracer.cpp:47-109)
@@ -1148,10 +1250,18 @@ void launch_path(const RenderArgs &a, hipStream_t st) {
   if (a.nprim > 0) slot0_kernel<<<nblk(a.nprim, 256), 256, 0, st>>>(a);
   if (a.total_ind > 0) {
     unsigned g = nblk(a.total_ind, 128);
-    if (a.ind_waves <= 1) ind_kernel<1><<<g, 128, 0, st>>>(a);
-    else if (a.ind_waves == 2) ind_kernel<2><<<g, 128, 0, st>>>(a);
-    else if (a.ind_waves == 3) ind_kernel<3><<<g, 128, 0, st>>>(a);
-    else ind_kernel<4><<<g, 128, 0, st>>>(a);
+    if (a.split_ind) (void)hipMemsetAsync(a.ind_ncont, 0, sizeof(uint32_t), st);
+    if (!a.split_ind) ind_kernel<2, false><<<g, 128, 0, st>>>(a);
+    else if (a.ind_waves <= 2) ind_kernel<2, true><<<g, 128, 0, st>>>(a);
+    else if (a.ind_waves == 3) ind_kernel<3, true><<<g, 128, 0, st>>>(a);
+    else if (a.ind_waves == 4) ind_kernel<4, true><<<g, 128, 0, st>>>(a);
+    else ind_kernel<5, true><<<g, 128, 0, st>>>(a);
+    // continuations: at most total_ind; a grid of ~8 blocks per CU strides over the queue
+    if (a.split_ind) {
+      unsigned gc = nblk(a.total_ind, 128);
+      if (gc > 2048u) gc = 2048u;
+      ind_cont_kernel<<<gc, 128, 0, st>>>(a);
+    }
   }
   if (a.total_mc > 0) mc_kernel<<<nblk(a.total_mc, 128), 128, 0, st>>>(a);
 }

@@ -171,3 +171,38 @@ def test_cylinder_and_line_cases_match_oracle(renderer):
     both = (gh == 1) & (oh == 1)
     np.testing.assert_allclose(gt[both], ot[both], rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(gn[both], on[both], atol=1e-9)
+
+
+@pytest.mark.parametrize("name,extra", [
+    ("cornell.scn", ["-global", "20000", "-caustic", "20000"]),
+    ("jensen.scn", ["-global", "4000", "-caustic", "20000", "-lt", "4", "-ss", "4"])])
+def test_indirect_continuation_queue_is_exact(name, extra):
+    """ind_kernel's continuation queue (GI_SPLIT_IND=1, default) only regroups the bounces of
+    MonteCarlo_IndirectSample (montecarlo.cpp:177-305) that follow a glass/mirror hit: the f32
+    image and every -v counter equal the one-loop-per-lane kernel's (GI_SPLIT_IND=0)."""
+    args = [scene(name), "/tmp/x.png", "-resolution", "32", "32", "-aa", "1", "-it", "32",
+            "-tt", "8", "-st", "8", "-seed", "4"] + extra
+    p, sc, _o, w, h, aa, real = gi_amd.ParseArgs(args)
+    out = []
+    old = os.environ.get("GI_SPLIT_IND")
+    try:
+        for v in ("0", "1"):
+            os.environ["GI_SPLIT_IND"] = v
+            r = gi_amd.Renderer(0, p)
+            try:
+                r.ReadScene(sc, real)
+                r.MapPhotons()
+                _rgb, f, st = r.RenderImage(aa, w, h, want_float=True)
+                out.append((f, st))
+            finally:
+                r.close()
+    finally:
+        if old is None:
+            os.environ.pop("GI_SPLIT_IND", None)
+        else:
+            os.environ["GI_SPLIT_IND"] = old
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    for k in ("screen_rays", "shadow_rays", "monte_carlo_rays", "transmissive_samples",
+              "specular_samples", "indirect_samples", "caustic_samples", "knn_queries"):
+        assert out[0][1][k] == out[1][1][k], k
+    assert out[1][1]["transmissive_samples"] > 0

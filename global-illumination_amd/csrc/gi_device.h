@@ -114,7 +114,8 @@ struct SceneView {
   const DTri *tris;
   const DMaterial *mats;
   const DLight *lights;
-  int32_t nnodes, nelems, nlights, pad;
+  int32_t nnodes, nelems, nlights;
+  uint32_t kinds;  // bit k set: the scene holds shapes of ShapeKind k
   double radius;
   double centroid[3];
   double ambient[3];
@@ -317,10 +318,30 @@ GI_HD bool ray_cylinder(V o, V R, V p1, V p2, double radius, double &t_out, V &p
   return true;
 }
 
+// shape kinds a kernel instance is compiled for (KINDS template argument): the host launches
+// the smallest instance covering SceneView::kinds, so scenes of triangles and spheres do not
+// carry the mesh/box/cylinder code (registers and instruction cache) through their hot loops
+constexpr uint32_t KIND_BIT(int k) { return 1u << k; }
+constexpr uint32_t KINDS_ALL = ~0u;
+constexpr uint32_t KINDS_TRI_SPHERE = (1u << SK_TRI) | (1u << SK_SPHERE);
+constexpr uint32_t KINDS_POLY = (1u << SK_TRI) | (1u << SK_SPHERE) | (1u << SK_MESH) | (1u << SK_BOX);
+
 // R3Shape::Intersects dispatch (R3Shape.cpp:328-329); SK_MESH is R3Intersects(ray,
 // R3TriangleArray) (R3Isect.cpp:800-833): min t over ALL triangles, t >= -1e-6 allowed (Q2).
+template <uint32_t KINDS = KINDS_ALL>
 __device__ __forceinline__ bool shape_intersect(const SceneView &S, const DShape &sh, V o, V d,
                                              double &t, V &p, V &n) {
+  if (KINDS == KINDS_TRI_SPHERE) {
+    if (sh.kind == SK_TRI) {
+      const DTri &tr = S.tris[sh.tri_first];
+      if (!ray_tri(o, d, tr, t, p)) return false;
+      n = ld3(tr.n);
+      return true;
+    }
+    if (sh.kind == SK_SPHERE) return ray_sphere(o, d, ld3(sh.c), sh.r, t, p, n);
+    return false;
+  }
+  if (!(KINDS & KIND_BIT(sh.kind))) return false;
   switch (sh.kind) {
     case SK_TRI: {
       const DTri &tr = S.tris[sh.tri_first];
@@ -392,6 +413,7 @@ struct Hit {
 // Ray direction is renormalised per graph level (R3Line::InverseTransform, R3Line.cpp:140).
 // Inlined at every call site: node/element/shape records are wave-uniform (scalar loads) and
 // the root-first transform chain is precomputed per node, so nothing lives in scratch.
+template <uint32_t KINDS = KINDS_ALL>
 __device__ __forceinline__ bool scene_intersect(const SceneView &S, V org, V dir, Hit &h) {
   double closest = kInf;  // world-frame t (rigid transforms keep t; scale handled below)
   bool found = false;
@@ -432,7 +454,7 @@ __device__ __forceinline__ bool scene_intersect(const SceneView &S, V org, V dir
       for (int si = 0; si < el.shape_count; si++) {
         double t;
         V p, n;
-        if (shape_intersect(S, S.shapes[el.shape_first + si], lo, ldir, t, p, n)) {
+        if (shape_intersect<KINDS>(S, S.shapes[el.shape_first + si], lo, ldir, t, p, n)) {
           if ((t >= 0.0) && (t <= ec)) {
             ep = p;
             en = n;

@@ -208,6 +208,7 @@ struct gi_ctx {
   int leaf_size[2] = {64, 512};  // photons per kd leaf, per map (global, caustic)
   int wave_cap_mul = 1;
   int chunk_cap = 256;            // chunk kernel: LDS candidate capacity per 64-query chunk
+  int chunk_minsub = 64;          // chunk kernel: overflowing chunks retried down to this group size (64: no retry, measured best)
   hipEvent_t ev2 = nullptr;       // chunk kernel / fallback split
   double fb_ms[2] = {0, 0};       // fallback time and queries per map (since the last reset)
   uint64_t fb_q[2] = {0, 0};
@@ -224,7 +225,7 @@ struct gi_ctx {
   DBuf spawn, npaths, path_off, nmc, mc_off, nind, ind_off, base, pixels, rgbf, rgb8, gheap_d2, gheap_idx, qcount, stats_bak;
   DBuf qpos[2], qshade[2], qkey[2], qout[2];
   DBuf list_idx, list_d2, list_n;
-  DBuf fb_list, fb_count;          // chunk k-NN fallback queries
+  DBuf fb_list, fb_count, fb_dense;  // chunk k-NN fallback queries (striped, compacted)
   uint64_t fb_total = 0;
   DBuf qseg[2];  // K-best lists of the query-per-wave k-NN path
   size_t qcap_hint[2] = {0, 0};
@@ -289,6 +290,8 @@ SceneView make_view(gi_ctx *c) {
   S.nnodes = (int)H.nodes.size();
   S.nelems = (int)H.elems.size();
   S.nlights = (int)H.lights.size();
+  S.kinds = 0;
+  for (const DShape &sh : H.shapes) S.kinds |= 1u << sh.kind;
   S.radius = H.radius;
   for (int i = 0; i < 3; i++) {
     S.centroid[i] = H.centroid[i];
@@ -470,6 +473,19 @@ int trace_map(gi_ctx *c, int caustic, int64_t goal, const std::vector<double> &p
   return GI_OK;
 }
 
+// device counters: ST_STRIPES copies of ST_COUNT words (gi_kernels.h wave_add), summed here
+constexpr size_t ST_BYTES = (size_t)ST_STRIPES * ST_COUNT * 8;
+hipError_t read_stats(gi_ctx *c, unsigned long long *out) {
+  std::vector<unsigned long long> all((size_t)ST_STRIPES * ST_COUNT);
+  hipError_t e = hipMemcpyAsync(all.data(), c->d_stats.p, ST_BYTES, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  for (int i = 0; i < ST_COUNT; i++) {
+    out[i] = 0;
+    for (int s = 0; s < ST_STRIPES; s++) out[i] += all[(size_t)s * ST_COUNT + i];
+  }
+  return e;
+}
+
 KnnArgs knn_args(gi_ctx *c, int mi) {
   KnnArgs k;
   memset(&k, 0, sizeof k);
@@ -488,6 +504,7 @@ KnnArgs knn_args(gi_ctx *c, int mi) {
   k.stats = c->d_stats.as<unsigned long long>();
   k.stat_off = mi == GI_MAP_GLOBAL ? 0 : ST_KNN_MAP;
   k.sel_slack = c->sel_slack;
+  k.chunk_minsub = c->chunk_minsub;
   k.qpl = c->knn_qpl;
   if (const char *s = getenv("GI_KNN_DBG")) k.dbg = atoi(s);
   return k;
@@ -507,24 +524,34 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
   if (kind == 2 && (int64_t)k.K * 64 * 8 > 80 * 1024) kind = 1;
   if ((kind >= 5 && kind <= 7) && k.K <= 64 && k.mode != KNN_MODE_LIST) {
     // chunk kernel, then the per-lane kernel on the chunks that overflowed its LDS gather
-    HIPCHK(c, c->fb_list.ensure((size_t)nq * 4));
-    HIPCHK(c, c->fb_count.ensure(4));
-    HIPCHK(c, hipMemsetAsync(c->fb_count.p, 0, 4, c->stream));
+    // striped fallback list (gi_knn_chunk.hip to_fallback): block b -> stripe b % FB_QS, at most
+    // 64 queries per chunk, ceil(chunks / grid) chunks per block
+    int64_t chunks = (nq + 63) / 64;
+    int64_t grid = knn_chunk_grid(nq);
+    uint32_t cap_s = (uint32_t)(64 * ((chunks + grid - 1) / grid) * ((grid + FB_QS - 1) / FB_QS));
+    HIPCHK(c, c->fb_list.ensure((size_t)FB_QS * cap_s * 4));
+    HIPCHK(c, c->fb_dense.ensure((size_t)nq * 4 + 4));
+    HIPCHK(c, c->fb_count.ensure(FB_QS * 32 * 4));
+    HIPCHK(c, hipMemsetAsync(c->fb_count.p, 0, FB_QS * 32 * 4, c->stream));
     k.nq = nq;
     k.q0 = 0;
     k.fb_list = c->fb_list.as<uint32_t>();
     k.fb_count = c->fb_count.as<uint32_t>();
+    k.fb_cap_s = cap_s;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     launch_knn_chunk(k, c->chunk_cap, kind - 5, c->stream);
     HIPCHK(c, hipGetLastError());
+    uint32_t *dense = c->fb_dense.as<uint32_t>();
+    launch_fb_compact(k.fb_list, k.fb_count, cap_s, dense, dense + nq, c->stream);
+    HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->ev2, c->stream));
     uint32_t nfb = 0;
-    HIPCHK(c, hipMemcpyAsync(&nfb, c->fb_count.p, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&nfb, dense + nq, 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->fb_total += nfb;
     if (nfb) {
       KnnArgs f = k;
-      f.perm = c->fb_list.as<uint32_t>();
+      f.perm = dense;
       f.nq = nfb;
       f.q0 = 0;
       launch_knn_lane(f, c->lane_chunk, c->heap_arity, c->stream);
@@ -656,7 +683,7 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
   double knn_ms[2] = {0, 0}, launches[2] = {0, 0};
   HIPCHK(c, upload(c->pixels, pix_xy.data(), pix_xy.size() * 4, c->stream));
   HIPCHK(c, c->qcount.ensure(16));
-  HIPCHK(c, c->stats_bak.ensure(ST_COUNT * 8));
+  HIPCHK(c, c->stats_bak.ensure(ST_BYTES));
   for (int64_t p0 = 0; p0 < npix_total; p0 += pix_batch) {
     int64_t npix = std::min(pix_batch, npix_total - p0);
     int64_t nprim = npix * per_pix;
@@ -711,14 +738,17 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     HIPCHK(c, c->base.ensure((size_t)total_paths * 24));
     a.base = c->base.as<double>();
     if (a.split_ind && a.total_ind > 0) {
-      HIPCHK(c, c->ind_cont.ensure((size_t)a.total_ind * sizeof(IndCont)));
-      HIPCHK(c, c->ind_ncont.ensure(4));
+      // stripe s takes the appends of waves w with w % IND_QS == s (<= 64 paths per wave)
+      uint64_t nwaves = ((uint64_t)a.total_ind + 63) / 64;
+      a.ind_cap_s = (uint32_t)(64 * ((nwaves + IND_QS - 1) / IND_QS));
+      HIPCHK(c, c->ind_cont.ensure((size_t)IND_QS * a.ind_cap_s * sizeof(IndCont)));
+      HIPCHK(c, c->ind_ncont.ensure(IND_QS * 32 * 4));
       a.ind_cont = c->ind_cont.as<IndCont>();
       a.ind_ncont = c->ind_ncont.as<uint32_t>();
     }
     // single Monte Carlo pass; grow the query lists and re-run on overflow
     uint32_t nq[2] = {0, 0};
-    HIPCHK(c, hipMemcpyAsync(c->stats_bak.p, c->d_stats.p, ST_COUNT * 8,
+    HIPCHK(c, hipMemcpyAsync(c->stats_bak.p, c->d_stats.p, ST_BYTES,
                              hipMemcpyDeviceToDevice, c->stream));
     // deterministic slots: [0, nprim) per primary sample, then (global list) one per
     // indirect path; Monte Carlo paths append after qbase[l]
@@ -746,7 +776,7 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
         c->qcap_hint[l] = std::max<size_t>(c->qcap_hint[l], (size_t)(nq[l] * 1.25) + 1024);
       if (ok) break;
       if (attempt == 2) return fail(c, GI_ERR_ALLOC, "query list overflow");
-      HIPCHK(c, hipMemcpyAsync(c->d_stats.p, c->stats_bak.p, ST_COUNT * 8,
+      HIPCHK(c, hipMemcpyAsync(c->d_stats.p, c->stats_bak.p, ST_BYTES,
                                hipMemcpyDeviceToDevice, c->stream));
     }
     // photon-map estimates, then a deterministic (key) order of each list for the reduction
@@ -829,7 +859,7 @@ int gi_create(gi_ctx **out, int dev) {
   std::vector<double> lut;
   build_lut(lut);
   if (upload(c->d_lut, lut.data(), lut.size() * 8, c->stream) != hipSuccess ||
-      c->d_stats.ensure(ST_COUNT * 8) != hipSuccess) {
+      c->d_stats.ensure(ST_BYTES) != hipSuccess) {
     delete c;
     return GI_ERR_HIP;
   }
@@ -841,6 +871,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_WAVE_CAP_MUL")) c->wave_cap_mul = std::max(1, atoi(s));
   if (const char *s = getenv("GI_SEL_SLACK")) c->sel_slack = std::max(1, atoi(s));
   if (const char *s = getenv("GI_CHUNK_CAP")) c->chunk_cap = std::max(64, atoi(s));
+  if (const char *s = getenv("GI_CHUNK_MINSUB")) c->chunk_minsub = std::min(64, std::max(1, atoi(s)));
   if (const char *s = getenv("GI_KNN_GHEAP")) c->force_gheap = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_QPL")) c->knn_qpl = std::max(1, atoi(s));
   if (const char *s = getenv("GI_LANE_CHUNK")) c->lane_chunk = std::max(1, atoi(s));
@@ -860,7 +891,7 @@ void gi_destroy(gi_ctx *c) {
   DBuf *bufs[] = {&c->d_nodes, &c->d_elems, &c->d_shapes, &c->d_tris, &c->d_mats, &c->d_lights,
                   &c->d_lut, &c->d_stats, &c->spawn, &c->npaths, &c->path_off, &c->base,
                   &c->pixels, &c->rgbf, &c->rgb8, &c->gheap_d2, &c->gheap_idx, &c->qcount,
-                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont};
+                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont, &c->fb_list, &c->fb_count, &c->fb_dense};
   for (DBuf *b : bufs) b->release();
   for (int l = 0; l < 2; l++) {
     c->qpos[l].release(); c->qshade[l].release(); c->qkey[l].release(); c->qout[l].release();
@@ -1060,7 +1091,7 @@ static int render_common(gi_ctx *c, int aa, int w, int h, const std::vector<int3
     HIPCHK(c, hipMemsetAsync(c->rgbf.p, 0, npx * 4, c->stream));
   }
   HIPCHK(c, hipMemsetAsync(c->rgb8.p, 0, npx, c->stream));
-  HIPCHK(c, hipMemsetAsync(c->d_stats.p, 0, ST_COUNT * 8, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_stats.p, 0, ST_BYTES, c->stream));
   c->fb_ms[0] = c->fb_ms[1] = 0;
   c->fb_q[0] = c->fb_q[1] = 0;
   gi_render_stats local;
@@ -1070,8 +1101,7 @@ static int render_common(gi_ctx *c, int aa, int w, int h, const std::vector<int3
   if (rgbf) HIPCHK(c, hipMemcpyAsync(rgbf, c->rgbf.p, npx * 4, hipMemcpyDeviceToHost, c->stream));
   if (rgb8) HIPCHK(c, hipMemcpyAsync(rgb8, c->rgb8.p, npx, hipMemcpyDeviceToHost, c->stream));
   unsigned long long s[ST_COUNT];
-  HIPCHK(c, hipMemcpyAsync(s, c->d_stats.p, sizeof s, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, read_stats(c, s));
   if (const char *kd = getenv("GI_KNN_DBG"); kd && (atoi(kd) & 16)) {
     fprintf(stderr, "[gi] k-NN phase cycles (sum over waves):");
     for (int i = 0; i < 16; i++) fprintf(stderr, " %llu", s[ST_PHASE + i]);
@@ -1286,15 +1316,14 @@ int gi_knn_bench(gi_ctx *c, int map, int64_t n, const double *pts, const double 
   k.perm = perm;
   int saved = c->knn_kernel_kind;
   if (kernel >= 0) c->knn_kernel_kind = kernel;
-  HIPCHK(c, hipMemsetAsync(c->d_stats.p, 0, ST_COUNT * 8, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_stats.p, 0, ST_BYTES, c->stream));
   double ms = 0;
   int rc = GI_OK;
   for (int it = 0; it < iters && rc == GI_OK; it++) rc = run_knn(c, k, n, &ms);
   c->knn_kernel_kind = saved;
   if (rc) return rc;
   unsigned long long st[ST_COUNT];
-  HIPCHK(c, hipMemcpyAsync(st, c->d_stats.p, sizeof st, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, read_stats(c, st));
   if (ms_out) *ms_out = ms / iters;
   int so = map * ST_KNN_MAP;
   double nqd = (double)std::max<unsigned long long>(1, st[ST_KNN + so]);

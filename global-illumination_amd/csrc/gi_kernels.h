@@ -40,6 +40,12 @@ struct IndCont {
   int32_t mat, pad;
 };
 
+// continuation queue stripes: wave w appends to stripe w % IND_QS (one atomic per wave on a
+// counter shared by 1/IND_QS of the waves)
+constexpr int IND_QS = 64;
+// chunk k-NN fallback list stripes: block b appends to stripe b % FB_QS
+constexpr int FB_QS = 64;
+
 struct QShade {
   double n[3];   // surface normal
   double ex[3];  // exact reflection direction (Phong lobe term)
@@ -78,8 +84,9 @@ struct RenderArgs {
   int32_t ind_waves;    // occupancy target of the indirect-path kernel (waves per SIMD)
   int32_t dbg;          // diagnostics: 1 = skip the indirect trace, 2 = skip diffuse sampling too
   int32_t split_ind;    // 1: indirect paths trace their first bounce, continuations are queued
-  IndCont *ind_cont;    // [total_ind] continuation queue
-  uint32_t *ind_ncont;  // its length (device counter)
+  IndCont *ind_cont;    // continuation queue: IND_QS stripes of ind_cap_s entries
+  uint32_t *ind_ncont;  // fill of stripe s at [s * 32] (one 128-B line per counter)
+  uint32_t ind_cap_s;
   int64_t qind_base;    // global list: indirect path t owns slot qind_base + t
   // query lists (0 = global map, 1 = caustic map). Deterministic slots first: list l slot p
   // = primary sample p's own query (slot-0 path), then (global list only) slot
@@ -184,11 +191,24 @@ __device__ __forceinline__ void heapn_accept(uint64_t *h, int &size, int K, uint
   }
 }
 
-// wave-level counter reduction (one atomic per wave)
+// The -v counters live in ST_STRIPES copies of ST_COUNT words (the host sums them). One
+// counter word takes ~10^8 atomics/s (MI355X_MICROARCH.md): a launch of ~500k waves adding to
+// one word would serialise for ~5 ms, so each wave adds to the copy its global wave id selects.
+constexpr int ST_STRIPES = 64;
+__device__ __forceinline__ unsigned long long *stat_stripe(unsigned long long *stats) {
+  uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  return stats + (size_t)(w & (ST_STRIPES - 1)) * ST_COUNT;
+}
+
+// wave-level counter reduction (one atomic per wave, on the wave's stripe; dst points into
+// stripe 0)
 __device__ __forceinline__ void wave_add(unsigned long long *dst, uint64_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, (unsigned long long)v);
+  if ((threadIdx.x & 63) == 0 && v) {
+    uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    atomicAdd(dst + (size_t)(w & (ST_STRIPES - 1)) * ST_COUNT, (unsigned long long)v);
+  }
 }
 
 // query-list slot with no query (deterministic slots a path did not use): qpos.w bits
@@ -210,6 +230,7 @@ struct KnnArgs {
   int32_t mode;
   int32_t stat_off;        // 0 (global map) or ST_KNN_MAP (caustic map)
   int32_t sel_slack;       // query-per-wave kernel: re-select once K + slack candidates held
+  int32_t chunk_minsub;    // chunk kernel: smallest query group an overflowing chunk is split to
   int32_t qpl;             // per-lane kernel: consecutive (sorted) queries per lane
   int32_t dbg;             // diagnostics: chunk kernel phase skips (timing only)
   int32_t pad4;
@@ -224,8 +245,9 @@ struct KnnArgs {
   int32_t *list_idx;       // query-per-wave kernel: K-best lists [nq][K] (kd-order index)
   float *list_d2;          //   and their d2; -1 past list_n[q]
   int32_t *list_n;
-  uint32_t *fb_list;       // chunk kernel: queries (original slots) handed to the fallback
-  uint32_t *fb_count;
+  uint32_t *fb_list;       // chunk kernel: queries (original slots) handed to the fallback,
+  uint32_t *fb_count;      // FB_QS stripes of fb_cap_s entries; fill of stripe s at [s * 32]
+  uint32_t fb_cap_s;
   float *gheap_d2;         // global heap scratch (K > 64)
   int32_t *gheap_idx;
   unsigned long long *stats;
@@ -252,7 +274,10 @@ struct ScanTemp {
 hipError_t launch_scan(const uint32_t *in, uint32_t *out, int64_t n, ScanTemp &tmp,
                        hipStream_t st);
 void launch_primary(const RenderArgs &a, hipStream_t st);
-void launch_path(const RenderArgs &a, hipStream_t st);  // slot0 + indirect + Monte Carlo
+void launch_path(const RenderArgs &a, hipStream_t st);
+// dense copy of the striped chunk fallback list; total length to *total
+void launch_fb_compact(const uint32_t *list, const uint32_t *count, uint32_t cap_s, uint32_t *dense,
+                       uint32_t *total, hipStream_t st);  // slot0 + indirect + Monte Carlo
 void launch_reduce(const RenderArgs &a, hipStream_t st);
 void launch_segments(const uint64_t *skeys, uint32_t n, uint32_t nprim, uint32_t *seg,
                      hipStream_t st);
@@ -262,6 +287,7 @@ bool launch_knn_packet(const KnnArgs &a, hipStream_t st);
 bool launch_knn_lane(const KnnArgs &a, int chunk, int arity, hipStream_t st);
 bool launch_knn_group(const KnnArgs &a, int lanes, hipStream_t st);
 bool launch_knn_chunk(const KnnArgs &a, int cap, int variant, hipStream_t st);  // 0 wave, 1 heaps, 2 lane select
+unsigned knn_chunk_grid(int64_t nq);  // blocks of the chunk kernels (one 64-query chunk each, grid-stride)
 void launch_list_estimate(const KnnArgs &a, hipStream_t st);
 void launch_cached(const KnnArgs &a, hipStream_t st);
 void launch_photons(const PhotonArgs &a, bool emit, hipStream_t st);

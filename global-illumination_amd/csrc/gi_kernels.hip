@@ -451,7 +451,7 @@ __global__ __launch_bounds__(256) void slot0_kernel(RenderArgs a) {
 // make all 64 lanes execute the Fresnel pow, refraction trig and Phong-lobe sampling (and hold
 // them idle through the glass bounces). Such paths are queued at the hit (wave-aggregated
 // append) and finish compacted in ind_cont_kernel; the arithmetic and RNG stream are unchanged.
-template <int W, bool SPLIT>
+template <int W, bool SPLIT, uint32_t KINDS>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void ind_kernel(RenderArgs a) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   Counts cnt = {0, 0, 0, 0, 0, 0};
@@ -482,7 +482,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void i
       V org = p + sb * kEps, dir = sb;
       C3 tw = rgb(1, 1, 1);
       Hit h;
-      if (!scene_intersect(a.S, org, dir, h)) {
+      if (!scene_intersect<KINDS>(a.S, org, dir, h)) {
         P.base += Wt * (tw * ldc(a.S.background));
       } else {
         P.cnt.monte++;
@@ -494,10 +494,12 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void i
           uint64_t act = __ballot(1);
           int lane = (int)(threadIdx.x & 63);
           int leader = __ffsll((long long)act) - 1;
+          const uint32_t stripe = (uint32_t)(t >> 6) & (IND_QS - 1);
           uint32_t base = 0;
-          if (lane == leader) base = atomicAdd(a.ind_ncont, (uint32_t)__popcll(act));
+          if (lane == leader) base = atomicAdd(&a.ind_ncont[stripe * 32], (uint32_t)__popcll(act));
           base = (uint32_t)__shfl((int)base, leader, 64);
-          IndCont &q = a.ind_cont[base + (uint32_t)__popcll(act & ((1ull << lane) - 1ull))];
+          IndCont &q = a.ind_cont[(size_t)stripe * a.ind_cap_s + base +
+                                  (uint32_t)__popcll(act & ((1ull << lane) - 1ull))];
           q.org[0] = org.x; q.org[1] = org.y; q.org[2] = org.z;
           q.hp[0] = h.p.x; q.hp[1] = h.p.y; q.hp[2] = h.p.z;
           q.hn[0] = h.n.x; q.hn[1] = h.n.y; q.hn[2] = h.n.z;
@@ -524,16 +526,19 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void i
   path_stats(a, cnt);
 }
 
-// the queued indirect paths from iteration 1 on (MonteCarlo_IndirectSample's loop), one per
-// thread over a grid-stride loop: the queue length is known only on the device
+// the queued indirect paths (shading of the first hit, then MonteCarlo_IndirectSample's loop
+// from iteration 1 on), one per thread: block b serves stripe b % IND_QS, striding over its fill
+// (the fills are known only on the device)
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void ind_cont_kernel(RenderArgs a) {
-  const uint32_t n = *a.ind_ncont;
+  const uint32_t stripe = blockIdx.x % IND_QS, part = blockIdx.x / IND_QS;
+  const uint32_t parts = gridDim.x / IND_QS;
+  const uint32_t n = a.ind_ncont[stripe * 32];
   Counts tot = {0, 0, 0, 0, 0, 0};
-  const int64_t rounds = ((int64_t)n + (int64_t)gridDim.x * blockDim.x - 1) / ((int64_t)gridDim.x * blockDim.x);
-  for (int64_t r = 0; r < rounds; r++) {
-    int64_t t = (r * gridDim.x + blockIdx.x) * (int64_t)blockDim.x + threadIdx.x;
-    if (t >= (int64_t)n) continue;
-    const IndCont &q = a.ind_cont[t];
+  const uint32_t rounds = (n + parts * blockDim.x - 1) / (parts * blockDim.x);
+  for (uint32_t r = 0; r < rounds; r++) {
+    uint32_t idx = (r * parts + part) * blockDim.x + threadIdx.x;
+    if (idx >= n) continue;
+    const IndCont &q = a.ind_cont[(size_t)stripe * a.ind_cap_s + idx];
     PathCtx P;
     path_init(P, a, q.g, q.prim, (int)q.pslot);
     P.fixed[0] = q.qslot;
@@ -1246,22 +1251,24 @@ hipError_t launch_scan(const uint32_t *in, uint32_t *out, int64_t n, ScanTemp &t
 void launch_primary(const RenderArgs &a, hipStream_t st) {
   primary_kernel<<<nblk(a.nprim, 256), 256, 0, st>>>(a);
 }
+template <uint32_t KINDS>
+void launch_ind(const RenderArgs &a, unsigned g, hipStream_t st) {
+  if (a.ind_waves <= 2) ind_kernel<2, true, KINDS><<<g, 128, 0, st>>>(a);
+  else if (a.ind_waves == 3) ind_kernel<3, true, KINDS><<<g, 128, 0, st>>>(a);
+  else if (a.ind_waves == 4) ind_kernel<4, true, KINDS><<<g, 128, 0, st>>>(a);
+  else ind_kernel<5, true, KINDS><<<g, 128, 0, st>>>(a);
+}
 void launch_path(const RenderArgs &a, hipStream_t st) {
   if (a.nprim > 0) slot0_kernel<<<nblk(a.nprim, 256), 256, 0, st>>>(a);
   if (a.total_ind > 0) {
     unsigned g = nblk(a.total_ind, 128);
-    if (a.split_ind) (void)hipMemsetAsync(a.ind_ncont, 0, sizeof(uint32_t), st);
-    if (!a.split_ind) ind_kernel<2, false><<<g, 128, 0, st>>>(a);
-    else if (a.ind_waves <= 2) ind_kernel<2, true><<<g, 128, 0, st>>>(a);
-    else if (a.ind_waves == 3) ind_kernel<3, true><<<g, 128, 0, st>>>(a);
-    else if (a.ind_waves == 4) ind_kernel<4, true><<<g, 128, 0, st>>>(a);
-    else ind_kernel<5, true><<<g, 128, 0, st>>>(a);
-    // continuations: at most total_ind; a grid of ~8 blocks per CU strides over the queue
-    if (a.split_ind) {
-      unsigned gc = nblk(a.total_ind, 128);
-      if (gc > 2048u) gc = 2048u;
-      ind_cont_kernel<<<gc, 128, 0, st>>>(a);
-    }
+    if (a.split_ind) (void)hipMemsetAsync(a.ind_ncont, 0, IND_QS * 32 * sizeof(uint32_t), st);
+    if (!a.split_ind) ind_kernel<2, false, KINDS_ALL><<<g, 128, 0, st>>>(a);
+    else if ((a.S.kinds & ~KINDS_TRI_SPHERE) == 0) launch_ind<KINDS_TRI_SPHERE>(a, g, st);
+    else if ((a.S.kinds & ~KINDS_POLY) == 0) launch_ind<KINDS_POLY>(a, g, st);
+    else launch_ind<KINDS_ALL>(a, g, st);
+    // continuations: 32 blocks per stripe stride over its fill
+    if (a.split_ind) ind_cont_kernel<<<IND_QS * 32, 128, 0, st>>>(a);
   }
   if (a.total_mc > 0) mc_kernel<<<nblk(a.total_mc, 128), 128, 0, st>>>(a);
 }

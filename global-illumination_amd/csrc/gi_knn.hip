@@ -220,9 +220,10 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
     __syncthreads();
   }
   if (a.stats && lane == 0) {
-    if (st_q) atomicAdd(&a.stats[ST_KNN + a.stat_off], (unsigned long long)st_q);
-    if (st_found) atomicAdd(&a.stats[ST_KNN_PHOTONS + a.stat_off], (unsigned long long)st_found);
-    if (st_vis) atomicAdd(&a.stats[ST_KNN_VISITED + a.stat_off], (unsigned long long)st_vis);
+    unsigned long long *sd = stat_stripe(a.stats);
+    if (st_q) atomicAdd(&sd[ST_KNN + a.stat_off], (unsigned long long)st_q);
+    if (st_found) atomicAdd(&sd[ST_KNN_PHOTONS + a.stat_off], (unsigned long long)st_found);
+    if (st_vis) atomicAdd(&sd[ST_KNN_VISITED + a.stat_off], (unsigned long long)st_vis);
   }
 }
 

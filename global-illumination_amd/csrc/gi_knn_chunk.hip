@@ -384,11 +384,15 @@ __device__ __forceinline__ float query_lim2(const KnnArgs &a, const ChunkGeom &G
 // hand the wave's valid queries to the per-lane fallback kernel
 __device__ __forceinline__ void to_fallback(const KnnArgs &a, uint64_t vmask, bool valid, int64_t qi,
                                             int lane) {
+  // one atomic per wave, on the block's stripe (a single counter would serialise the waves)
   uint32_t nv = (uint32_t)__popcll(vmask);
+  const uint32_t s = blockIdx.x & (FB_QS - 1);
   uint32_t base = 0;
-  if (lane == 0) base = atomicAdd(a.fb_count, nv);
+  if (lane == 0) base = atomicAdd(&a.fb_count[s * 32], nv);
   base = (uint32_t)__shfl((int)base, 0, 64);
-  if (valid) a.fb_list[base + (uint32_t)__popcll(vmask & ((1ull << lane) - 1ull))] = (uint32_t)qi;
+  if (valid)
+    a.fb_list[(size_t)s * a.fb_cap_s + base + (uint32_t)__popcll(vmask & ((1ull << lane) - 1ull))] =
+        (uint32_t)qi;
 }
 
 // ---- 4. the estimate of one query from LDS-staged photons (slot_at(s) = s-th kept slot).
@@ -564,6 +568,7 @@ void knn_chunk_lane_kernel(KnnArgs a) {
   P.on = (a.dbg & 16) != 0;
   P.t = 0;
   for (int i = 0; i < 10; i++) P.c[i] = 0;
+  const int minsub = a.chunk_minsub > 0 ? a.chunk_minsub : 64;
   for (int64_t chunk = blockIdx.x; chunk * 64 < a.nq; chunk += gridDim.x) {
     bool valid;
     int64_t qi;
@@ -571,22 +576,28 @@ void knn_chunk_lane_kernel(KnnArgs a) {
     chunk_load_query(a, chunk, lane, valid, qi, qp);
     uint64_t vmask = __ballot(valid);
     if (vmask == 0) continue;
+    // A chunk whose gather overflows is retried as halves, quarters, ... down to minsub
+    // Morton-adjacent queries (smaller boxes gather fewer photons); what still overflows goes
+    // to the per-lane kernel. Lanes outside the current group idle through its select.
+    uint64_t pending = vmask;
+    for (int sub = 64; sub >= minsub && pending; sub >>= 1) {
+    for (int g0 = 0; g0 < 64; g0 += sub) {
+    const uint64_t gm = (sub == 64) ? ~0ull : (((1ull << sub) - 1ull) << g0);
+    if (!(pending & gm)) continue;
+    const bool act = valid && ((gm >> lane) & 1ull);
     if (P.on) P.t = clock64();
     ChunkGeom G;
     // byte counters below: at most 255 candidates per chunk
-    chunk_bound_gather<CAPC>(a, lane, valid, qp, CAPC - 1, cpos, cidx, crgbe, hist, G, P);
-    if (G.overflow) {
-      to_fallback(a, vmask, valid, qi, lane);
-      __syncthreads();
-      continue;
-    }
+    chunk_bound_gather<CAPC>(a, lane, act, qp, CAPC - 1, cpos, cidx, crgbe, hist, G, P);
     __syncthreads();
+    if (G.overflow) continue;
+    pending &= ~gm;
     const uint32_t count = G.count;
     const float qx = qp.x, qy = qp.y, qz = qp.z;
     // ---- 3. lane select. State: every valid candidate with d2 < A is kept; `need` more come
     //         from the bracket [A, B] (smallest (d2, kd index) first); above B nothing is kept.
     float A = 0.0f, B = query_lim2(a, G, qx, qy, qz);
-    int need = (valid && K > 0) ? K : 0;
+    int need = (act && K > 0) ? K : 0;
     int mode = need > 0 ? 1 : 0;  // 1 counting, 2 bracket resolved by the collect pass, 0 done
     if (!(a.dbg & 4)) {
       for (int pass = 0; pass < LS_PASSES && __ballot(mode == 1); pass++) {
@@ -640,10 +651,10 @@ void knn_chunk_lane_kernel(KnnArgs a) {
     const bool fb = mode == 1 || mode == 3;
     uint64_t fbm = __ballot(fb);
     if (fbm) {
-      if (fb) a.fb_list[atomicAdd(a.fb_count, 1u)] = (uint32_t)qi;
+      to_fallback(a, fbm, fb, qi, lane);
       if (P.on) P.c[9] += (uint64_t)__popcll(fbm);
     }
-    const bool col = valid && !fb && !(a.dbg & 4);
+    const bool col = act && !fb && !(a.dbg & 4);
     // collect: everything below A, and the bracket's photons into a small register buffer
     int n = 0;
     float km = 0.0f;
@@ -702,6 +713,11 @@ void knn_chunk_lane_kernel(KnnArgs a) {
     }
     __syncthreads();
     P.lap(3);
+    }
+    }
+    if (pending) {
+      to_fallback(a, pending, valid && ((pending >> lane) & 1ull), qi, lane);
+    }
   }
   chunk_flush_stats(a, P, st_q, st_found, st_vis);
 }
@@ -932,12 +948,36 @@ __global__ __launch_bounds__(64) void knn_chunk_heap_kernel(KnnArgs a) {
   chunk_flush_stats(a, P, st_q, st_found, st_vis);
 }
 
+// dense copy of the striped fallback list: block b copies stripe b % FB_QS after the fills of
+// the stripes before it
+__global__ __launch_bounds__(256) void fb_compact_kernel(const uint32_t *list, const uint32_t *count,
+                                                         uint32_t cap_s, uint32_t *dense,
+                                                         uint32_t *total) {
+  const uint32_t s = blockIdx.x % FB_QS, part = blockIdx.x / FB_QS, parts = gridDim.x / FB_QS;
+  uint32_t off = 0;
+  for (uint32_t i = 0; i < s; i++) off += count[i * 32];
+  const uint32_t n = count[s * 32];
+  for (uint32_t idx = part * blockDim.x + threadIdx.x; idx < n; idx += parts * blockDim.x)
+    dense[off + idx] = list[(size_t)s * cap_s + idx];
+  if (s == FB_QS - 1 && part == 0 && threadIdx.x == 0) *total = off + n;
+}
+
+void launch_fb_compact(const uint32_t *list, const uint32_t *count, uint32_t cap_s, uint32_t *dense,
+                       uint32_t *total, hipStream_t st) {
+  fb_compact_kernel<<<FB_QS * 8, 256, 0, st>>>(list, count, cap_s, dense, total);
+}
+
+// chunk kernels' grid: one 64-query chunk per block, at most 2^17 blocks (grid-stride beyond)
+unsigned knn_chunk_grid(int64_t nq) {
+  int64_t chunks = (nq + 63) / 64;
+  return (unsigned)(chunks < (1 << 17) ? chunks : (1 << 17));
+}
+
 // variant: 0 wave select, 1 per-lane heaps, 2 lane select
 bool launch_knn_chunk(const KnnArgs &a, int cap, int variant, hipStream_t st) {
   if (a.nq == 0) return true;
   if (a.mode == KNN_MODE_LIST || a.K > 64) return false;
-  int64_t chunks = (a.nq + 63) / 64;
-  unsigned grid = (unsigned)(chunks < (1 << 17) ? chunks : (1 << 17));
+  unsigned grid = knn_chunk_grid(a.nq);
   static const int wpe = getenv("GI_CHUNK_WPE") ? atoi(getenv("GI_CHUNK_WPE")) : 3;
   if (variant == 1) {
     size_t lds = (size_t)a.K * 64 * sizeof(uint64_t);

@@ -5,6 +5,8 @@ The variants are chosen when a context is created (gi_host.cpp tuning environmen
 GI_KNN_KERNEL 0 = per-lane LDS heap, 1 = query per wave, 2 = packet, 3 = per-lane with
 batched inserts, 4 = L-lane groups (GI_GROUP_LANES). Each must return the oracle's k-NN sets
 exactly: the fp32 metric is shared, and only photons tied at the k-th distance may differ.
+GI_KNN_KERNEL 5-7 = chunk kernels; GI_CHUNK_MINSUB sets how far an overflowing chunk is split
+(1 = down to single queries, 64 = straight to the per-lane fallback).
 It must also return its EstimateRadiance within rtol 1e-10 (fp64 sums in a different order).
 Leaf sizes are varied too, because the result set may not depend on the tree shape."""
 import os
@@ -34,6 +36,8 @@ VARIANTS = [
     {"GI_KNN_KERNEL": "6", "GI_CHUNK_CAP": "256"},
     {"GI_KNN_KERNEL": "7"},
     {"GI_KNN_KERNEL": "7", "GI_LEAF_SIZE": "50"},
+    {"GI_KNN_KERNEL": "7", "GI_CHUNK_MINSUB": "1"},
+    {"GI_KNN_KERNEL": "7", "GI_CHUNK_MINSUB": "64"},
 ]
 
 

@@ -115,6 +115,23 @@ struct KdNode {
   float4 lo, hi;
 };
 
+// The maps are read-only during a k-NN launch. Reading a node through the constant address
+// space lets wave-uniform node reads compile to scalar loads into SGPRs (through a generic
+// pointer, which could alias the kernel's own writes, the compiler emits vector loads into
+// VGPRs). The host compilation pass has no address spaces.
+__device__ __forceinline__ KdNode ld_node(const float *nodes, int n) {
+  KdNode r;
+#if __HIP_DEVICE_COMPILE__
+  typedef __attribute__((address_space(4))) const float cfloat;
+  cfloat *p = (cfloat *)nodes + 8 * n;
+  r.lo = make_float4(p[0], p[1], p[2], p[3]);
+  r.hi = make_float4(p[4], p[5], p[6], p[7]);
+#else
+  r = reinterpret_cast<const KdNode *>(nodes)[n];
+#endif
+  return r;
+}
+
 // squared distance from q to a node's tight box, evaluated with the same fp32 operation
 // sequence as the photon metric (d2 = fma(dz,dz, fma(dy,dy, dx*dx))): every rounding step is
 // monotone, so box_d2 <= metric d2 of every photon inside the box -- pruning on

@@ -15,6 +15,7 @@
 // LDS per wave: CAP * 8 bytes (1 KiB for K <= 64, 4 KiB for K <= 448), so occupancy is set
 // by registers, not by a per-lane heap.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include "gi_device.h"
 #include "gi_kernels.h"
 
@@ -121,17 +122,22 @@ __device__ __forceinline__ void select_k(uint64_t *buf, uint32_t *hist, int lane
   thr = T;
 }
 
-template <int CAP>
+template <int CAP, int LB, bool PROF>
 __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
   __shared__ uint64_t buf[CAP];
   __shared__ uint32_t hist[256];
+  __shared__ uint32_t stk[64];   // traversal stack: pending far children and their box distances
+  __shared__ float sdist[64];
   const int lane = threadIdx.x;
-  const KdNode *nodes = reinterpret_cast<const KdNode *>(a.map.nodes);
   const float4 *pos = reinterpret_cast<const float4 *>(a.map.pos4);
   const int L = a.map.nleaves;
   const int64_t N = a.map.n;
   const int K = a.K;
   uint64_t st_q = 0, st_found = 0, st_vis = 0;
+  // GI_KNN_DBG & 16: cycle counters ST_PHASE + 10.. (traversal, leaf scans, selects, select
+  // calls, node visits, whole queries)
+  const bool prof = PROF;  // a template argument: the counters cost registers
+  uint64_t pc[6] = {0, 0, 0, 0, 0, 0}, pt = 0, pq = 0;
   for (int64_t qq = blockIdx.x; qq < a.nq; qq += gridDim.x) {
     int64_t qg = a.q0 + qq;
     int64_t qi = a.perm ? (int64_t)a.perm[qg] : qg;
@@ -146,25 +152,65 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
     uint64_t thr = ((uint64_t)__float_as_uint(a.r2f) << 32) + 0x100000000ull;
     uint32_t visited = 0;
     bool tight = false;
+    if (prof) { pt = clock64(); pq = pt; }
+    // Traversal with a per-wave LDS stack: expanding a node loads both children's tight boxes
+    // (adjacent 32-B records, one scalar load) and pushes the far child with its box distance,
+    // so backtracking re-reads nothing from memory (the stackless walk re-read one parent per
+    // level climbed, each a dependent round trip). Near child = the smaller box distance; the
+    // visiting order does not change the result set.
     if (N > 0) {
-      int node = 1;
-      while (true) {
-        KdNode nd = nodes[node];
-        float pr = __uint_as_float((uint32_t)((thr - 1ull) >> 32));
-        if (kd_box_d2(nd.lo, nd.hi, qx, qy, qz) <= pr) {
-          if (node < L) {
-            float q = kd_axis_q(__float_as_int(nd.hi.w), qx, qy, qz);
-            node = 2 * node + ((q - nd.lo.w >= 0.0f) ? 1 : 0);
+      int sp = 0;
+      int node = 0;
+      {
+        KdNode r = ld_node(a.map.nodes, 1);
+        if (prof) pc[4]++;
+        if (kd_box_d2(r.lo, r.hi, qx, qy, qz) <= __uint_as_float((uint32_t)((thr - 1ull) >> 32)))
+          node = 1;
+      }
+      while (node) {
+        node = __builtin_amdgcn_readfirstlane(node);  // wave-uniform: scalar node loads
+        if (node < L) {
+          KdNode c0 = ld_node(a.map.nodes, 2 * node), c1 = ld_node(a.map.nodes, 2 * node + 1);
+          if (prof) pc[4]++;
+          float pr = __uint_as_float((uint32_t)((thr - 1ull) >> 32));
+          float d0 = kd_box_d2(c0.lo, c0.hi, qx, qy, qz), d1 = kd_box_d2(c1.lo, c1.hi, qx, qy, qz);
+          int nn = 2 * node, fn = nn + 1;
+          if (d1 < d0) {
+            float t = d0; d0 = d1; d1 = t;
+            nn = fn; fn = 2 * node;
+          }
+          if (d1 <= pr) {
+            stk[sp] = (uint32_t)fn;  // every lane stores the same value: no cross-lane LDS hazard
+            sdist[sp] = d1;
+            sp++;
+          }
+          if (d0 <= pr) {
+            node = nn;
             continue;
           }
+        } else {
           int leaf = node - L;
           int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
           visited += (uint32_t)(s1 - s0);
-          for (int64_t base = s0; base < s1; base += 64) {
+          if (prof) { uint64_t n = clock64(); pc[0] += n - pt; pt = n; }
+          // the leaf's photons, LB batches of 64 loaded before any is used: one memory round
+          // trip per leaf instead of one per batch (a wave's traversal is a dependent chain,
+          // and ~7 waves per SIMD cannot hide a round trip per 64 photons)
+          for (int64_t base0 = s0; base0 < s1; base0 += 64 * LB) {
+            float4 pf[LB];
+#pragma unroll
+            for (int u = 0; u < LB; u++) {
+              int64_t ii = base0 + u * 64 + lane;
+              pf[u] = pos[ii < s1 ? ii : s0];
+            }
+#pragma unroll
+            for (int u = 0; u < LB; u++) {
+            const int64_t base = base0 + u * 64;
+            if (base >= s1) break;
             int64_t ii = base + lane;
             uint64_t key = ~0ull;
             if (ii < s1) {
-              float4 p = pos[ii];
+              float4 p = pf[u];
               float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
               float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
               key = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)(uint32_t)ii;
@@ -174,7 +220,9 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
             uint32_t nnew = (uint32_t)__popcll(m);
             if (nnew == 0) continue;
             if (count + nnew > (uint32_t)CAP) {
+              if (prof) { uint64_t n = clock64(); pc[1] += n - pt; pt = n; pc[3]++; }
               select_k<CAP>(buf, hist, lane, count, K, thr);
+              if (prof) { uint64_t n = clock64(); pc[2] += n - pt; pt = n; }
               pass = key < thr;
               m = __ballot(pass);
               nnew = (uint32_t)__popcll(m);
@@ -186,27 +234,35 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
             }
             count += nnew;
             __syncthreads();
+            }
           }
           // first time K candidates are held: select now so the prune bound tightens from
           // r^2 to the K-th distance early (otherwise it stays r^2 until the buffer fills)
+          if (prof) { uint64_t n = clock64(); pc[1] += n - pt; pt = n; }
           if (K > 0 && count >= (uint32_t)K + (tight ? (uint32_t)a.sel_slack : 0u)) {
             select_k<CAP>(buf, hist, lane, count, K, thr);
             tight = true;
+            if (prof) { uint64_t n = clock64(); pc[2] += n - pt; pt = n; pc[3]++; }
           }
         }
-        while (node != 1) {
-          const KdNode &pn = nodes[node >> 1];
-          float q = kd_axis_q(__float_as_int(pn.hi.w), qx, qy, qz);
-          int near_is_right = (q - pn.lo.w >= 0.0f) ? 1 : 0;
-          if ((node & 1) == near_is_right) break;
-          node >>= 1;
+        // pop the nearest pending subtree still within the (possibly tightened) bound
+        node = 0;
+        float pr = __uint_as_float((uint32_t)((thr - 1ull) >> 32));
+        while (sp > 0) {
+          sp--;
+          if (ffirst(sdist[sp]) <= pr) {  // uniform: keeps the walk in scalar registers
+            node = (int)ufirst(stk[sp]);
+            break;
+          }
         }
-        if (node == 1) break;
-        node ^= 1;
       }
     }
     // exact K best
-    if (count > (uint32_t)K) select_k<CAP>(buf, hist, lane, count, K, thr);
+    if (prof) { uint64_t n = clock64(); pc[0] += n - pt; pt = n; }
+    if (count > (uint32_t)K) {
+      select_k<CAP>(buf, hist, lane, count, K, thr);
+      if (prof) { uint64_t n = clock64(); pc[2] += n - pt; pt = n; pc[3]++; }
+    }
     int num = (int)count;
     st_q += 1;
     st_found += (uint64_t)num;
@@ -218,7 +274,10 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
     }
     if (lane == 0) a.list_n[qi] = num;
     __syncthreads();
+    if (prof) pc[5] += clock64() - pq;
   }
+  if (prof && a.stats)
+    for (int i = 0; i < 6; i++) wave_add(&a.stats[ST_PHASE + 10 + i], pc[i]);
   if (a.stats && lane == 0) {
     unsigned long long *sd = stat_stripe(a.stats);
     if (st_q) atomicAdd(&sd[ST_KNN + a.stat_off], (unsigned long long)st_q);
@@ -810,15 +869,34 @@ void launch_list_estimate(const KnnArgs &a, hipStream_t st) {
   knn_list_estimate_kernel<<<(unsigned)grid, 64, 0, st>>>(a);
 }
 
+template <bool PROF>
+bool wave_launch(const KnnArgs &a, int need, int lb, unsigned grid, hipStream_t st) {
+  if (lb <= 1) {
+    if (need <= 128) knn_wave_kernel<128, 1, PROF><<<grid, 64, 0, st>>>(a);
+    else if (need <= 256) knn_wave_kernel<256, 1, PROF><<<grid, 64, 0, st>>>(a);
+    else if (need <= 512) knn_wave_kernel<512, 1, PROF><<<grid, 64, 0, st>>>(a);
+    else if (need <= 1024) knn_wave_kernel<1024, 1, PROF><<<grid, 64, 0, st>>>(a);
+    else return false;
+  } else {
+    if (need <= 128) knn_wave_kernel<128, 8, PROF><<<grid, 64, 0, st>>>(a);
+    else if (need <= 256) knn_wave_kernel<256, 8, PROF><<<grid, 64, 0, st>>>(a);
+    else if (need <= 512) knn_wave_kernel<512, 8, PROF><<<grid, 64, 0, st>>>(a);
+    else if (need <= 1024) knn_wave_kernel<1024, 8, PROF><<<grid, 64, 0, st>>>(a);
+    else return false;
+  }
+  return true;
+}
+
 bool launch_knn_wave(const KnnArgs &a, int cap_mul, hipStream_t st) {
   if (a.nq == 0) return true;
   int need = (a.K + 64) * cap_mul;
   int64_t grid = a.nq < (1 << 16) ? a.nq : (1 << 16);
-  if (need <= 128) knn_wave_kernel<128><<<(unsigned)grid, 64, 0, st>>>(a);
-  else if (need <= 256) knn_wave_kernel<256><<<(unsigned)grid, 64, 0, st>>>(a);
-  else if (need <= 512) knn_wave_kernel<512><<<(unsigned)grid, 64, 0, st>>>(a);
-  else if (need <= 1024) knn_wave_kernel<1024><<<(unsigned)grid, 64, 0, st>>>(a);
-  else return false;
+  // photon batches of 64 prefetched per leaf (GI_WAVE_LB: 1 or 8); GI_KNN_DBG & 16 selects the
+  // instance with phase cycle counters
+  static const int lb = getenv("GI_WAVE_LB") ? atoi(getenv("GI_WAVE_LB")) : 1;
+  bool ok = (a.dbg & 16) ? wave_launch<true>(a, need, lb, (unsigned)grid, st)
+                         : wave_launch<false>(a, need, lb, (unsigned)grid, st);
+  if (!ok) return false;
   if (a.mode != KNN_MODE_LIST) knn_list_estimate_kernel<<<(unsigned)grid, 64, 0, st>>>(a);
   return true;
 }

@@ -188,13 +188,47 @@ struct ChunkProf {
   }
 };
 
+// Wave-uniform walk over every kd leaf whose node box passes boxd(node) <= bound, with a
+// per-wave LDS stack (stk, >= tree depth entries): an expansion reads both children's boxes
+// (scalar loads, ld_node) and pushes one, so backtracking reads nothing from memory. leaf(l)
+// returns true to stop the walk. The visiting order does not matter to the callers (they
+// collect every photon within a fixed bound). Returns the number of node records read.
+template <typename BoxD, typename Leaf>
+__device__ __forceinline__ uint32_t walk_within(const float *nodes, int L, float bound, uint32_t *stk,
+                                                BoxD boxd, Leaf leaf) {
+  uint32_t reads = 1;
+  int sp = 0;
+  int node = (boxd(ld_node(nodes, 1)) <= bound) ? 1 : 0;
+  while (node) {
+    node = __builtin_amdgcn_readfirstlane(node);
+    if (node < L) {
+      KdNode c0 = ld_node(nodes, 2 * node), c1 = ld_node(nodes, 2 * node + 1);
+      reads += 2;
+      bool in0 = boxd(c0) <= bound, in1 = boxd(c1) <= bound;
+      if (in0 && in1) {
+        stk[sp] = (uint32_t)(2 * node + 1);  // every lane stores the same value
+        sp++;
+      }
+      if (in0) { node = 2 * node; continue; }
+      if (in1) { node = 2 * node + 1; continue; }
+    } else if (leaf(node - L)) {
+      return reads;
+    }
+    node = 0;
+    if (sp > 0) {
+      sp--;
+      node = (int)__builtin_amdgcn_readfirstlane((int)stk[sp]);
+    }
+  }
+  return reads;
+}
+
 template <int CAPC>
 __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, bool valid, float4 qp,
                                                    uint32_t cap, float4 *cpos, uint32_t *cidx,
-                                                   uint32_t *crgbe, uint32_t *hist, ChunkGeom &G,
-                                                   ChunkProf &P) {
+                                                   uint32_t *crgbe, uint32_t *hist, uint32_t *stk,
+                                                   ChunkGeom &G, ChunkProf &P) {
   constexpr int PER = CAPC / 64;
-  const KdNode *nodes = reinterpret_cast<const KdNode *>(a.map.nodes);
   const float4 *pos = reinterpret_cast<const float4 *>(a.map.pos4);
   const int L = a.map.nleaves;
   const int64_t N = a.map.n;
@@ -217,7 +251,7 @@ __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, b
   if (N > 0 && K > 0) {
     int node = 1;
     while (node < L) {
-      KdNode nd = nodes[node];
+      KdNode nd = ld_node(a.map.nodes, node);
       float qa = kd_axis_q(__float_as_int(nd.hi.w), cx, cy, cz);
       node = 2 * node + ((qa - nd.lo.w >= 0.0f) ? 1 : 0);
       if (P.on) P.c[5]++;
@@ -233,47 +267,31 @@ __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, b
       float RA2 = __double2float_ru((double)dk2 * (1.0 + 1e-5));
       uint32_t na = 0;
       bool ovf = false;
-      int nd = 1;
-      while (true) {
-        KdNode b = nodes[nd];
-        if (P.on) P.c[5]++;
-        if (kd_box_d2(b.lo, b.hi, cx, cy, cz) <= RA2) {
-          if (nd < L) {
-            float qa = kd_axis_q(__float_as_int(b.hi.w), cx, cy, cz);
-            nd = 2 * nd + ((qa - b.lo.w >= 0.0f) ? 1 : 0);
-            continue;
-          }
-          int lf = nd - L;
-          int64_t a0 = ((int64_t)lf * N) / L, a1 = ((int64_t)(lf + 1) * N) / L;
-          for (int64_t bb = a0; bb < a1; bb += 64) {
-            int64_t ii = bb + lane;
-            bool take = false;
-            float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (ii < a1) {
-              p = pos[ii];
-              take = metric(cx, cy, cz, p) <= RA2;
+      uint32_t rd = walk_within(a.map.nodes, L, RA2, stk,
+          [&](const KdNode &b) { return kd_box_d2(b.lo, b.hi, cx, cy, cz); },
+          [&](int lf) {
+            int64_t a0 = ((int64_t)lf * N) / L, a1 = ((int64_t)(lf + 1) * N) / L;
+            for (int64_t bb = a0; bb < a1; bb += 64) {
+              int64_t ii = bb + lane;
+              bool take = false;
+              float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+              if (ii < a1) {
+                p = pos[ii];
+                take = metric(cx, cy, cz, p) <= RA2;
+              }
+              uint64_t m = __ballot(take);
+              uint32_t nn = (uint32_t)__popcll(m);
+              if (na + nn > (uint32_t)CAPC) { ovf = true; return true; }
+              if (take) {
+                uint32_t off = na + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                cpos[off] = p;
+                cidx[off] = (uint32_t)ii;
+              }
+              na += nn;
             }
-            uint64_t m = __ballot(take);
-            uint32_t nn = (uint32_t)__popcll(m);
-            if (na + nn > (uint32_t)CAPC) { ovf = true; break; }
-            if (take) {
-              uint32_t off = na + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-              cpos[off] = p;
-              cidx[off] = (uint32_t)ii;
-            }
-            na += nn;
-          }
-          if (ovf) break;
-        }
-        while (nd != 1) {
-          const KdNode &pn = nodes[nd >> 1];
-          float qa = kd_axis_q(__float_as_int(pn.hi.w), cx, cy, cz);
-          if ((nd & 1) == ((qa - pn.lo.w >= 0.0f) ? 1 : 0)) break;
-          nd >>= 1;
-        }
-        if (nd == 1) break;
-        nd ^= 1;
-      }
+            return false;
+          });
+      if (P.on) P.c[5] += rd;
       __syncthreads();
       if (!ovf && na >= (uint32_t)K) {
         uint64_t kc[PER];
@@ -309,53 +327,37 @@ __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, b
   uint32_t count = 0;
   bool overflow = false;
   if (N > 0 && K > 0) {
-    int node = 1;
-    while (true) {
-      KdNode nd = nodes[node];
-      if (P.on) P.c[6]++;
-      if (gap2(nd.lo.x, nd.lo.y, nd.lo.z, nd.hi.x, nd.hi.y, nd.hi.z, bl, bh) <= U2) {
-        if (node < L) {
-          float qa = kd_axis_q(__float_as_int(nd.hi.w), cx, cy, cz);
-          node = 2 * node + ((qa - nd.lo.w >= 0.0f) ? 1 : 0);
-          continue;
-        }
-        int leaf = node - L;
-        int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
-        for (int64_t b = s0; b < s1; b += 64) {
-          int64_t ii = b + lane;
-          bool take = false;
-          float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (ii < s1) {
-            p = pos[ii];
-            take = gap2(p.x, p.y, p.z, p.x, p.y, p.z, bl, bh) <= U2;
+    uint32_t rd = walk_within(a.map.nodes, L, U2, stk,
+        [&](const KdNode &b) {
+          return gap2(b.lo.x, b.lo.y, b.lo.z, b.hi.x, b.hi.y, b.hi.z, bl, bh);
+        },
+        [&](int leaf) {
+          int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
+          for (int64_t b = s0; b < s1; b += 64) {
+            int64_t ii = b + lane;
+            bool take = false;
+            float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (ii < s1) {
+              p = pos[ii];
+              take = gap2(p.x, p.y, p.z, p.x, p.y, p.z, bl, bh) <= U2;
+            }
+            uint64_t m = __ballot(take);
+            uint32_t nn = (uint32_t)__popcll(m);
+            if (count + nn > cap) {
+              overflow = true;
+              return true;
+            }
+            if (take) {
+              uint32_t off = count + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+              cpos[off] = p;
+              cidx[off] = (uint32_t)ii;
+              crgbe[off] = a.map.rgbe[ii];
+            }
+            count += nn;
           }
-          uint64_t m = __ballot(take);
-          uint32_t nn = (uint32_t)__popcll(m);
-          if (count + nn > cap) {
-            overflow = true;
-            break;
-          }
-          if (take) {
-            uint32_t off = count + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-            cpos[off] = p;
-            cidx[off] = (uint32_t)ii;
-            crgbe[off] = a.map.rgbe[ii];
-          }
-          count += nn;
-        }
-        if (overflow) break;
-      }
-      // stackless backtrack (near side by c)
-      while (node != 1) {
-        const KdNode &pn = nodes[node >> 1];
-        float qa = kd_axis_q(__float_as_int(pn.hi.w), cx, cy, cz);
-        int near_is_right = (qa - pn.lo.w >= 0.0f) ? 1 : 0;
-        if ((node & 1) == near_is_right) break;
-        node >>= 1;
-      }
-      if (node == 1) break;
-      node ^= 1;
-    }
+          return false;
+        });
+    if (P.on) P.c[6] += rd;
   }
   G.count = count;
   G.overflow = overflow;
@@ -552,7 +554,7 @@ __device__ __forceinline__ float bin_floor(uint32_t b, float lo, float hi, float
 __device__ __forceinline__ float next_up(float x) { return __uint_as_float(__float_as_uint(x) + 1u); }
 __device__ __forceinline__ float next_down(float x) { return __uint_as_float(__float_as_uint(x) - 1u); }
 
-template <int WPE>
+template <int WPE, bool PROF>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE)))
 void knn_chunk_lane_kernel(KnnArgs a) {
   constexpr int CAPC = 256;
@@ -560,12 +562,13 @@ void knn_chunk_lane_kernel(KnnArgs a) {
   __shared__ uint32_t cidx[CAPC];
   __shared__ uint32_t crgbe[CAPC];
   __shared__ uint32_t hist[256];
+  __shared__ uint32_t stk[64];  // kd walk stack (walk_within)
   __shared__ uint8_t sel[64 * 64];  // kept LDS slots, [s][lane] (K <= 64)
   const int lane = threadIdx.x;
   const int K = a.K;
   uint64_t st_q = 0, st_found = 0, st_vis = 0;
   ChunkProf P;
-  P.on = (a.dbg & 16) != 0;
+  P.on = PROF;  // a template argument: the counters cost registers
   P.t = 0;
   for (int i = 0; i < 10; i++) P.c[i] = 0;
   const int minsub = a.chunk_minsub > 0 ? a.chunk_minsub : 64;
@@ -588,7 +591,7 @@ void knn_chunk_lane_kernel(KnnArgs a) {
     if (P.on) P.t = clock64();
     ChunkGeom G;
     // byte counters below: at most 255 candidates per chunk
-    chunk_bound_gather<CAPC>(a, lane, act, qp, CAPC - 1, cpos, cidx, crgbe, hist, G, P);
+    chunk_bound_gather<CAPC>(a, lane, act, qp, CAPC - 1, cpos, cidx, crgbe, hist, stk, G, P);
     __syncthreads();
     if (G.overflow) continue;
     pending &= ~gm;
@@ -734,6 +737,7 @@ void knn_chunk_kernel(KnnArgs a) {
   __shared__ uint32_t cidx[CAPC];
   __shared__ uint32_t crgbe[CAPC];
   __shared__ uint32_t hist[256];
+  __shared__ uint32_t stk[64];  // kd walk stack (walk_within)
   __shared__ SlotT sel[64 * 64];      // kept LDS slots per query of the chunk (K <= 64)
   __shared__ float smax[64];          // per query: K-th d2
   __shared__ int snum[64];
@@ -753,7 +757,7 @@ void knn_chunk_kernel(KnnArgs a) {
     if (vmask == 0) continue;
     if (P.on) P.t = clock64();
     ChunkGeom G;
-    chunk_bound_gather<CAPC>(a, lane, valid, qp, CAPC, cpos, cidx, crgbe, hist, G, P);
+    chunk_bound_gather<CAPC>(a, lane, valid, qp, CAPC, cpos, cidx, crgbe, hist, stk, G, P);
     if (G.overflow) {
       to_fallback(a, vmask, valid, qi, lane);
       __syncthreads();
@@ -868,6 +872,7 @@ __global__ __launch_bounds__(64) void knn_chunk_heap_kernel(KnnArgs a) {
   __shared__ uint32_t cidx[CAPC];
   __shared__ uint32_t crgbe[CAPC];
   __shared__ uint32_t hist[256];
+  __shared__ uint32_t stk[64];  // kd walk stack (walk_within)
   __shared__ uint16_t ord[CAPC];      // candidate slots sorted by distance to the chunk centre
   extern __shared__ uint64_t hsm[];   // per-lane 4-ary heaps [K][64]
   uint64_t *h = hsm + threadIdx.x;
@@ -886,7 +891,7 @@ __global__ __launch_bounds__(64) void knn_chunk_heap_kernel(KnnArgs a) {
     uint64_t vmask = __ballot(valid);
     if (vmask == 0) continue;
     ChunkGeom G;
-    chunk_bound_gather<CAPC>(a, lane, valid, qp, CAPC, cpos, cidx, crgbe, hist, G, P);
+    chunk_bound_gather<CAPC>(a, lane, valid, qp, CAPC, cpos, cidx, crgbe, hist, stk, G, P);
     if (G.overflow) {
       to_fallback(a, vmask, valid, qi, lane);
       __syncthreads();
@@ -978,7 +983,7 @@ bool launch_knn_chunk(const KnnArgs &a, int cap, int variant, hipStream_t st) {
   if (a.nq == 0) return true;
   if (a.mode == KNN_MODE_LIST || a.K > 64) return false;
   unsigned grid = knn_chunk_grid(a.nq);
-  static const int wpe = getenv("GI_CHUNK_WPE") ? atoi(getenv("GI_CHUNK_WPE")) : 3;
+  static const int wpe = getenv("GI_CHUNK_WPE") ? atoi(getenv("GI_CHUNK_WPE")) : 4;
   if (variant == 1) {
     size_t lds = (size_t)a.K * 64 * sizeof(uint64_t);
     if (cap <= 256) knn_chunk_heap_kernel<256><<<grid, 64, lds, st>>>(a);
@@ -986,9 +991,10 @@ bool launch_knn_chunk(const KnnArgs &a, int cap, int variant, hipStream_t st) {
     return true;
   }
   if (variant == 2) {
-    if (wpe >= 4) knn_chunk_lane_kernel<4><<<grid, 64, 0, st>>>(a);
-    else if (wpe == 3) knn_chunk_lane_kernel<3><<<grid, 64, 0, st>>>(a);
-    else knn_chunk_lane_kernel<2><<<grid, 64, 0, st>>>(a);
+    if (a.dbg & 16) knn_chunk_lane_kernel<3, true><<<grid, 64, 0, st>>>(a);
+    else if (wpe >= 4) knn_chunk_lane_kernel<4, false><<<grid, 64, 0, st>>>(a);
+    else if (wpe == 3) knn_chunk_lane_kernel<3, false><<<grid, 64, 0, st>>>(a);
+    else knn_chunk_lane_kernel<2, false><<<grid, 64, 0, st>>>(a);
     return true;
   }
   if (cap <= 256) {

@@ -173,6 +173,9 @@ void kd_build(HostMap &M, int leaf_size, int threads) {
 
 struct DevMap {
   DBuf pos4, rgbe, nodes;
+  DBuf dk;               // per-photon K-th distance bounds (KdView::dk), valid for dk_k / dk_r2
+  int dk_k = -1;
+  float dk_r2 = -1.0f;
   int64_t n = 0;
   int nleaves = 1, levels = 0;
   KdView view() const {
@@ -184,6 +187,7 @@ struct DevMap {
     v.nleaves = nleaves;
     v.levels = levels;
     for (int k = 0; k < 3; k++) v.bmin[k] = v.bmax[k] = 0;
+    v.dk = nullptr;
     return v;
   }
 };
@@ -226,6 +230,8 @@ struct gi_ctx {
   DBuf qpos[2], qshade[2], qkey[2], qout[2];
   DBuf list_idx, list_d2, list_n;
   DBuf fb_list, fb_count, fb_dense;  // chunk k-NN fallback queries (striped, compacted)
+  DBuf dk_q;                       // photon positions as queries (ensure_dk)
+  bool use_dk = true;              // wave k-NN kernel starts from per-photon K-th bounds
   uint64_t fb_total = 0;
   DBuf qseg[2];  // K-best lists of the query-per-wave k-NN path
   size_t qcap_hint[2] = {0, 0};
@@ -234,7 +240,7 @@ struct gi_ctx {
   DBuf scan_lvl[8], scan_out[8];
   // photon tracing scratch
   DBuf pcounts, poffs, pbuf;
-  int64_t prim_per_batch = 1 << 17;
+  int64_t prim_per_batch = 1 << 19;  // denser query batches: fewer chunk k-NN overflows (measured best)
   SortScratch sorter;
   bool sort_queries = true;
   float sbmin[3] = {0, 0, 0}, sbmax[3] = {1, 1, 1};
@@ -363,6 +369,7 @@ int upload_map(gi_ctx *c, int mi) {
   D.n = n;
   D.nleaves = H.nleaves;
   D.levels = H.levels;
+  D.dk_k = -1;
   c->map_valid[mi] = n > 0;
   return GI_OK;
 }
@@ -510,6 +517,41 @@ KnnArgs knn_args(gi_ctx *c, int mi) {
   return k;
 }
 
+// Per-photon K-th distance bounds of map mi for this launch's K and r (KdView::dk): one
+// KNN_MODE_DK pass of the wave kernel with the photons themselves as queries, computed once
+// per map and (K, r). The wave kernel then starts each query from the bound of the photons in
+// its leaf instead of from r.
+int ensure_dk(gi_ctx *c, KnnArgs &k) {
+  int mi = k.stat_off ? 1 : 0;
+  DevMap &D = c->dmap[mi];
+  if (!c->use_dk || D.n == 0 || k.K <= 0) return GI_OK;
+  if (D.dk_k != k.K || D.dk_r2 != k.r2f) {
+    D.dk_k = -1;
+    HIPCHK(c, c->dk_q.ensure((size_t)D.n * 16));
+    HIPCHK(c, D.dk.ensure((size_t)D.n * 4));
+    launch_photon_queries(D.pos4.as<float>(), D.n, c->dk_q.as<float4>(), c->stream);
+    KnnArgs d = k;
+    d.mode = KNN_MODE_DK;
+    d.map.dk = nullptr;
+    d.qpos = c->dk_q.as<float4>();
+    d.qshade = nullptr;
+    d.perm = nullptr;
+    d.nq = D.n;
+    d.q0 = 0;
+    d.out_dk = D.dk.as<float>();
+    d.stats = nullptr;
+    d.dbg = 0;
+    if (!launch_knn_wave(d, c->wave_cap_mul, c->stream))
+      return fail(c, GI_ERR_ARG, "k-NN bound pass: unsupported estimate size");
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    D.dk_k = k.K;
+    D.dk_r2 = k.r2f;
+  }
+  k.map.dk = D.dk.as<float>();
+  return GI_OK;
+}
+
 // run a k-NN launch over nq queries (chunked when the heap lives in global scratch)
 int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
   // auto (-1): chunk kernel with lane select (+ per-lane fallback) for K <= 64, the per-lane
@@ -603,6 +645,10 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
         k.list_d2 = c->list_d2.as<float>();
         k.list_n = c->list_n.as<int32_t>();
       }
+    }
+    if (kind == 1) {
+      int rc = ensure_dk(c, k);
+      if (rc) return rc;
     }
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     bool ok = true;
@@ -879,6 +925,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_HEAP_ARITY")) c->heap_arity = std::max(2, atoi(s));
   if (const char *s = getenv("GI_IND_WAVES")) c->ind_waves = std::max(1, atoi(s));
   if (const char *s = getenv("GI_SPLIT_IND")) c->split_ind = atoi(s) != 0;
+  if (const char *s = getenv("GI_KNN_DK")) c->use_dk = atoi(s) != 0;
   if (const char *s = getenv("GI_SORT_QUERIES")) c->sort_queries = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_KERNEL")) c->knn_kernel_kind = atoi(s);
   *out = c;
@@ -891,7 +938,7 @@ void gi_destroy(gi_ctx *c) {
   DBuf *bufs[] = {&c->d_nodes, &c->d_elems, &c->d_shapes, &c->d_tris, &c->d_mats, &c->d_lights,
                   &c->d_lut, &c->d_stats, &c->spawn, &c->npaths, &c->path_off, &c->base,
                   &c->pixels, &c->rgbf, &c->rgb8, &c->gheap_d2, &c->gheap_idx, &c->qcount,
-                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont, &c->fb_list, &c->fb_count, &c->fb_dense};
+                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont, &c->fb_list, &c->fb_count, &c->fb_dense, &c->dk_q};
   for (DBuf *b : bufs) b->release();
   for (int l = 0; l < 2; l++) {
     c->qpos[l].release(); c->qshade[l].release(); c->qkey[l].release(); c->qout[l].release();
@@ -902,6 +949,7 @@ void gi_destroy(gi_ctx *c) {
     c->dmap[m].pos4.release();
     c->dmap[m].rgbe.release();
     c->dmap[m].nodes.release();
+    c->dmap[m].dk.release();
   }
   sort_scratch_release(c->sorter);
   if (c->ev0) hipEventDestroy(c->ev0);

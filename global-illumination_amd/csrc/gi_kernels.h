@@ -231,7 +231,7 @@ __device__ __forceinline__ void wave_add(unsigned long long *dst, uint64_t v) {
 // query-list slot with no query (deterministic slots a path did not use): qpos.w bits
 constexpr uint32_t QMETA_NONE = 0xffffffffu;
 
-enum { KNN_MODE_RADIANCE = 0, KNN_MODE_IRRADIANCE = 1, KNN_MODE_LIST = 2 };
+enum { KNN_MODE_RADIANCE = 0, KNN_MODE_IRRADIANCE = 1, KNN_MODE_LIST = 2, KNN_MODE_DK = 3 };
 
 struct KnnArgs {
   KdView map;
@@ -257,6 +257,7 @@ struct KnnArgs {
   double *out;             // [nq*3]
   int32_t *out_n;          // optional
   float *out_maxd2;        // optional
+  float *out_dk;           // KNN_MODE_DK: per query, the K-th distance bound (KdView::dk)
   int32_t *out_idx;        // KNN_MODE_LIST
   float *out_d2;
   int32_t *list_idx;       // query-per-wave kernel: K-best lists [nq][K] (kd-order index)
@@ -292,6 +293,8 @@ hipError_t launch_scan(const uint32_t *in, uint32_t *out, int64_t n, ScanTemp &t
                        hipStream_t st);
 void launch_primary(const RenderArgs &a, hipStream_t st);
 void launch_path(const RenderArgs &a, hipStream_t st);
+// float4 queries {x, y, z, 0} at the photons of a map (KNN_MODE_DK input)
+void launch_photon_queries(const float *pos4, int64_t n, float4 *q, hipStream_t st);
 // dense copy of the striped chunk fallback list; total length to *total
 void launch_fb_compact(const uint32_t *list, const uint32_t *count, uint32_t cap_s, uint32_t *dense,
                        uint32_t *total, hipStream_t st);  // slot0 + indirect + Monte Carlo

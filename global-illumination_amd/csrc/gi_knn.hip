@@ -64,48 +64,85 @@ __device__ __forceinline__ uint32_t radix_pick(uint32_t *hist, int lane, uint32_
   return (uint32_t)__shfl((int)d, L, 64);
 }
 
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
+}
+
+// Narrow [lo, hi] (inclusive, u32 digit values of the keys that pass `member`) to the single
+// value of the need-th smallest, with 256-bin LDS histograms over the live range: pass p bins
+// by (v - lo) >> shift with 2^shift the smallest power of two giving <= 256 bins. Unlike fixed
+// radix bytes, the bins always span the keys actually present (a fixed top byte of nearby d2
+// values is one exponent: every lane's LDS atomic would hit one or two bins).
+template <typename Digit, typename Member>
+__device__ __forceinline__ uint32_t range_select(const uint64_t *buf, uint32_t *hist, int lane,
+                                                 uint32_t count, uint32_t &need, uint32_t lo,
+                                                 uint32_t hi, Digit digit, Member member) {
+  while (hi > lo) {
+    uint32_t span = hi - lo;
+    int shift = 32 - __clz((int)span) - 8;
+    if (shift < 0) shift = 0;
+    hist[4 * lane] = hist[4 * lane + 1] = hist[4 * lane + 2] = hist[4 * lane + 3] = 0u;
+    __syncthreads();
+    for (uint32_t s = (uint32_t)lane; s < count; s += 64) {
+      uint64_t k = buf[s];
+      uint32_t v = digit(k);
+      if (member(k) && v >= lo && v <= hi) atomicAdd(&hist[(v - lo) >> shift], 1u);
+    }
+    __syncthreads();
+    uint32_t B = radix_pick(hist, lane, need);
+    __syncthreads();
+    uint32_t nlo = lo + (B << shift);
+    uint32_t w = (shift >= 32) ? 0xffffffffu : ((1u << shift) - 1u);
+    hi = (hi - nlo > w) ? nlo + w : hi;
+    lo = nlo;
+  }
+  return lo;
+}
+
+// Wave-level selection over the candidate buffer buf[0, count): find the K-th smallest key T,
+// keep exactly the keys <= T (compacted to buf[0, K)) and set thr = T (a later candidate must
+// be < T). The d2 bits are resolved by range_select; the index bits only when several keys
+// share the K-th distance. Keys are re-read from LDS on every pass (no per-lane key arrays:
+// the register budget sets this kernel's occupancy).
 template <int CAP>
 __device__ __forceinline__ void select_k(uint64_t *buf, uint32_t *hist, int lane, uint32_t &count,
                                          int K, uint64_t &thr) {
-  uint32_t need = (uint32_t)K, prefix = 0;
-#pragma unroll 1
-  for (int shift = 24; shift >= 0; shift -= 8) {
-    hist[4 * lane] = hist[4 * lane + 1] = hist[4 * lane + 2] = hist[4 * lane + 3] = 0u;
-    __syncthreads();
-    uint32_t hm = (shift == 24) ? 0u : (0xffffffffu << (shift + 8));
-    for (uint32_t s = (uint32_t)lane; s < count; s += 64) {
-      uint32_t h = (uint32_t)(buf[s] >> 32);
-      if (((h ^ prefix) & hm) == 0u) atomicAdd(&hist[(h >> shift) & 255u], 1u);
-    }
-    __syncthreads();
-    prefix |= radix_pick(hist, lane, need) << shift;
-    __syncthreads();
+  uint32_t lo = 0xffffffffu, hi = 0u;
+  for (uint32_t s = (uint32_t)lane; s < count; s += 64) {
+    uint32_t h = (uint32_t)(buf[s] >> 32);
+    lo = min(lo, h);
+    hi = max(hi, h);
   }
+  lo = wave_min_u32(lo);
+  hi = wave_max_u32(hi);
+  uint32_t need = (uint32_t)K;
+  const uint32_t prefix = range_select(buf, hist, lane, count, need, lo, hi,
+                                       [](uint64_t k) { return (uint32_t)(k >> 32); },
+                                       [](uint64_t) { return true; });
   // prefix = d2 bits of the K-th key; `need` of the keys with exactly that d2 are kept
-  uint32_t eq = 0;
+  uint32_t eq = 0, ilo = 0xffffffffu, ihi = 0u;
   for (uint32_t s0 = 0; s0 < count; s0 += 64) {
     uint32_t s = s0 + (uint32_t)lane;
-    eq += (uint32_t)__popcll(__ballot(s < count && (uint32_t)(buf[s < count ? s : 0] >> 32) == prefix));
+    uint64_t k = (s < count) ? buf[s] : ~0ull;
+    bool e = s < count && (uint32_t)(k >> 32) == prefix;
+    if (e) {
+      ilo = min(ilo, (uint32_t)k);
+      ihi = max(ihi, (uint32_t)k);
+    }
+    eq += (uint32_t)__popcll(__ballot(e));
   }
   uint32_t tidx = 0xffffffffu;
-  if (need < eq) {
-    uint32_t lp = 0;
-#pragma unroll 1
-    for (int shift = 24; shift >= 0; shift -= 8) {
-      hist[4 * lane] = hist[4 * lane + 1] = hist[4 * lane + 2] = hist[4 * lane + 3] = 0u;
-      __syncthreads();
-      uint32_t lm = (shift == 24) ? 0u : (0xffffffffu << (shift + 8));
-      for (uint32_t s = (uint32_t)lane; s < count; s += 64) {
-        uint64_t k = buf[s];
-        uint32_t h = (uint32_t)(k >> 32), l = (uint32_t)k;
-        if (h == prefix && ((l ^ lp) & lm) == 0u) atomicAdd(&hist[(l >> shift) & 255u], 1u);
-      }
-      __syncthreads();
-      lp |= radix_pick(hist, lane, need) << shift;
-      __syncthreads();
-    }
-    tidx = lp;
-  }
+  if (need < eq)
+    tidx = range_select(buf, hist, lane, count, need, wave_min_u32(ilo), wave_max_u32(ihi),
+                        [](uint64_t k) { return (uint32_t)k; },
+                        [prefix](uint64_t k) { return (uint32_t)(k >> 32) == prefix; });
   uint64_t T = ((uint64_t)prefix << 32) | (uint64_t)tidx;
   // compact the keys <= T (exactly K) to buf[0, K); writes never pass unread entries
   uint32_t base = 0;
@@ -153,6 +190,41 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
     uint32_t visited = 0;
     bool tight = false;
     if (prof) { pt = clock64(); pq = pt; }
+    if (a.map.dk && N > 0 && K > 0) {
+      // Start from a bound instead of r: for any photon p, d_K(q) <= |q - p| + d_K(p)
+      // (triangle inequality; the map's per-photon dk holds d_K(p)). The photons of the leaf
+      // containing q give a bound within a few percent of d_K(q), so the walk prunes to the
+      // K-neighbourhood from the first leaf on and the buffer rarely needs a select before
+      // the final one.
+      int node = 1;
+      while (node < L) {
+        KdNode nd = ld_node(a.map.nodes, node);
+        float qa = kd_axis_q(__float_as_int(nd.hi.w), qx, qy, qz);
+        node = 2 * node + ((qa - nd.lo.w >= 0.0f) ? 1 : 0);
+      }
+      int leaf = node - L;
+      int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
+      double best = INFINITY;
+      for (int64_t b = s0; b < s1; b += 64) {
+        int64_t ii = b + lane;
+        if (ii < s1) {
+          float4 p = pos[ii];
+          float dkp = a.map.dk[ii];
+          float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
+          float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
+          // fp32 metric -> true distance: 1e-5 relative margin
+          if (dkp < INFINITY) best = fmin(best, sqrt((double)d2 * (1.0 + 1e-5)) + (double)dkp);
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) best = fmin(best, __shfl_xor(best, o, 64));
+      if (best < INFINITY) {
+        double U = best * (1.0 + 1e-6) + 1e-12;
+        float U2 = __double2float_ru(U * U * (1.0 + 1e-5));
+        if (U2 < a.r2f) thr = ((uint64_t)__float_as_uint(U2) << 32) + 0x100000000ull;
+        tight = true;
+      }
+    }
     // Traversal with a per-wave LDS stack: expanding a node loads both children's tight boxes
     // (adjacent 32-B records, one scalar load) and pushes the far child with its box distance,
     // so backtracking re-reads nothing from memory (the stackless walk re-read one parent per
@@ -267,12 +339,22 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
     st_q += 1;
     st_found += (uint64_t)num;
     st_vis += visited;
-    for (int s = lane; s < K; s += 64) {
-      bool v = s < num;
-      a.list_idx[qi * K + s] = v ? (int32_t)(uint32_t)buf[s] : -1;
-      a.list_d2[qi * K + s] = v ? __uint_as_float((uint32_t)(buf[s] >> 32)) : -1.0f;
+    if (a.mode == KNN_MODE_DK) {
+      // true-distance upper bound of the K-th neighbour: K-th fp32 metric, 1e-5 margin, round up
+      float km = 0.0f;
+      for (int s = lane; s < num; s += 64) km = fmaxf(km, __uint_as_float((uint32_t)(buf[s] >> 32)));
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) km = fmaxf(km, __shfl_xor(km, o, 64));
+      if (lane == 0)
+        a.out_dk[qi] = (num < K) ? INFINITY : __double2float_ru(sqrt((double)km * (1.0 + 1e-5)));
+    } else {
+      for (int s = lane; s < K; s += 64) {
+        bool v = s < num;
+        a.list_idx[qi * K + s] = v ? (int32_t)(uint32_t)buf[s] : -1;
+        a.list_d2[qi * K + s] = v ? __uint_as_float((uint32_t)(buf[s] >> 32)) : -1.0f;
+      }
+      if (lane == 0) a.list_n[qi] = num;
     }
-    if (lane == 0) a.list_n[qi] = num;
     __syncthreads();
     if (prof) pc[5] += clock64() - pq;
   }
@@ -897,8 +979,23 @@ bool launch_knn_wave(const KnnArgs &a, int cap_mul, hipStream_t st) {
   bool ok = (a.dbg & 16) ? wave_launch<true>(a, need, lb, (unsigned)grid, st)
                          : wave_launch<false>(a, need, lb, (unsigned)grid, st);
   if (!ok) return false;
-  if (a.mode != KNN_MODE_LIST) knn_list_estimate_kernel<<<(unsigned)grid, 64, 0, st>>>(a);
+  if (a.mode != KNN_MODE_LIST && a.mode != KNN_MODE_DK)
+    knn_list_estimate_kernel<<<(unsigned)grid, 64, 0, st>>>(a);
   return true;
+}
+
+__global__ void photon_queries_kernel(const float4 *pos, int64_t n, float4 *q) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    float4 p = pos[i];
+    q[i] = make_float4(p.x, p.y, p.z, 0.0f);
+  }
+}
+
+void launch_photon_queries(const float *pos4, int64_t n, float4 *q, hipStream_t st) {
+  if (n == 0) return;
+  photon_queries_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(
+      reinterpret_cast<const float4 *>(pos4), n, q);
 }
 
 }  // namespace gi

@@ -108,6 +108,10 @@ struct KdView {
   int32_t nleaves;
   int32_t levels;
   float bmin[3], bmax[3];
+  // optional, per photon (kd order): an upper bound on the true distance from the photon to
+  // its K-th nearest photon within r (the launch's K and r), +inf where fewer than K lie
+  // within r; nullptr when not computed for this K / r
+  const float *dk;
 };
 
 }  // namespace gi

@@ -6,7 +6,8 @@ GI_KNN_KERNEL 0 = per-lane LDS heap, 1 = query per wave, 2 = packet, 3 = per-lan
 batched inserts, 4 = L-lane groups (GI_GROUP_LANES). Each must return the oracle's k-NN sets
 exactly: the fp32 metric is shared, and only photons tied at the k-th distance may differ.
 GI_KNN_KERNEL 5-7 = chunk kernels; GI_CHUNK_MINSUB sets how far an overflowing chunk is split
-(1 = down to single queries, 64 = straight to the per-lane fallback).
+(1 = down to single queries, 64 = straight to the per-lane fallback). GI_KNN_DK=0 turns off the
+wave kernel's start from per-photon K-th distance bounds (on by default).
 It must also return its EstimateRadiance within rtol 1e-10 (fp64 sums in a different order).
 Leaf sizes are varied too, because the result set may not depend on the tree shape."""
 import os
@@ -24,6 +25,7 @@ pytestmark = pytest.mark.gpu
 VARIANTS = [
     {"GI_KNN_KERNEL": "0", "GI_LEAF_SIZE": "16"},
     {"GI_KNN_KERNEL": "1", "GI_LEAF_SIZE": "512"},
+    {"GI_KNN_KERNEL": "1", "GI_KNN_DK": "0"},
     {"GI_KNN_KERNEL": "2"},
     {"GI_KNN_KERNEL": "3", "GI_LANE_CHUNK": "4"},
     {"GI_KNN_KERNEL": "3", "GI_LANE_CHUNK": "16", "GI_LEAF_SIZE": "32"},

@@ -209,7 +209,7 @@ struct gi_ctx {
   HostMap hmap[2];
   DevMap dmap[2];
   bool map_valid[2] = {false, false};
-  int leaf_size[2] = {64, 512};  // photons per kd leaf, per map (global, caustic)
+  int leaf_size[2] = {64, 256};  // photons per kd leaf, per map (global, caustic)
   int wave_cap_mul = 1;
   int chunk_cap = 256;            // chunk kernel: LDS candidate capacity per 64-query chunk
   int chunk_minsub = 64;          // chunk kernel: overflowing chunks retried down to this group size (64: no retry, measured best)

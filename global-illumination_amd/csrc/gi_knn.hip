@@ -159,8 +159,125 @@ __device__ __forceinline__ void select_k(uint64_t *buf, uint32_t *hist, int lane
   thr = T;
 }
 
-template <int CAP, int LB, bool PROF>
-__global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
+// EstimateRadiance / EstimateIrradiance (photon_utils.cpp:72-162, 209-246) of one query from its
+// num K-best photons (fetch_id(s), fetch_d2(s) for s < num), one wave per query: photons spread
+// over the lanes, fp64 partial sums reduced across the wave (butterfly). Shared by the
+// list-estimate kernel and the wave kernel's fused estimate, so both sum in the same order.
+template <typename FetchId, typename FetchD2>
+__device__ __forceinline__ void wave_estimate(const KnnArgs &a, int64_t qi, float4 qp, int num,
+                                              FetchId fetch_id, FetchD2 fetch_d2) {
+  const int lane = threadIdx.x;
+  const int K = a.K;
+  double maxd2 = kEps;
+  double o0 = 0, o1 = 0, o2 = 0;
+  if (num > 0) {
+    if (num < K) {
+      maxd2 = a.rmax * a.rmax;
+    } else {
+      double lm = 0.0;
+      for (int s = lane; s < num; s += 64) {
+        double d = (double)fetch_d2(s);
+        lm = d > lm ? d : lm;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        double t = __shfl_xor(lm, o, 64);
+        lm = t > lm ? t : lm;
+      }
+      if (lm > maxd2) maxd2 = lm;
+    }
+    if (a.mode == KNN_MODE_IRRADIANCE) {
+      for (int s = lane; s < num; s += 64) {
+        uint32_t e = a.map.rgbe[fetch_id(s)];
+        uint32_t ee = e >> 24;
+        if (ee) {
+          double inv = ldexp(1.0, (int)ee - 128 - 8);
+          o0 += (double)(e & 255u) * inv;
+          o1 += (double)((e >> 8) & 255u) * inv;
+          o2 += (double)((e >> 16) & 255u) * inv;
+        }
+      }
+      o0 = wave_sum(o0); o1 = wave_sum(o1); o2 = wave_sum(o2);
+      double den = kPi * maxd2;
+      o0 /= den; o1 /= den; o2 /= den;
+    } else {
+      const QShade &sh = a.qshade[qi];
+      uint32_t meta = __float_as_uint(qp.w);
+      uint32_t sign = meta & 3u;
+      const DMaterial &m = a.mats[meta >> 2];
+      double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
+      double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
+      bool spec = (m.flags & MF_SPECULAR) || (m.n < 0);
+      double c1 = 1.0, c2 = 1.0, tw = 0;
+      if (a.filter == 1) c1 = 1.0 / (a.fk * sqrt(maxd2));
+      else if (a.filter == 2) {
+        c1 = pow(2.7182818284590452354, -a.fb);
+        c2 = 1.0 / (2.0 * maxd2);
+      }
+      for (int s = lane; s < num; s += 64) {
+        uint32_t id = fetch_id(s);
+        double d2 = (double)fetch_d2(s);
+        uint32_t dcode = __float_as_uint(a.map.pos4[4 * (int64_t)id + 3]) & 0xffffu;
+        double ix = a.lut[3 * dcode], iy = a.lut[3 * dcode + 1], iz = a.lut[3 * dcode + 2];
+        double perp = N0 * ix + N1 * iy + N2 * iz;
+        if ((sign == 2u && perp < 0) || (sign == 1u && perp > 0)) continue;
+        uint32_t e = a.map.rgbe[id];
+        uint32_t ee = e >> 24;
+        double inv = ee ? ldexp(1.0, (int)ee - 128 - 8) : 0.0;
+        double p0 = ee ? (double)(e & 255u) * inv : 0.0;
+        double p1 = ee ? (double)((e >> 8) & 255u) * inv : 0.0;
+        double p2 = ee ? (double)((e >> 16) & 255u) * inv : 0.0;
+        double ca = E0 * -ix + E1 * -iy + E2 * -iz;
+        if (ca < 0) ca = 0;
+        double ap = fabs(perp);
+        double pw = spec ? pow(ca, m.n) : 0.0;
+        p0 *= ap * m.kd[0] + pw * m.ks[0];
+        p1 *= ap * m.kd[1] + pw * m.ks[1];
+        p2 *= ap * m.kd[2] + pw * m.ks[2];
+        if (a.filter == 1) {
+          double f = (1.0 - c1 * sqrt(d2));
+          p0 *= f; p1 *= f; p2 *= f;
+        } else if (a.filter == 2) {
+          double w = (1.0 - (1.0 - pow(c1, c2 * d2)) / (1.0 - c1));
+          p0 *= w; p1 *= w; p2 *= w;
+          tw += w;
+        }
+        o0 += p0; o1 += p1; o2 += p2;
+      }
+      o0 = wave_sum(o0); o1 = wave_sum(o1); o2 = wave_sum(o2);
+      if (a.filter == 2) tw = wave_sum(tw);
+      bool ok = true;
+      if (a.filter == 0 && maxd2 > 0) {
+        double den = kPi * maxd2;
+        o0 /= den; o1 /= den; o2 /= den;
+      } else if (a.filter == 1 && maxd2 > 0) {
+        double den = (1.0 - 2.0 / 3.0 / a.fk) * kPi * maxd2;
+        o0 /= den; o1 /= den; o2 /= den;
+      } else if (a.filter == 2 && tw > 0 && maxd2 > 0) {
+        double sc = a.fa * (num / tw) / (kPi * maxd2);
+        o0 *= sc; o1 *= sc; o2 *= sc;
+      } else {
+        ok = false;
+      }
+      if (ok) {
+        o0 *= sh.w[0]; o1 *= sh.w[1]; o2 *= sh.w[2];
+      } else {
+        o0 = o1 = o2 = 0;
+      }
+    }
+  }
+  if (lane == 0) {
+    a.out[3 * qi] = o0;
+    a.out[3 * qi + 1] = o1;
+    a.out[3 * qi + 2] = o2;
+    if (a.out_n) a.out_n[qi] = num;
+    if (a.out_maxd2) a.out_maxd2[qi] = (num > 0) ? (float)maxd2 : 0.0f;
+  }
+}
+
+template <int CAP, int LB, bool PROF, bool FUSE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FUSE ? 6 : 1)))
+void knn_wave_kernel(KnnArgs a) {
   __shared__ uint64_t buf[CAP];
   __shared__ uint32_t hist[256];
   __shared__ uint32_t stk[64];   // traversal stack: pending far children and their box distances
@@ -180,7 +297,15 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
     int64_t qi = a.perm ? (int64_t)a.perm[qg] : qg;
     float4 qp = a.qpos[qi];
     if (__float_as_uint(qp.w) == QMETA_NONE) {  // empty deterministic slot
-      if (lane == 0) a.list_n[qi] = 0;
+      if (FUSE) {
+        if (lane == 0) {
+          a.out[3 * qi] = a.out[3 * qi + 1] = a.out[3 * qi + 2] = 0.0;
+          if (a.out_n) a.out_n[qi] = 0;
+          if (a.out_maxd2) a.out_maxd2[qi] = 0.0f;
+        }
+      } else if (lane == 0 && a.list_n) {
+        a.list_n[qi] = 0;
+      }
       continue;
     }
     float qx = ffirst(qp.x), qy = ffirst(qp.y), qz = ffirst(qp.z);
@@ -347,6 +472,10 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
       for (int o = 32; o > 0; o >>= 1) km = fmaxf(km, __shfl_xor(km, o, 64));
       if (lane == 0)
         a.out_dk[qi] = (num < K) ? INFINITY : __double2float_ru(sqrt((double)km * (1.0 + 1e-5)));
+    } else if (FUSE) {
+      // the estimate straight from the K best keys in LDS (no list round trip through HBM)
+      wave_estimate(a, qi, qp, num, [&](int s) { return (uint32_t)buf[s]; },
+                    [&](int s) { return __uint_as_float((uint32_t)(buf[s] >> 32)); });
     } else {
       for (int s = lane; s < K; s += 64) {
         bool v = s < num;
@@ -368,123 +497,18 @@ __global__ __launch_bounds__(64) void knn_wave_kernel(KnnArgs a) {
   }
 }
 
-// EstimateRadiance / EstimateIrradiance (photon_utils.cpp:72-162, 209-246) over the K-best
-// lists written by knn_wave_kernel: one wave per query, photons spread over the lanes,
-// fp64 partial sums reduced across the wave. Split from the search so the search kernel
-// keeps a small register footprint (50 VGPRs: 7 waves/SIMD instead of 3).
+// the estimate over the K-best lists written by knn_wave_kernel in list mode (kept for
+// GI_WAVE_FUSE=0 and the group kernel); split from the search so the search kernel keeps a
+// small register footprint
 __global__ __launch_bounds__(64) void knn_list_estimate_kernel(KnnArgs a) {
-  const int lane = threadIdx.x;
   const int K = a.K;
   for (int64_t qq = blockIdx.x; qq < a.nq; qq += gridDim.x) {
     int64_t qg = a.q0 + qq;
     int64_t qi = a.perm ? (int64_t)a.perm[qg] : qg;
     float4 qp = a.qpos[qi];
-    int num = a.list_n[qi];
-    double maxd2 = kEps;
-    double o0 = 0, o1 = 0, o2 = 0;
-    if (num > 0) {
-      if (num < K) {
-        maxd2 = a.rmax * a.rmax;
-      } else {
-        double lm = 0.0;
-        for (int s = lane; s < num; s += 64) {
-          double d = (double)a.list_d2[qi * K + s];
-          lm = d > lm ? d : lm;
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          double t = __shfl_xor(lm, o, 64);
-          lm = t > lm ? t : lm;
-        }
-        if (lm > maxd2) maxd2 = lm;
-      }
-      if (a.mode == KNN_MODE_IRRADIANCE) {
-        for (int s = lane; s < num; s += 64) {
-          uint32_t e = a.map.rgbe[(uint32_t)a.list_idx[qi * K + s]];
-          uint32_t ee = e >> 24;
-          if (ee) {
-            double inv = ldexp(1.0, (int)ee - 128 - 8);
-            o0 += (double)(e & 255u) * inv;
-            o1 += (double)((e >> 8) & 255u) * inv;
-            o2 += (double)((e >> 16) & 255u) * inv;
-          }
-        }
-        o0 = wave_sum(o0); o1 = wave_sum(o1); o2 = wave_sum(o2);
-        double den = kPi * maxd2;
-        o0 /= den; o1 /= den; o2 /= den;
-      } else {
-        const QShade &sh = a.qshade[qi];
-        uint32_t meta = __float_as_uint(qp.w);
-        uint32_t sign = meta & 3u;
-        const DMaterial &m = a.mats[meta >> 2];
-        double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
-        double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
-        bool spec = (m.flags & MF_SPECULAR) || (m.n < 0);
-        double c1 = 1.0, c2 = 1.0, tw = 0;
-        if (a.filter == 1) c1 = 1.0 / (a.fk * sqrt(maxd2));
-        else if (a.filter == 2) {
-          c1 = pow(2.7182818284590452354, -a.fb);
-          c2 = 1.0 / (2.0 * maxd2);
-        }
-        for (int s = lane; s < num; s += 64) {
-          uint32_t id = (uint32_t)a.list_idx[qi * K + s];
-          double d2 = (double)a.list_d2[qi * K + s];
-          uint32_t dcode = __float_as_uint(a.map.pos4[4 * (int64_t)id + 3]) & 0xffffu;
-          double ix = a.lut[3 * dcode], iy = a.lut[3 * dcode + 1], iz = a.lut[3 * dcode + 2];
-          double perp = N0 * ix + N1 * iy + N2 * iz;
-          if ((sign == 2u && perp < 0) || (sign == 1u && perp > 0)) continue;
-          uint32_t e = a.map.rgbe[id];
-          uint32_t ee = e >> 24;
-          double inv = ee ? ldexp(1.0, (int)ee - 128 - 8) : 0.0;
-          double p0 = ee ? (double)(e & 255u) * inv : 0.0;
-          double p1 = ee ? (double)((e >> 8) & 255u) * inv : 0.0;
-          double p2 = ee ? (double)((e >> 16) & 255u) * inv : 0.0;
-          double ca = E0 * -ix + E1 * -iy + E2 * -iz;
-          if (ca < 0) ca = 0;
-          double ap = fabs(perp);
-          double pw = spec ? pow(ca, m.n) : 0.0;
-          p0 *= ap * m.kd[0] + pw * m.ks[0];
-          p1 *= ap * m.kd[1] + pw * m.ks[1];
-          p2 *= ap * m.kd[2] + pw * m.ks[2];
-          if (a.filter == 1) {
-            double f = (1.0 - c1 * sqrt(d2));
-            p0 *= f; p1 *= f; p2 *= f;
-          } else if (a.filter == 2) {
-            double w = (1.0 - (1.0 - pow(c1, c2 * d2)) / (1.0 - c1));
-            p0 *= w; p1 *= w; p2 *= w;
-            tw += w;
-          }
-          o0 += p0; o1 += p1; o2 += p2;
-        }
-        o0 = wave_sum(o0); o1 = wave_sum(o1); o2 = wave_sum(o2);
-        if (a.filter == 2) tw = wave_sum(tw);
-        bool ok = true;
-        if (a.filter == 0 && maxd2 > 0) {
-          double den = kPi * maxd2;
-          o0 /= den; o1 /= den; o2 /= den;
-        } else if (a.filter == 1 && maxd2 > 0) {
-          double den = (1.0 - 2.0 / 3.0 / a.fk) * kPi * maxd2;
-          o0 /= den; o1 /= den; o2 /= den;
-        } else if (a.filter == 2 && tw > 0 && maxd2 > 0) {
-          double sc = a.fa * (num / tw) / (kPi * maxd2);
-          o0 *= sc; o1 *= sc; o2 *= sc;
-        } else {
-          ok = false;
-        }
-        if (ok) {
-          o0 *= sh.w[0]; o1 *= sh.w[1]; o2 *= sh.w[2];
-        } else {
-          o0 = o1 = o2 = 0;
-        }
-      }
-    }
-    if (lane == 0) {
-      a.out[3 * qi] = o0;
-      a.out[3 * qi + 1] = o1;
-      a.out[3 * qi + 2] = o2;
-      if (a.out_n) a.out_n[qi] = num;
-      if (a.out_maxd2) a.out_maxd2[qi] = (num > 0) ? (float)maxd2 : 0.0f;
-    }
+    wave_estimate(a, qi, qp, a.list_n[qi],
+                  [&](int s) { return (uint32_t)a.list_idx[qi * K + s]; },
+                  [&](int s) { return a.list_d2[qi * K + s]; });
   }
 }
 
@@ -951,19 +975,19 @@ void launch_list_estimate(const KnnArgs &a, hipStream_t st) {
   knn_list_estimate_kernel<<<(unsigned)grid, 64, 0, st>>>(a);
 }
 
-template <bool PROF>
+template <bool PROF, bool FUSE>
 bool wave_launch(const KnnArgs &a, int need, int lb, unsigned grid, hipStream_t st) {
   if (lb <= 1) {
-    if (need <= 128) knn_wave_kernel<128, 1, PROF><<<grid, 64, 0, st>>>(a);
-    else if (need <= 256) knn_wave_kernel<256, 1, PROF><<<grid, 64, 0, st>>>(a);
-    else if (need <= 512) knn_wave_kernel<512, 1, PROF><<<grid, 64, 0, st>>>(a);
-    else if (need <= 1024) knn_wave_kernel<1024, 1, PROF><<<grid, 64, 0, st>>>(a);
+    if (need <= 128) knn_wave_kernel<128, 1, PROF, FUSE><<<grid, 64, 0, st>>>(a);
+    else if (need <= 256) knn_wave_kernel<256, 1, PROF, FUSE><<<grid, 64, 0, st>>>(a);
+    else if (need <= 512) knn_wave_kernel<512, 1, PROF, FUSE><<<grid, 64, 0, st>>>(a);
+    else if (need <= 1024) knn_wave_kernel<1024, 1, PROF, FUSE><<<grid, 64, 0, st>>>(a);
     else return false;
   } else {
-    if (need <= 128) knn_wave_kernel<128, 8, PROF><<<grid, 64, 0, st>>>(a);
-    else if (need <= 256) knn_wave_kernel<256, 8, PROF><<<grid, 64, 0, st>>>(a);
-    else if (need <= 512) knn_wave_kernel<512, 8, PROF><<<grid, 64, 0, st>>>(a);
-    else if (need <= 1024) knn_wave_kernel<1024, 8, PROF><<<grid, 64, 0, st>>>(a);
+    if (need <= 128) knn_wave_kernel<128, 8, PROF, FUSE><<<grid, 64, 0, st>>>(a);
+    else if (need <= 256) knn_wave_kernel<256, 8, PROF, FUSE><<<grid, 64, 0, st>>>(a);
+    else if (need <= 512) knn_wave_kernel<512, 8, PROF, FUSE><<<grid, 64, 0, st>>>(a);
+    else if (need <= 1024) knn_wave_kernel<1024, 8, PROF, FUSE><<<grid, 64, 0, st>>>(a);
     else return false;
   }
   return true;
@@ -976,11 +1000,19 @@ bool launch_knn_wave(const KnnArgs &a, int cap_mul, hipStream_t st) {
   // photon batches of 64 prefetched per leaf (GI_WAVE_LB: 1 or 8); GI_KNN_DBG & 16 selects the
   // instance with phase cycle counters
   static const int lb = getenv("GI_WAVE_LB") ? atoi(getenv("GI_WAVE_LB")) : 1;
-  bool ok = (a.dbg & 16) ? wave_launch<true>(a, need, lb, (unsigned)grid, st)
-                         : wave_launch<false>(a, need, lb, (unsigned)grid, st);
+  // the estimate fused into the search (GI_WAVE_FUSE=0: lists + knn_list_estimate_kernel)
+  static const bool fuse = getenv("GI_WAVE_FUSE") ? atoi(getenv("GI_WAVE_FUSE")) != 0 : true;
+  const bool est = a.mode != KNN_MODE_LIST && a.mode != KNN_MODE_DK;
+  bool ok;
+  if (est && fuse) {
+    ok = (a.dbg & 16) ? wave_launch<true, true>(a, need, lb, (unsigned)grid, st)
+                      : wave_launch<false, true>(a, need, lb, (unsigned)grid, st);
+  } else {
+    ok = (a.dbg & 16) ? wave_launch<true, false>(a, need, lb, (unsigned)grid, st)
+                      : wave_launch<false, false>(a, need, lb, (unsigned)grid, st);
+  }
   if (!ok) return false;
-  if (a.mode != KNN_MODE_LIST && a.mode != KNN_MODE_DK)
-    knn_list_estimate_kernel<<<(unsigned)grid, 64, 0, st>>>(a);
+  if (est && !fuse) knn_list_estimate_kernel<<<(unsigned)grid, 64, 0, st>>>(a);
   return true;
 }
 

@@ -567,11 +567,12 @@ struct Counts {  // per-thread -v counters (render.cpp:26-32)
 };
 
 // RayIlluminationTest, illumination_utils.cpp:16-31 (Q13 distance equality)
+template <uint32_t KINDS = KINDS_ALL>
 __device__ __noinline__ bool illum_test(const SceneView &S, V p_scene, V p_light, Counts &cnt) {
   double unocc = dist(p_light, p_scene);
   V d = normalize(p_scene - p_light);
   Hit h;
-  double l = scene_intersect(S, p_light, d, h) ? dist(p_light, h.p) : kInf;
+  double l = scene_intersect<KINDS>(S, p_light, d, h) ? dist(p_light, h.p) : kInf;
   cnt.shadow++;
   return fabs(l - unocc) < kEps;
 }
@@ -613,6 +614,7 @@ GI_HD V light_sample_point(const DLight &L, Rng &rng) {
 
 // ComputeAreaLightReflection / ComputeRectLightReflection, illumination_utils.cpp:91-417
 // (Q1: the whole accumulated colour is scaled by the shadow hit rate)
+template <uint32_t KINDS = KINDS_ALL>
 __device__ __noinline__ void soft_light(const SceneView &S, const DLight &L, C3 &color,
                                         const DMaterial &m, V eye, V p, V nrm, int nls, int nes,
                                         Rng &rng, Counts &cnt) {
@@ -625,7 +627,7 @@ __device__ __noinline__ void soft_light(const SceneView &S, const DLight &L, C3 
     int hits = 0;
     for (int i = 0; i < nls; i++) {
       V sp = light_sample_point(L, rng);
-      if (illum_test(S, p, sp, cnt)) {
+      if (illum_test<KINDS>(S, p, sp, cnt)) {
         hits++;
         double I = L.intensity;
         double dd = dist(p, sp);
@@ -649,7 +651,7 @@ __device__ __noinline__ void soft_light(const SceneView &S, const DLight &L, C3 
     V Vv = normalize(eye - p);
     for (int i = 0; i < n2; i++) {
       V sp = light_sample_point(L, rng);
-      if (illum_test(S, p, sp, cnt)) {
+      if (illum_test<KINDS>(S, p, sp, cnt)) {
         hits++;
         double I = L.intensity;
         double dd = dist(p, sp);
@@ -673,7 +675,7 @@ __device__ __noinline__ void soft_light(const SceneView &S, const DLight &L, C3 
   int hits = 0;
   for (int i = 0; i < nes; i++) {
     V sp = light_sample_point(L, rng);
-    if (illum_test(S, p, sp, cnt)) hits++;
+    if (illum_test<KINDS>(S, p, sp, cnt)) hits++;
   }
   tot_h += hits;
   tot_s += nes;
@@ -772,6 +774,7 @@ __device__ __noinline__ C3 light_reflection(const DLight &L, const DMaterial &m,
 }
 
 // ComputeIllumination, illumination_utils.cpp:425-494
+template <uint32_t KINDS = KINDS_ALL>
 __device__ __noinline__ void compute_illumination(const SceneView &S, const Flags &F, C3 &color,
                                                   const DLight &L, const DMaterial &m, V eye,
                                                   V p, V nrm, double ct, bool inMC, Rng &rng,
@@ -792,16 +795,17 @@ __device__ __noinline__ void compute_illumination(const SceneView &S, const Flag
     if (!F.soft_shadows) {
       pol = ld3(L.pos) + kEps * ld3(L.dir);
     } else {
-      soft_light(S, L, color, m, eye, p, nrm, nls, nes, rng, cnt);
+      soft_light<KINDS>(S, L, color, m, eye, p, nrm, nls, nes, rng, cnt);
       return;
     }
   }
   double side = dot(nrm, pol - p);
   if ((side > 0 && ct < 0) || (side < 0 && ct > 0)) return;
-  if (illum_test(S, p, pol, cnt)) color += light_reflection(L, m, eye, p, nrm, nls, rng);
+  if (illum_test<KINDS>(S, p, pol, cnt)) color += light_reflection(L, m, eye, p, nrm, nls, rng);
 }
 
 // DirectIllumination, raytracer.cpp:18-44
+template <uint32_t KINDS = KINDS_ALL>
 __device__ __noinline__ void direct_illumination(const SceneView &S, const Flags &F, V p, V nrm,
                                                  V eye, C3 &color, const DMaterial &m, double ct,
                                                  bool inMC, Rng &rng, Counts &cnt) {
@@ -813,7 +817,7 @@ __device__ __noinline__ void direct_illumination(const SceneView &S, const Flags
       if (li == -1) emit = false;
       continue;
     }
-    compute_illumination(S, F, color, L, m, eye, p, nrm, ct, inMC, rng, cnt);
+    compute_illumination<KINDS>(S, F, color, L, m, eye, p, nrm, ct, inMC, rng, cnt);
   }
   if (emit) color += ldc(m.e);
 }

@@ -225,6 +225,7 @@ struct gi_ctx {
   int ind_waves = 3;              // indirect-path kernel occupancy target (waves per SIMD)
   DBuf ind_cont, ind_ncont;       // indirect paths that continue past their first bounce
   bool split_ind = true;          // continuation queue for indirect paths (else one loop per lane)
+  double ind_frac = 0.25;         // continuation queue size, as a fraction of its worst case
   // render scratch
   DBuf spawn, npaths, path_off, nmc, mc_off, nind, ind_off, base, pixels, rgbf, rgb8, gheap_d2, gheap_idx, qcount, stats_bak;
   DBuf qpos[2], qshade[2], qkey[2], qout[2];
@@ -783,15 +784,11 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     a.total_ind = totals[2];
     HIPCHK(c, c->base.ensure((size_t)total_paths * 24));
     a.base = c->base.as<double>();
-    if (a.split_ind && a.total_ind > 0) {
-      // stripe s takes the appends of waves w with w % IND_QS == s (<= 64 paths per wave)
-      uint64_t nwaves = ((uint64_t)a.total_ind + 63) / 64;
-      a.ind_cap_s = (uint32_t)(64 * ((nwaves + IND_QS - 1) / IND_QS));
-      HIPCHK(c, c->ind_cont.ensure((size_t)IND_QS * a.ind_cap_s * sizeof(IndCont)));
-      HIPCHK(c, c->ind_ncont.ensure(IND_QS * 32 * 4));
-      a.ind_cont = c->ind_cont.as<IndCont>();
-      a.ind_ncont = c->ind_ncont.as<uint32_t>();
-    }
+    // continuation queue: stripe s takes the appends of waves w with w % IND_QS == s (<= 64
+    // paths per wave, so `full` entries per stripe can never overflow); sized from the fill
+    // seen so far (c->ind_frac of full), re-run with more room when a stripe overflows
+    const uint64_t ind_full = 64 * ((((uint64_t)a.total_ind + 63) / 64 + IND_QS - 1) / IND_QS);
+    if (a.split_ind && a.total_ind > 0) HIPCHK(c, c->ind_ncont.ensure(IND_QS * 32 * 4));
     // single Monte Carlo pass; grow the query lists and re-run on overflow
     uint32_t nq[2] = {0, 0};
     HIPCHK(c, hipMemcpyAsync(c->stats_bak.p, c->d_stats.p, ST_BYTES,
@@ -811,13 +808,29 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
         a.qkey[l] = c->qkey[l].as<uint64_t>();
         a.qcap[l] = (uint32_t)std::min<size_t>(cap, 0xFFFFFFF0u);
       }
+      if (a.split_ind && a.total_ind > 0) {
+        uint64_t cap_s = std::min<uint64_t>(ind_full, 64 * ((uint64_t)(ind_full * c->ind_frac) / 64 + 1));
+        HIPCHK(c, c->ind_cont.ensure((size_t)IND_QS * cap_s * sizeof(IndCont)));
+        a.ind_cap_s = (uint32_t)cap_s;
+        a.ind_cont = c->ind_cont.as<IndCont>();
+        a.ind_ncont = c->ind_ncont.as<uint32_t>();
+      }
       a.qcount = c->qcount.as<uint32_t>();
       HIPCHK(c, hipMemcpyAsync(c->qcount.p, qbase, 8, hipMemcpyHostToDevice, c->stream));
       launch_path(a, c->stream);
       HIPCHK(c, hipGetLastError());
       HIPCHK(c, hipMemcpyAsync(nq, c->qcount.p, 8, hipMemcpyDeviceToHost, c->stream));
+      uint32_t fills[IND_QS * 32];
+      if (a.split_ind && a.total_ind > 0)
+        HIPCHK(c, hipMemcpyAsync(fills, c->ind_ncont.p, sizeof fills, hipMemcpyDeviceToHost, c->stream));
       HIPCHK(c, hipStreamSynchronize(c->stream));
       bool ok = nq[0] <= a.qcap[0] && nq[1] <= a.qcap[1];
+      if (a.split_ind && a.total_ind > 0) {
+        uint32_t mx = 0;
+        for (int q = 0; q < IND_QS; q++) mx = std::max(mx, fills[q * 32]);
+        c->ind_frac = std::max(c->ind_frac, std::min(1.0, 1.25 * mx / (double)ind_full));
+        if (mx > a.ind_cap_s) ok = false;
+      }
       for (int l = 0; l < 2; l++)
         c->qcap_hint[l] = std::max<size_t>(c->qcap_hint[l], (size_t)(nq[l] * 1.25) + 1024);
       if (ok) break;
@@ -926,6 +939,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_IND_WAVES")) c->ind_waves = std::max(1, atoi(s));
   if (const char *s = getenv("GI_SPLIT_IND")) c->split_ind = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_DK")) c->use_dk = atoi(s) != 0;
+  if (const char *s = getenv("GI_IND_FRAC")) c->ind_frac = std::min(1.0, std::max(1e-6, atof(s)));
   if (const char *s = getenv("GI_SORT_QUERIES")) c->sort_queries = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_KERNEL")) c->knn_kernel_kind = atoi(s);
   *out = c;

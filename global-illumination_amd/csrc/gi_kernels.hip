@@ -272,9 +272,10 @@ __device__ __forceinline__ bool diffuse_only(const DMaterial &m) {
 }
 
 // one full iteration: trace, then shade (background on a miss)
+template <uint32_t KINDS = KINDS_ALL>
 __device__ __forceinline__ bool ind_bounce(PathCtx &P, V &org, V &dir, Rng &rng, C3 W, C3 &tw) {
   Hit h;
-  if (!scene_intersect(*P.S, org, dir, h)) {
+  if (!scene_intersect<KINDS>(*P.S, org, dir, h)) {
     P.base += W * (tw * ldc(P.S->background));
     return false;
   }
@@ -283,17 +284,20 @@ __device__ __forceinline__ bool ind_bounce(PathCtx &P, V &org, V &dir, Rng &rng,
 }
 
 // MonteCarlo_IndirectSample, montecarlo.cpp:177-305 (W = outer weight of this path)
+template <uint32_t KINDS = KINDS_ALL>
 __device__ __forceinline__ void mc_indirect_body(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
   C3 tw = rgb(1, 1, 1);
   for (int iter = 0; iter < P.F->max_monte_depth; iter++)
-    if (!ind_bounce(P, org, dir, rng, W, tw)) break;
+    if (!ind_bounce<KINDS>(P, org, dir, rng, W, tw)) break;
 }
 
+template <uint32_t KINDS = KINDS_ALL>
 __device__ __noinline__ void mc_indirect(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
-  mc_indirect_body(P, org, dir, rng, W);
+  mc_indirect_body<KINDS>(P, org, dir, rng, W);
 }
 
 // MonteCarlo_PathTrace, montecarlo.cpp:16-171
+template <uint32_t KINDS = KINDS_ALL>
 __device__ __noinline__ void mc_path(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
   const SceneView &S = *P.S;
   const Flags &F = *P.F;
@@ -302,7 +306,7 @@ __device__ __noinline__ void mc_path(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
   V ray_start = org;
   for (int iter = 0; iter < F.max_monte_depth; iter++) {
     Hit h;
-    if (!scene_intersect(S, org, dir, h)) {
+    if (!scene_intersect<KINDS>(S, org, dir, h)) {
       P.base += W * (tw * ldc(S.background));
       break;
     }
@@ -313,7 +317,7 @@ __device__ __noinline__ void mc_path(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
     V view = normalize(h.p - ray_start);
     double ct = dot(h.n, -view);
     if (m.flags & (MF_DIFFUSE | MF_SPECULAR))
-      direct_illumination(S, F, h.p, h.n, ray_start, cb, m, ct, true, rng, P.cnt);
+      direct_illumination<KINDS>(S, F, h.p, h.n, ray_start, cb, m, ct, true, rng, P.cnt);
     if (F.caustic && (m.flags & MF_DIFFUSE)) {
       V ex = reflective_bounce(h.n, view, ct);
       put_query(P, 1, h.p, h.n, ex, ct, h.mat, W * tw);
@@ -336,7 +340,7 @@ __device__ __noinline__ void mc_path(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
       if (F.indirect) {
         // IndirectIllumination(inMC): one sample continuing this path's stream
         V s2 = diffuse_sample(h.n, ct, rng);
-        mc_indirect(P, h.p + s2 * kEps, s2, rng, W * ((kd * kd * tw) / pd));
+        mc_indirect<KINDS>(P, h.p + s2 * kEps, s2, rng, W * ((kd * kd * tw) / pd));
         P.cnt.indirect++;
       } else if (F.fast_global) {
         V ex = reflective_bounce(h.n, view, ct);
@@ -498,8 +502,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void i
           uint32_t base = 0;
           if (lane == leader) base = atomicAdd(&a.ind_ncont[stripe * 32], (uint32_t)__popcll(act));
           base = (uint32_t)__shfl((int)base, leader, 64);
-          IndCont &q = a.ind_cont[(size_t)stripe * a.ind_cap_s + base +
-                                  (uint32_t)__popcll(act & ((1ull << lane) - 1ull))];
+          const uint32_t slot = base + (uint32_t)__popcll(act & ((1ull << lane) - 1ull));
+          // a full stripe drops the entry; the host sees the fill and re-runs the batch
+          IndCont &q = a.ind_cont[(size_t)stripe * a.ind_cap_s + (slot < a.ind_cap_s ? slot : 0)];
+          if (slot < a.ind_cap_s) {
           q.org[0] = org.x; q.org[1] = org.y; q.org[2] = org.z;
           q.hp[0] = h.p.x; q.hp[1] = h.p.y; q.hp[2] = h.p.z;
           q.hn[0] = h.n.x; q.hn[1] = h.n.y; q.hn[2] = h.n.z;
@@ -511,6 +517,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void i
           q.pslot = (uint32_t)pslot;
           q.qslot = (uint32_t)P.fixed[0];
           q.mat = h.mat;
+          }
         }
       }
     }
@@ -529,10 +536,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void i
 // the queued indirect paths (shading of the first hit, then MonteCarlo_IndirectSample's loop
 // from iteration 1 on), one per thread: block b serves stripe b % IND_QS, striding over its fill
 // (the fills are known only on the device)
+template <uint32_t KINDS>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void ind_cont_kernel(RenderArgs a) {
   const uint32_t stripe = blockIdx.x % IND_QS, part = blockIdx.x / IND_QS;
   const uint32_t parts = gridDim.x / IND_QS;
-  const uint32_t n = a.ind_ncont[stripe * 32];
+  const uint32_t n = min(a.ind_ncont[stripe * 32], a.ind_cap_s);
   Counts tot = {0, 0, 0, 0, 0, 0};
   const uint32_t rounds = (n + parts * blockDim.x - 1) / (parts * blockDim.x);
   for (uint32_t r = 0; r < rounds; r++) {
@@ -554,7 +562,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void i
     h.mat = q.mat;
     if (ind_shade<false>(P, h, org, dir, rng, W, tw))
       for (int iter = 1; iter < a.F.max_monte_depth; iter++)
-        if (!ind_bounce(P, org, dir, rng, W, tw)) break;
+        if (!ind_bounce<KINDS>(P, org, dir, rng, W, tw)) break;
     if (P.fixed[0] >= 0) put_none(a, 0, P.fixed[0]);
     a.base[3 * (int64_t)q.g] = P.base.r;
     a.base[3 * (int64_t)q.g + 1] = P.base.g;
@@ -566,6 +574,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void i
 }
 
 // TransmissiveIllumination / SpecularIllumination sample (raytracer.cpp:47-109)
+template <uint32_t KINDS>
 __global__ __launch_bounds__(128) void mc_kernel(RenderArgs a) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   Counts cnt = {0, 0, 0, 0, 0, 0};
@@ -590,7 +599,7 @@ __global__ __launch_bounds__(128) void mc_kernel(RenderArgs a) {
       V ex = transmissive_bounce(F.ir_air, n, view, ct, m.ir);
       C3 tw = (1.0 - R) * ldc(m.kt);
       V sb = F.distrib_trans ? specular_sample(ex, m.n, ct, rng) : ex;
-      mc_path(P, p + sb * kEps, sb, rng, tw / (double)sp.n_t);
+      mc_path<KINDS>(P, p + sb * kEps, sb, rng, tw / (double)sp.n_t);
       P.cnt.trans++;
     } else {
       s -= sp.n_t;
@@ -598,7 +607,7 @@ __global__ __launch_bounds__(128) void mc_kernel(RenderArgs a) {
       V ex = reflective_bounce(n, view, ct);
       C3 tw = ldc(m.kt) * R + ldc(m.ks);
       V sb = F.distrib_spec ? specular_sample(ex, m.n, ct, rng) : ex;
-      mc_path(P, p + sb * kEps, sb, rng, tw / (double)sp.n_s);
+      mc_path<KINDS>(P, p + sb * kEps, sb, rng, tw / (double)sp.n_s);
       P.cnt.spec++;
     }
     a.base[3 * g] = P.base.r;
@@ -1268,9 +1277,18 @@ void launch_path(const RenderArgs &a, hipStream_t st) {
     else if ((a.S.kinds & ~KINDS_POLY) == 0) launch_ind<KINDS_POLY>(a, g, st);
     else launch_ind<KINDS_ALL>(a, g, st);
     // continuations: 32 blocks per stripe stride over its fill
-    if (a.split_ind) ind_cont_kernel<<<IND_QS * 32, 128, 0, st>>>(a);
+    if (a.split_ind) {
+      if ((a.S.kinds & ~KINDS_TRI_SPHERE) == 0) ind_cont_kernel<KINDS_TRI_SPHERE><<<IND_QS * 32, 128, 0, st>>>(a);
+      else if ((a.S.kinds & ~KINDS_POLY) == 0) ind_cont_kernel<KINDS_POLY><<<IND_QS * 32, 128, 0, st>>>(a);
+      else ind_cont_kernel<KINDS_ALL><<<IND_QS * 32, 128, 0, st>>>(a);
+    }
   }
-  if (a.total_mc > 0) mc_kernel<<<nblk(a.total_mc, 128), 128, 0, st>>>(a);
+  if (a.total_mc > 0) {
+    unsigned g = nblk(a.total_mc, 128);
+    if ((a.S.kinds & ~KINDS_TRI_SPHERE) == 0) mc_kernel<KINDS_TRI_SPHERE><<<g, 128, 0, st>>>(a);
+    else if ((a.S.kinds & ~KINDS_POLY) == 0) mc_kernel<KINDS_POLY><<<g, 128, 0, st>>>(a);
+    else mc_kernel<KINDS_ALL><<<g, 128, 0, st>>>(a);
+  }
 }
 void launch_reduce(const RenderArgs &a, hipStream_t st) {
   reduce_kernel<<<nblk(a.npix, 64), 64, 0, st>>>(a);

@@ -179,15 +179,20 @@ def test_cylinder_and_line_cases_match_oracle(renderer):
 def test_indirect_continuation_queue_is_exact(name, extra):
     """ind_kernel's continuation queue (GI_SPLIT_IND=1, default) only regroups the bounces of
     MonteCarlo_IndirectSample (montecarlo.cpp:177-305) that follow a glass/mirror hit: the f32
-    image and every -v counter equal the one-loop-per-lane kernel's (GI_SPLIT_IND=0)."""
+    image and every -v counter equal the one-loop-per-lane kernel's (GI_SPLIT_IND=0), also when
+    the queue starts far too small (GI_IND_FRAC) and the batch is re-run with more room."""
     args = [scene(name), "/tmp/x.png", "-resolution", "32", "32", "-aa", "1", "-it", "32",
             "-tt", "8", "-st", "8", "-seed", "4"] + extra
     p, sc, _o, w, h, aa, real = gi_amd.ParseArgs(args)
     out = []
-    old = os.environ.get("GI_SPLIT_IND")
+    keys = ("GI_SPLIT_IND", "GI_IND_FRAC")
+    old = {k: os.environ.get(k) for k in keys}
     try:
-        for v in ("0", "1"):
-            os.environ["GI_SPLIT_IND"] = v
+        for env in ({"GI_SPLIT_IND": "0"}, {"GI_SPLIT_IND": "1"},
+                    {"GI_SPLIT_IND": "1", "GI_IND_FRAC": "0.00001"}):
+            for k in keys:
+                os.environ.pop(k, None)
+            os.environ.update(env)
             r = gi_amd.Renderer(0, p)
             try:
                 r.ReadScene(sc, real)
@@ -197,12 +202,14 @@ def test_indirect_continuation_queue_is_exact(name, extra):
             finally:
                 r.close()
     finally:
-        if old is None:
-            os.environ.pop("GI_SPLIT_IND", None)
-        else:
-            os.environ["GI_SPLIT_IND"] = old
-    np.testing.assert_array_equal(out[0][0], out[1][0])
-    for k in ("screen_rays", "shadow_rays", "monte_carlo_rays", "transmissive_samples",
-              "specular_samples", "indirect_samples", "caustic_samples", "knn_queries"):
-        assert out[0][1][k] == out[1][1][k], k
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    for other in out[1:]:
+        np.testing.assert_array_equal(out[0][0], other[0])
+        for k in ("screen_rays", "shadow_rays", "monte_carlo_rays", "transmissive_samples",
+                  "specular_samples", "indirect_samples", "caustic_samples", "knn_queries"):
+            assert out[0][1][k] == other[1][k], k
     assert out[1][1]["transmissive_samples"] > 0

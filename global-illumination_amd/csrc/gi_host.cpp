@@ -838,23 +838,34 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
       HIPCHK(c, hipMemcpyAsync(c->d_stats.p, c->stats_bak.p, ST_BYTES,
                                hipMemcpyDeviceToDevice, c->stream));
     }
-    // photon-map estimates, then a deterministic (key) order of each list for the reduction
+    // photon-map estimates, then a deterministic order of each list for the reduction. The
+    // deterministic slots (a primary's own query at slot b; indirect path t's at qind_base + t)
+    // are already in (primary, slot-in-primary) order; only the Monte Carlo appends after
+    // qbase[l] are key-sorted and indexed per primary (CSR over the sorted keys).
     for (int l = 0; l < 2; l++) {
       a.nq[l] = nq[l];
-      if (!nq[l]) {  // no queries: empty segments for every primary
-        HIPCHK(c, c->qseg[l].ensure((size_t)(nprim + 1) * 4));
-        HIPCHK(c, hipMemsetAsync(c->qseg[l].p, 0, (size_t)(nprim + 1) * 4, c->stream));
-        a.qseg[l] = c->qseg[l].as<uint32_t>();
-        continue;
+      a.qapp[l] = qbase[l];
+      a.qout[l] = nullptr;
+      if (nq[l]) {
+        HIPCHK(c, c->qout[l].ensure((size_t)nq[l] * 24));
+        a.qout[l] = c->qout[l].as<double>();
+        if (!c->map_valid[l]) {
+          HIPCHK(c, hipMemsetAsync(c->qout[l].p, 0, (size_t)nq[l] * 24, c->stream));
+        } else {
+          int rc = knn_list(c, l, a.qpos[l], a.qshade[l], nq[l], c->qout[l].as<double>(),
+                            rs ? &knn_ms[l] : nullptr);
+          if (rc) return rc;
+          launches[l]++;
+        }
       }
-      HIPCHK(c, c->qout[l].ensure((size_t)nq[l] * 24));
-      if (!c->map_valid[l]) {
-        HIPCHK(c, hipMemsetAsync(c->qout[l].p, 0, (size_t)nq[l] * 24, c->stream));
-      } else {
-        int rc = knn_list(c, l, a.qpos[l], a.qshade[l], nq[l], c->qout[l].as<double>(),
-                          rs ? &knn_ms[l] : nullptr);
-        if (rc) return rc;
-        launches[l]++;
+      HIPCHK(c, c->qseg[l].ensure((size_t)(nprim + 1) * 4));
+      a.qseg[l] = c->qseg[l].as<uint32_t>();
+      const int64_t napp = (int64_t)nq[l] - (int64_t)qbase[l];
+      if (napp <= 0) {  // no appends: empty segments for every primary
+        HIPCHK(c, hipMemsetAsync(c->qseg[l].p, 0, (size_t)(nprim + 1) * 4, c->stream));
+        a.skey[l] = nullptr;
+        a.sslot[l] = nullptr;
+        continue;
       }
       uint64_t *sk = nullptr;
       uint32_t *ss = nullptr;
@@ -862,14 +873,11 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
       int bits = 32;
       while (bits < 64 && ((uint64_t)nprim >> (bits - 32)) != 0) bits++;
       if (bits < 64) bits++;  // room for the empty-slot key's top bits
-      HIPCHK(c, key_order(a.qkey[l], nq[l], bits, c->keysort[l], &sk, &ss, c->stream));
+      HIPCHK(c, key_order(a.qkey[l] + qbase[l], napp, bits, c->keysort[l], &sk, &ss, c->stream));
       a.skey[l] = sk;
-      a.sslot[l] = ss;
-      HIPCHK(c, c->qseg[l].ensure((size_t)(nprim + 1) * 4));
-      a.qseg[l] = c->qseg[l].as<uint32_t>();
-      launch_segments(sk, nq[l], (uint32_t)nprim, a.qseg[l], c->stream);
+      a.sslot[l] = ss;  // slots relative to qbase[l]
+      launch_segments(sk, (uint32_t)napp, (uint32_t)nprim, a.qseg[l], c->stream);
       HIPCHK(c, hipGetLastError());
-      a.qout[l] = c->qout[l].as<double>();
     }
     a.rgbf = c->rgbf.as<float>();
     a.rgb8 = c->rgb8.as<uint8_t>();

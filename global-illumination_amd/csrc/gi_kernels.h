@@ -99,9 +99,10 @@ struct RenderArgs {
   uint64_t *qkey[2];
   uint32_t *qcount;     // [2] device counters
   uint32_t qcap[2];
-  const uint64_t *skey[2];    // sorted keys
-  const uint32_t *sslot[2];   // slot of each sorted key
-  uint32_t *qseg[2];          // [nprim + 1]: sorted queries of primary b are [qseg[b], qseg[b+1])
+  uint32_t qapp[2];           // first Monte Carlo (appended) slot of each list
+  const uint64_t *skey[2];    // sorted keys of the appended slots [qapp, nq)
+  const uint32_t *sslot[2];   // slot - qapp of each sorted key
+  uint32_t *qseg[2];          // [nprim + 1]: sorted appends of primary b are [qseg[b], qseg[b+1])
   uint32_t nq[2];
   double *base;         // [total_paths * 3]
   const double *qout[2];       // k-NN contributions per slot

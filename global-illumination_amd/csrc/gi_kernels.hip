@@ -1021,14 +1021,22 @@ __global__ __launch_bounds__(64) void reduce_kernel(RenderArgs a) {
         c1 += a.base[3 * (int64_t)g + 1];
         c2 += a.base[3 * (int64_t)g + 2];
       }
+      // each list in (primary, slot in primary, query in path) order: the primary's own
+      // query (slot b), its Monte Carlo paths' appends (sorted), then (global list) its
+      // indirect paths' queries (slots qind_base + t, in path order); empty slots skipped
       for (int l = 0; l < 2; l++) {
+        if (!a.qout[l]) continue;
+        auto add = [&](int64_t sl) {
+          if (a.qkey[l][sl] == ~0ull) return;
+          c0 += a.qout[l][3 * sl];
+          c1 += a.qout[l][3 * sl + 1];
+          c2 += a.qout[l][3 * sl + 2];
+        };
+        add(b);
         uint32_t q0 = a.qseg[l][b], q1 = a.qseg[l][b + 1];
-        for (uint32_t q = q0; q < q1; q++) {
-          uint32_t sl = a.sslot[l][q];
-          c0 += a.qout[l][3 * (int64_t)sl];
-          c1 += a.qout[l][3 * (int64_t)sl + 1];
-          c2 += a.qout[l][3 * (int64_t)sl + 2];
-        }
+        for (uint32_t q = q0; q < q1; q++) add((int64_t)a.qapp[l] + a.sslot[l][q]);
+        if (l == 0)
+          for (uint32_t t = a.ind_off[b]; t < a.ind_off[b + 1]; t++) add(a.qind_base + t);
       }
       s0 += c0; s1 += c1; s2 += c2;
     }

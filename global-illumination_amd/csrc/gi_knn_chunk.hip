@@ -436,15 +436,33 @@ __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, flo
         c1 = pow(2.7182818284590452354, -a.fb);
         c2 = 1.0 / (2.0 * maxd2);
       }
-      for (int s = 0; s < num; s++) {
-        uint32_t slot = slot_at(s);
-        float4 p = cpos[slot];
+      // photons in groups of EB: the LDS slot reads and direction-LUT loads of a group are
+      // issued before its arithmetic (one memory round trip per group, not per photon); the
+      // sums still run in photon order
+      constexpr int EB = 4;
+      for (int s0 = 0; s0 < num; s0 += EB) {
+      float4 pg[EB];
+      uint32_t eg[EB];
+      double lg[EB][3];
+#pragma unroll
+      for (int u = 0; u < EB; u++) {
+        uint32_t slot = slot_at(s0 + u < num ? s0 + u : s0);
+        pg[u] = cpos[slot];
+        eg[u] = crgbe[slot];
+        uint32_t dc = __float_as_uint(pg[u].w) & 0xffffu;
+        lg[u][0] = a.lut[3 * dc];
+        lg[u][1] = a.lut[3 * dc + 1];
+        lg[u][2] = a.lut[3 * dc + 2];
+      }
+#pragma unroll
+      for (int u = 0; u < EB; u++) {
+        if (s0 + u >= num) break;
+        float4 p = pg[u];
         double d2 = (double)metric(qp.x, qp.y, qp.z, p);
-        uint32_t dcode = __float_as_uint(p.w) & 0xffffu;
-        double ix = a.lut[3 * dcode], iy = a.lut[3 * dcode + 1], iz = a.lut[3 * dcode + 2];
+        double ix = lg[u][0], iy = lg[u][1], iz = lg[u][2];
         double perp = N0 * ix + N1 * iy + N2 * iz;
         if ((sign == 2u && perp < 0) || (sign == 1u && perp > 0)) continue;
-        uint32_t e = crgbe[slot];
+        uint32_t e = eg[u];
         uint32_t ee = e >> 24;
         double inv = ee ? ldexp(1.0, (int)ee - 128 - 8) : 0.0;
         double p0 = ee ? (double)(e & 255u) * inv : 0.0;
@@ -466,6 +484,7 @@ __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, flo
           tw += w;
         }
         o0 += p0; o1 += p1; o2 += p2;
+      }
       }
       bool ok = true;
       if (a.filter == 0 && maxd2 > 0) {
@@ -600,19 +619,31 @@ void knn_chunk_lane_kernel(KnnArgs a) {
     // ---- 3. lane select. State: every valid candidate with d2 < A is kept; `need` more come
     //         from the bracket [A, B] (smallest (d2, kd index) first); above B nothing is kept.
     float A = 0.0f, B = query_lim2(a, G, qx, qy, qz);
+    // Bin origin of the first pass: d_K(q) >= d_K(c) - |q - c|, so the K-th key most likely
+    // lies in [O, B] with O = (d_K(c) - |q - c|)^2; bin 0 takes everything below O. The
+    // origin only shapes the bins (any O < B gives the same result), so no rounding margin.
+    float O = A;
+    if (G.dkc >= 0.0) {
+      double ex = (double)qx - G.cx, ey = (double)qy - G.cy, ez = (double)qz - G.cz;
+      double lo = G.dkc - sqrt(ex * ex + ey * ey + ez * ez);
+      if (lo > 0.0) {
+        float o = (float)(lo * lo);
+        if (o < B) O = o;
+      }
+    }
     int need = (act && K > 0) ? K : 0;
     int mode = need > 0 ? 1 : 0;  // 1 counting, 2 bracket resolved by the collect pass, 0 done
     if (!(a.dbg & 4)) {
       for (int pass = 0; pass < LS_PASSES && __ballot(mode == 1); pass++) {
         if (P.on) P.c[8]++;
         const bool on = mode == 1;
-        const float sc = 16.0f / (B - A);
+        const float sc = 16.0f / (B - O);
         uint64_t w0 = 0, w1 = 0;  // 16 bins x 8-bit counters
 #pragma unroll 4
         for (uint32_t s = 0; s < count; s++) {
           float d2 = metric(qx, qy, qz, cpos[s]);
           bool mem = on && d2 >= A && d2 <= B;
-          uint32_t b = bin16(d2, A, sc);
+          uint32_t b = bin16(d2, O, sc);
           uint64_t inc = mem ? (1ull << ((b & 7u) << 3)) : 0ull;
           if (b & 8u) w1 += inc;
           else w0 += inc;
@@ -634,8 +665,8 @@ void knn_chunk_lane_kernel(KnnArgs a) {
             mode = 0;
           } else {
             need -= (int)before;
-            float nA = (bs == 0) ? A : bin_floor(bs, A, B, sc);
-            float nB = (bs == 15) ? B : next_down(bin_floor(bs + 1, A, B, sc));
+            float nA = (bs == 0) ? A : bin_floor(bs, O, B, sc);
+            float nB = (bs == 15) ? B : next_down(bin_floor(bs + 1, O, B, sc));
             if (cb == (uint32_t)need) {
               A = next_up(nB);
               need = 0;
@@ -648,6 +679,7 @@ void knn_chunk_lane_kernel(KnnArgs a) {
             }
           }
         }
+        O = A;
       }
     }
     // queries the counting passes did not resolve go to the exact per-lane kernel

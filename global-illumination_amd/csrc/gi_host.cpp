@@ -212,6 +212,8 @@ struct gi_ctx {
   int leaf_size[2] = {64, 256};  // photons per kd leaf, per map (global, caustic)
   int wave_cap_mul = 1;
   int chunk_cap = 256;            // chunk kernel: LDS candidate capacity per 64-query chunk
+  int chunk_cap_big = 512;        // large-K chunk kernel: the same (384 or 512)
+  int chunk_minsub_big = 64;      // large-K chunk kernel: overflowing chunks retried down to this (64: none, measured best)
   int chunk_minsub = 64;          // chunk kernel: overflowing chunks retried down to this group size (64: no retry, measured best)
   hipEvent_t ev2 = nullptr;       // chunk kernel / fallback split
   double fb_ms[2] = {0, 0};       // fallback time and queries per map (since the last reset)
@@ -558,13 +560,67 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
   // auto (-1): chunk kernel with lane select (+ per-lane fallback) for K <= 64, the per-lane
   // kernel for list mode, one query per wave beyond (measured)
   int kind = c->knn_kernel_kind;
-  int auto_kind = (k.K <= 64) ? (k.mode == KNN_MODE_LIST ? 3 : 7) : 1;
+  int auto_kind = (k.K <= 64) ? (k.mode == KNN_MODE_LIST ? 3 : 7)
+                              : ((k.mode == KNN_MODE_LIST || !c->use_dk) ? 1 : 8);
   if (kind < 0) kind = auto_kind;
   // an override that cannot serve this map's K (or list mode) falls back to the automatic one
+  if (kind == 8 && (k.mode == KNN_MODE_LIST || k.mode == KNN_MODE_DK || k.K + 64 > 1024 || !c->use_dk))
+    kind = auto_kind == 8 ? 1 : auto_kind;
   if (((kind >= 5 && kind <= 7) && (k.K > 64 || k.mode == KNN_MODE_LIST)) || (kind == 3 && k.K > 128) ||
       (kind == 0 && k.K > 64))
     kind = auto_kind;
   if (kind == 2 && (int64_t)k.K * 64 * 8 > 80 * 1024) kind = 1;
+  if (kind == 8) {
+    // large-K chunk kernel, then the query-per-wave kernel on what it hands over
+    int rc = ensure_dk(c, k);
+    if (rc) return rc;
+    int64_t chunks = (nq + 63) / 64;
+    int64_t grid = knn_chunk_grid(nq);
+    uint32_t cap_s = (uint32_t)(64 * ((chunks + grid - 1) / grid) * ((grid + FB_QS - 1) / FB_QS));
+    HIPCHK(c, c->fb_list.ensure((size_t)FB_QS * cap_s * 4));
+    HIPCHK(c, c->fb_dense.ensure((size_t)nq * 4 + 4));
+    HIPCHK(c, c->fb_count.ensure(FB_QS * 32 * 4));
+    HIPCHK(c, hipMemsetAsync(c->fb_count.p, 0, FB_QS * 32 * 4, c->stream));
+    k.nq = nq;
+    k.q0 = 0;
+    k.fb_list = c->fb_list.as<uint32_t>();
+    k.fb_count = c->fb_count.as<uint32_t>();
+    k.fb_cap_s = cap_s;
+    k.chunk_minsub = c->chunk_minsub_big;
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    if (!launch_knn_chunk_big(k, c->chunk_cap_big, c->stream))
+      return fail(c, GI_ERR_ARG, "k-NN launch: large-K chunk kernel unavailable");
+    HIPCHK(c, hipGetLastError());
+    uint32_t *dense = c->fb_dense.as<uint32_t>();
+    launch_fb_compact(k.fb_list, k.fb_count, cap_s, dense, dense + nq, c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->ev2, c->stream));
+    uint32_t nfb = 0;
+    HIPCHK(c, hipMemcpyAsync(&nfb, dense + nq, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->fb_total += nfb;
+    if (nfb) {
+      KnnArgs f = k;
+      f.perm = dense;
+      f.nq = nfb;
+      f.q0 = 0;
+      if (!launch_knn_wave(f, c->wave_cap_mul, c->stream))
+        return fail(c, GI_ERR_ARG, "k-NN launch: unsupported estimate size for this kernel");
+      HIPCHK(c, hipGetLastError());
+    }
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    if (ms) {
+      HIPCHK(c, hipEventSynchronize(c->ev1));
+      float t = 0, tf = 0;
+      HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+      HIPCHK(c, hipEventElapsedTime(&tf, c->ev2, c->ev1));
+      *ms += t;
+      int mi = k.stat_off ? 1 : 0;
+      c->fb_ms[mi] += tf;
+      c->fb_q[mi] += nfb;
+    }
+    return GI_OK;
+  }
   if ((kind >= 5 && kind <= 7) && k.K <= 64 && k.mode != KNN_MODE_LIST) {
     // chunk kernel, then the per-lane kernel on the chunks that overflowed its LDS gather
     // striped fallback list (gi_knn_chunk.hip to_fallback): block b -> stripe b % FB_QS, at most
@@ -938,6 +994,8 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_WAVE_CAP_MUL")) c->wave_cap_mul = std::max(1, atoi(s));
   if (const char *s = getenv("GI_SEL_SLACK")) c->sel_slack = std::max(1, atoi(s));
   if (const char *s = getenv("GI_CHUNK_CAP")) c->chunk_cap = std::max(64, atoi(s));
+  if (const char *s = getenv("GI_CHUNK_CAP_BIG")) c->chunk_cap_big = atoi(s) <= 384 ? 384 : 512;
+  if (const char *s = getenv("GI_CHUNK_MINSUB_BIG")) c->chunk_minsub_big = std::min(64, std::max(1, atoi(s)));
   if (const char *s = getenv("GI_CHUNK_MINSUB")) c->chunk_minsub = std::min(64, std::max(1, atoi(s)));
   if (const char *s = getenv("GI_KNN_GHEAP")) c->force_gheap = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_QPL")) c->knn_qpl = std::max(1, atoi(s));

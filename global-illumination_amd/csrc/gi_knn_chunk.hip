@@ -258,7 +258,24 @@ __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, b
     }
     int leaf = node - L;
     int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
-    if (s1 - s0 >= K && K <= 64) {
+    if (a.map.dk) {
+      // d_K(c) <= |c - p| + d_K(p) for every photon p of c's leaf (per-photon bounds, KdView::dk)
+      double best = INFINITY;
+      for (int64_t b = s0; b < s1; b += 64) {
+        int64_t ii = b + lane;
+        if (ii < s1) {
+          float dkp = a.map.dk[ii];
+          if (dkp < INFINITY)
+            best = fmin(best, sqrt((double)metric(cx, cy, cz, pos[ii]) * (1.0 + 1e-5)) + (double)dkp);
+        }
+      }
+      best = -wmax(-best);
+      if (best < INFINITY) {
+        G.dkc = best * (1.0 + 1e-6) + 1e-12;
+        double ub = G.dkc + rho * (1.0 + 1e-6) + 1e-12;
+        if (ub < U) U = ub;
+      }
+    } else if (s1 - s0 >= K && K <= 64) {
       float d2 = INFINITY;
       if (s0 + lane < s1) d2 = metric(cx, cy, cz, pos[s0 + lane]);
       float sorted = wave_sort(d2, lane);
@@ -758,6 +775,202 @@ void knn_chunk_lane_kernel(KnnArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// lane select for large K (the caustic map's 225): no per-query slot lists in LDS. The kept
+// candidates of a query are a bitmask over the chunk's LDS slots (NW words per lane), and the
+// bin counters are 16 bits wide (a chunk may gather more than 255 photons). The chunk bound
+// comes from the per-photon K-th distance bounds (KdView::dk), which the host requires here.
+// Overflowing chunks and unresolved queries go to the one-query-per-wave kernel.
+// ---------------------------------------------------------------------------------------------
+template <int CAPC, bool PROF>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
+void knn_chunk_big_kernel(KnnArgs a) {
+  constexpr int NW = CAPC / 32;
+  __shared__ float4 cpos[CAPC];
+  __shared__ uint32_t cidx[CAPC];
+  __shared__ uint32_t crgbe[CAPC];
+  __shared__ uint32_t hist[4];       // unused by the dk bound (chunk_bound_gather signature)
+  __shared__ uint32_t stk[64];
+  __shared__ uint32_t selw[NW * 64];  // kept-candidate bitmask, [word][lane]
+  const int lane = threadIdx.x;
+  const int K = a.K;
+  const int minsub = a.chunk_minsub > 0 ? a.chunk_minsub : 64;
+  uint64_t st_q = 0, st_found = 0, st_vis = 0;
+  ChunkProf P;
+  P.on = PROF;
+  P.t = 0;
+  for (int i = 0; i < 10; i++) P.c[i] = 0;
+  for (int64_t chunk = blockIdx.x; chunk * 64 < a.nq; chunk += gridDim.x) {
+    bool valid;
+    int64_t qi;
+    float4 qp;
+    chunk_load_query(a, chunk, lane, valid, qi, qp);
+    uint64_t vmask = __ballot(valid);
+    if (vmask == 0) continue;
+    // an overflowing chunk is retried as halves, quarters, ... down to minsub queries (the
+    // query-per-wave fallback costs several times a lane-select query even at 1/8 occupancy)
+    uint64_t pending = vmask;
+    for (int sub = 64; sub >= minsub && pending; sub >>= 1) {
+    for (int g0 = 0; g0 < 64; g0 += sub) {
+    const uint64_t gm = (sub == 64) ? ~0ull : (((1ull << sub) - 1ull) << g0);
+    if (!(pending & gm)) continue;
+    const bool act = valid && ((gm >> lane) & 1ull);
+    if (P.on) P.t = clock64();
+    ChunkGeom G;
+    chunk_bound_gather<CAPC>(a, lane, act, qp, CAPC, cpos, cidx, crgbe, hist, stk, G, P);
+    __syncthreads();
+    if (G.overflow || G.dkc < 0.0) continue;
+    pending &= ~gm;
+    const uint32_t count = G.count;
+    const float qx = qp.x, qy = qp.y, qz = qp.z;
+    // ---- lane select (see knn_chunk_lane_kernel), 16 bins x 16-bit counters
+    float A = 0.0f, B = query_lim2(a, G, qx, qy, qz);
+    float O = A;
+    {
+      double ex = (double)qx - G.cx, ey = (double)qy - G.cy, ez = (double)qz - G.cz;
+      double lo = G.dkc - sqrt(ex * ex + ey * ey + ez * ez);
+      if (lo > 0.0) {
+        float o = (float)(lo * lo);
+        if (o < B) O = o;
+      }
+    }
+    int need = (act && K > 0) ? K : 0;
+    int mode = need > 0 ? 1 : 0;
+    for (int pass = 0; pass < LS_PASSES && __ballot(mode == 1); pass++) {
+      if (P.on) P.c[8]++;
+      const bool on = mode == 1;
+      const float sc = 16.0f / (B - O);
+      uint64_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+#pragma unroll 4
+      for (uint32_t s = 0; s < count; s++) {
+        float d2 = metric(qx, qy, qz, cpos[s]);
+        bool mem = on && d2 >= A && d2 <= B;
+        uint32_t b = bin16(d2, O, sc);
+        uint64_t inc = mem ? (1ull << ((b & 3u) << 4)) : 0ull;
+        uint32_t g = b >> 2;
+        w0 += (g == 0) ? inc : 0ull;
+        w1 += (g == 1) ? inc : 0ull;
+        w2 += (g == 2) ? inc : 0ull;
+        w3 += (g == 3) ? inc : 0ull;
+      }
+      if (on) {
+        uint32_t before = 0, bs = 16, cb = 0;
+#pragma unroll
+        for (int b = 0; b < 16; b++) {
+          uint64_t w = (b < 4) ? w0 : (b < 8) ? w1 : (b < 12) ? w2 : w3;
+          uint32_t c = (uint32_t)((w >> (16 * (b & 3))) & 0xffffull);
+          if (bs == 16) {
+            if (before + c >= (uint32_t)need) { bs = (uint32_t)b; cb = c; }
+            else before += c;
+          }
+        }
+        if (bs == 16) {
+          A = next_up(B);
+          need = 0;
+          mode = 0;
+        } else {
+          need -= (int)before;
+          float nA = (bs == 0) ? A : bin_floor(bs, O, B, sc);
+          float nB = (bs == 15) ? B : next_down(bin_floor(bs + 1, O, B, sc));
+          if (cb == (uint32_t)need) {
+            A = next_up(nB);
+            need = 0;
+            mode = 0;
+          } else {
+            A = nA;
+            B = nB;
+            if (cb <= (uint32_t)LS_BR) mode = 2;
+            else if (!(B > A)) mode = 3;
+          }
+        }
+      }
+      O = A;
+    }
+    const bool fb = mode == 1 || mode == 3;
+    uint64_t fbm = __ballot(fb);
+    if (fbm) {
+      to_fallback(a, fbm, fb, qi, lane);
+      if (P.on) P.c[9] += (uint64_t)__popcll(fbm);
+    }
+    const bool col = act && !fb;
+    // ---- collect: bitmask of the candidates below A, plus the bracket's kept ones
+    int n = 0;
+    float km = 0.0f;
+    uint64_t br[LS_BR];
+#pragma unroll
+    for (int i = 0; i < LS_BR; i++) br[i] = ~0ull;
+    const bool inb_on = col && need > 0;
+    for (uint32_t w0 = 0; w0 < (count + 31) / 32; w0++) {
+      uint32_t bits = 0;
+#pragma unroll 4
+      for (uint32_t j = 0; j < 32; j++) {
+        uint32_t s = w0 * 32 + j;
+        if (s >= count) break;
+        float d2 = metric(qx, qy, qz, cpos[s]);
+        if (col && d2 < A) {
+          bits |= 1u << j;
+          km = fmaxf(km, d2);
+        }
+        if (inb_on && d2 >= A && d2 <= B) {
+#pragma unroll
+          for (int i = LS_BR - 1; i > 0; i--) br[i] = br[i - 1];
+          br[0] = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)s;
+        }
+      }
+      selw[w0 * 64 + lane] = bits;
+      n += __popc(bits);
+    }
+    if (inb_on) {
+      uint64_t fk[LS_BR];
+      uint32_t sl[LS_BR];
+#pragma unroll
+      for (int i = 0; i < LS_BR; i++) {
+        sl[i] = (uint32_t)br[i];
+        fk[i] = (br[i] == ~0ull) ? ~0ull : ((br[i] & 0xffffffff00000000ull) | (uint64_t)cidx[sl[i] % CAPC]);
+      }
+#pragma unroll
+      for (int i = 0; i < LS_BR; i++)
+#pragma unroll
+        for (int j = 0; j + 1 < LS_BR - i; j++)
+          if (fk[j + 1] < fk[j]) {
+            uint64_t t = fk[j]; fk[j] = fk[j + 1]; fk[j + 1] = t;
+            uint32_t u = sl[j]; sl[j] = sl[j + 1]; sl[j + 1] = u;
+          }
+#pragma unroll
+      for (int i = 0; i < LS_BR; i++)
+        if (i < need) {
+          selw[(sl[i] / 32) * 64 + lane] |= 1u << (sl[i] % 32);
+          n++;
+          km = fmaxf(km, __uint_as_float((uint32_t)(fk[i] >> 32)));
+        }
+    }
+    P.lap(2);
+    // ---- estimate: the lane walks its bitmask in slot order
+    if (col) {
+      uint32_t wi = 0, bits = selw[lane];
+      chunk_estimate(a, qi, qp, n, km, cpos, crgbe, [&](int) -> uint32_t {
+        while (!bits && wi + 1 < (uint32_t)NW) {
+          wi++;
+          bits = selw[wi * 64 + lane];
+        }
+        if (!bits) return 0u;
+        uint32_t b = (uint32_t)__ffs(bits) - 1u;
+        bits &= bits - 1u;
+        return wi * 32u + b;
+      });
+      st_q += 1;
+      st_found += (uint64_t)n;
+      st_vis += count;
+    }
+    __syncthreads();
+    P.lap(3);
+    }
+    }
+    if (pending) to_fallback(a, pending, valid && ((pending >> lane) & 1ull), qi, lane);
+  }
+  chunk_flush_stats(a, P, st_q, st_found, st_vis);
+}
+
+// ---------------------------------------------------------------------------------------------
 // wave select: one query at a time across the wave
 // ---------------------------------------------------------------------------------------------
 template <int CAPC, int WPE>
@@ -1008,6 +1221,22 @@ void launch_fb_compact(const uint32_t *list, const uint32_t *count, uint32_t cap
 unsigned knn_chunk_grid(int64_t nq) {
   int64_t chunks = (nq + 63) / 64;
   return (unsigned)(chunks < (1 << 17) ? chunks : (1 << 17));
+}
+
+// large-K chunk kernel (needs a.map.dk); cap = LDS candidates per chunk (384 or 512)
+bool launch_knn_chunk_big(const KnnArgs &a, int cap, hipStream_t st) {
+  if (a.nq == 0) return true;
+  if (a.mode == KNN_MODE_LIST || a.mode == KNN_MODE_DK || !a.map.dk) return false;
+  unsigned grid = knn_chunk_grid(a.nq);
+  bool prof = (a.dbg & 16) != 0;
+  if (cap <= 384) {
+    if (prof) knn_chunk_big_kernel<384, true><<<grid, 64, 0, st>>>(a);
+    else knn_chunk_big_kernel<384, false><<<grid, 64, 0, st>>>(a);
+  } else {
+    if (prof) knn_chunk_big_kernel<512, true><<<grid, 64, 0, st>>>(a);
+    else knn_chunk_big_kernel<512, false><<<grid, 64, 0, st>>>(a);
+  }
+  return true;
 }
 
 // variant: 0 wave select, 1 per-lane heaps, 2 lane select

@@ -5,7 +5,8 @@ The variants are chosen when a context is created (gi_host.cpp tuning environmen
 GI_KNN_KERNEL 0 = per-lane LDS heap, 1 = query per wave, 2 = packet, 3 = per-lane with
 batched inserts, 4 = L-lane groups (GI_GROUP_LANES). Each must return the oracle's k-NN sets
 exactly: the fp32 metric is shared, and only photons tied at the k-th distance may differ.
-GI_KNN_KERNEL 5-7 = chunk kernels; GI_CHUNK_MINSUB sets how far an overflowing chunk is split
+GI_KNN_KERNEL 5-7 = chunk kernels, 8 = the large-K chunk kernel (bitmask selection, bounds from
+per-photon K-th distances); GI_CHUNK_MINSUB sets how far an overflowing chunk is split
 (1 = down to single queries, 64 = straight to the per-lane fallback). GI_KNN_DK=0 turns off the
 wave kernel's start from per-photon K-th distance bounds (on by default).
 It must also return its EstimateRadiance within rtol 1e-10 (fp64 sums in a different order).
@@ -40,6 +41,10 @@ VARIANTS = [
     {"GI_KNN_KERNEL": "7", "GI_LEAF_SIZE": "50"},
     {"GI_KNN_KERNEL": "7", "GI_CHUNK_MINSUB": "1"},
     {"GI_KNN_KERNEL": "7", "GI_CHUNK_MINSUB": "64"},
+    {"GI_KNN_KERNEL": "8"},
+    {"GI_KNN_KERNEL": "8", "GI_CHUNK_CAP_BIG": "384", "GI_LEAF_SIZE": "128"},
+    {"GI_KNN_KERNEL": "8", "GI_CHUNK_MINSUB_BIG": "1"},
+    {"GI_KNN_KERNEL": "8", "GI_CHUNK_MINSUB_BIG": "64"},
 ]
 
 
@@ -115,7 +120,7 @@ def clustered_queries(n, seed, k, r, filt):
 
 
 @pytest.mark.parametrize("env", VARIANTS, ids=lambda e: "-".join(f"{k[3:]}{v}" for k, v in e.items()))
-@pytest.mark.parametrize("filt,k,r", [(DISK, 50, 2.5), (CONE, 32, 0.05)])
+@pytest.mark.parametrize("filt,k,r", [(DISK, 50, 2.5), (CONE, 32, 0.05), (DISK, 225, 0.225)])
 def test_variant_dense_queries(env, filt, k, r):
     r_ = make_renderer(env)
     try:

@@ -116,6 +116,7 @@ struct SceneView {
   const DLight *lights;
   int32_t nnodes, nelems, nlights;
   uint32_t kinds;  // bit k set: the scene holds shapes of ShapeKind k
+  int32_t hard_lights;  // every light is a point, spot or directional light
   double radius;
   double centroid[3];
   double ambient[3];
@@ -568,13 +569,17 @@ struct Counts {  // per-thread -v counters (render.cpp:26-32)
 
 // RayIlluminationTest, illumination_utils.cpp:16-31 (Q13 distance equality)
 template <uint32_t KINDS = KINDS_ALL>
-__device__ __noinline__ bool illum_test(const SceneView &S, V p_scene, V p_light, Counts &cnt) {
+__device__ __forceinline__ bool illum_test_inl(const SceneView &S, V p_scene, V p_light, Counts &cnt) {
   double unocc = dist(p_light, p_scene);
   V d = normalize(p_scene - p_light);
   Hit h;
   double l = scene_intersect<KINDS>(S, p_light, d, h) ? dist(p_light, h.p) : kInf;
   cnt.shadow++;
   return fabs(l - unocc) < kEps;
+}
+template <uint32_t KINDS = KINDS_ALL>
+__device__ __noinline__ bool illum_test(const SceneView &S, V p_scene, V p_light, Counts &cnt) {
+  return illum_test_inl<KINDS>(S, p_scene, p_light, cnt);
 }
 
 // TestLightIntersection, illumination_utils.cpp:35-84
@@ -685,9 +690,9 @@ __device__ __noinline__ void soft_light(const SceneView &S, const DLight &L, C3 
 // Light::Reflection: point/spot (R3PointLight.cpp:213-244, IntensityAtPoint :111-121,
 // R3SpotLight.cpp:105-115), directional (R3DirectionalLight.cpp:134-166), area/rect without
 // shadows (R3AreaLight.cpp:122-330, R3RectLight.cpp:150-340)
-__device__ __noinline__ C3 light_reflection(const DLight &L, const DMaterial &m, V eye, V p,
-                                            V nrm, int max_samples, Rng &rng) {
-  if (!L.active) return rgb(0, 0, 0);
+// the point/spot/directional part (no sampling), also inlined by the hard-light path
+__device__ __forceinline__ C3 light_reflection_hard(const DLight &L, const DMaterial &m, V eye, V p,
+                                                    V nrm) {
   C3 Dc = ldc(m.kd), Sc = ldc(m.ks), Ic = ldc(L.color);
   double s = m.n;
   if (L.kind == LK_POINT || L.kind == LK_SPOT) {
@@ -723,6 +728,16 @@ __device__ __noinline__ C3 light_reflection(const DLight &L, const DMaterial &m,
     if (isPos(VR)) o += (I * pow(VR, s) * Sc * Ic);
     return o;
   }
+  return rgb(0, 0, 0);
+}
+
+__device__ __noinline__ C3 light_reflection(const DLight &L, const DMaterial &m, V eye, V p,
+                                            V nrm, int max_samples, Rng &rng) {
+  if (!L.active) return rgb(0, 0, 0);
+  if (L.kind == LK_POINT || L.kind == LK_SPOT || L.kind == LK_DIR)
+    return light_reflection_hard(L, m, eye, p, nrm);
+  C3 Dc = ldc(m.kd), Sc = ldc(m.ks), Ic = ldc(L.color);
+  double s = m.n;
   bool area = (L.kind == LK_AREA);
   V dirn = ld3(L.dir), center = ld3(L.pos);
   if (dot(dirn, p - center) < 0) return rgb(0, 0, 0);
@@ -820,6 +835,31 @@ __device__ __noinline__ void direct_illumination(const SceneView &S, const Flags
     compute_illumination<KINDS>(S, F, color, L, m, eye, p, nrm, ct, inMC, rng, cnt);
   }
   if (emit) color += ldc(m.e);
+}
+
+// DirectIllumination for scenes whose lights are all point/spot/directional (SceneView::
+// hard_lights), inlined: no light sampling, so no calls, and the caller's registers are not
+// spilled around them. Same operations as direct_illumination -> compute_illumination ->
+// illum_test / light_reflection for those light kinds (TestLightIntersection is 0 for them).
+template <uint32_t KINDS = KINDS_ALL>
+__device__ __forceinline__ void direct_illumination_hard(const SceneView &S, const Flags &F, V p,
+                                                         V nrm, V eye, C3 &color,
+                                                         const DMaterial &m, double ct, bool inMC,
+                                                         Counts &cnt) {
+  bool shadows = F.shadows && (!inMC || (F.recursive_shadows && inMC));
+  for (int k = 0; k < S.nlights; k++) {
+    const DLight &L = S.lights[k];
+    if (!shadows) {
+      if (L.active) color += light_reflection_hard(L, m, eye, p, nrm);
+      continue;
+    }
+    V pol = (L.kind == LK_DIR) ? p - ld3(L.dir) * S.radius * 3.0 : ld3(L.pos);
+    double side = dot(nrm, pol - p);
+    if ((side > 0 && ct < 0) || (side < 0 && ct > 0)) continue;
+    if (illum_test_inl<KINDS>(S, p, pol, cnt) && L.active)
+      color += light_reflection_hard(L, m, eye, p, nrm);
+  }
+  color += ldc(m.e);
 }
 
 }  // namespace gi

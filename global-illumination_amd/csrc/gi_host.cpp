@@ -226,6 +226,7 @@ struct gi_ctx {
   int heap_arity = 4;             // per-lane kernel: d-ary heap
   int ind_waves = 3;              // indirect-path kernel occupancy target (waves per SIMD)
   DBuf ind_cont, ind_ncont;       // indirect paths that continue past their first bounce
+  DBuf mc_cont, mc_ncont;         // Monte Carlo paths' indirect sub-paths
   bool split_ind = true;          // continuation queue for indirect paths (else one loop per lane)
   double ind_frac = 0.25;         // continuation queue size, as a fraction of its worst case
   // render scratch
@@ -301,6 +302,9 @@ SceneView make_view(gi_ctx *c) {
   S.nlights = (int)H.lights.size();
   S.kinds = 0;
   for (const DShape &sh : H.shapes) S.kinds |= 1u << sh.kind;
+  S.hard_lights = 1;
+  for (const DLight &L : H.lights)
+    if (L.kind == LK_AREA || L.kind == LK_RECT) S.hard_lights = 0;
   S.radius = H.radius;
   for (int i = 0; i < 3; i++) {
     S.centroid[i] = H.centroid[i];
@@ -845,6 +849,15 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     // seen so far (c->ind_frac of full), re-run with more room when a stripe overflows
     const uint64_t ind_full = 64 * ((((uint64_t)a.total_ind + 63) / 64 + IND_QS - 1) / IND_QS);
     if (a.split_ind && a.total_ind > 0) HIPCHK(c, c->ind_ncont.ensure(IND_QS * 32 * 4));
+    // Monte Carlo paths' indirect sub-paths: at most one per path, so the worst case is sized
+    if (a.split_ind && a.total_mc > 0 && a.F.indirect) {
+      const uint64_t full = 64 * ((((uint64_t)a.total_mc + 63) / 64 + IND_QS - 1) / IND_QS);
+      HIPCHK(c, c->mc_cont.ensure((size_t)IND_QS * full * sizeof(IndCont)));
+      HIPCHK(c, c->mc_ncont.ensure(IND_QS * 32 * 4));
+      a.mc_cont = c->mc_cont.as<IndCont>();
+      a.mc_ncont = c->mc_ncont.as<uint32_t>();
+      a.mc_cap_s = (uint32_t)full;
+    }
     // single Monte Carlo pass; grow the query lists and re-run on overflow
     uint32_t nq[2] = {0, 0};
     HIPCHK(c, hipMemcpyAsync(c->stats_bak.p, c->d_stats.p, ST_BYTES,
@@ -1018,7 +1031,7 @@ void gi_destroy(gi_ctx *c) {
   DBuf *bufs[] = {&c->d_nodes, &c->d_elems, &c->d_shapes, &c->d_tris, &c->d_mats, &c->d_lights,
                   &c->d_lut, &c->d_stats, &c->spawn, &c->npaths, &c->path_off, &c->base,
                   &c->pixels, &c->rgbf, &c->rgb8, &c->gheap_d2, &c->gheap_idx, &c->qcount,
-                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont, &c->fb_list, &c->fb_count, &c->fb_dense, &c->dk_q};
+                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont, &c->mc_cont, &c->mc_ncont, &c->fb_list, &c->fb_count, &c->fb_dense, &c->dk_q};
   for (DBuf *b : bufs) b->release();
   for (int l = 0; l < 2; l++) {
     c->qpos[l].release(); c->qshade[l].release(); c->qkey[l].release(); c->qout[l].release();

@@ -30,14 +30,20 @@ struct Spawn {
 // an indirect sample path whose first bounce hit a material with a specular or transmissive
 // term: the state of MonteCarlo_IndirectSample's loop (montecarlo.cpp:177-305) at that hit,
 // queued so the shading and the rest of the path run compacted in ind_cont_kernel
+// Two kinds share the record (and ind_cont_kernel):
+//   mat >= 0: an indirect sample path queued at its first hit (hp, hn, mat) by ind_kernel;
+//   mat == -1: the IndirectIllumination(inMC) sub-path of a Monte Carlo path (montecarlo.cpp:
+//   144-152), queued by mc_kernel as a ray (org, direction in hp) with its path's query count j;
+//   its contribution is added to the path's base (the last term of that path's sum).
 struct IndCont {
   double org[3];          // origin of the traced ray (the loop's ray_start)
-  double hp[3], hn[3];    // hit point and normal
+  double hp[3], hn[3];    // hit point and normal (mat >= 0); hp = ray direction (mat == -1)
   double w[3];            // outer weight W (throughput is still 1)
   uint64_t rkey, rctr;    // RNG stream position
   uint32_t g, prim;       // path slot, primary sample
-  uint32_t pslot, qslot;  // slot within the primary, deterministic global-query slot
-  int32_t mat, pad;
+  uint32_t pslot, qslot;  // slot within the primary, global-query slot (~0: append)
+  int32_t mat;
+  uint32_t j;             // queries already issued by the path (mat == -1)
 };
 
 // continuation queue stripes: wave w appends to stripe w % IND_QS (one atomic per wave on a
@@ -87,6 +93,9 @@ struct RenderArgs {
   IndCont *ind_cont;    // continuation queue: IND_QS stripes of ind_cap_s entries
   uint32_t *ind_ncont;  // fill of stripe s at [s * 32] (one 128-B line per counter)
   uint32_t ind_cap_s;
+  IndCont *mc_cont;     // Monte Carlo paths' indirect sub-paths, striped the same way
+  uint32_t *mc_ncont;
+  uint32_t mc_cap_s;
   int64_t qind_base;    // global list: indirect path t owns slot qind_base + t
   // query lists (0 = global map, 1 = caustic map). Deterministic slots first: list l slot p
   // = primary sample p's own query (slot-0 path), then (global list only) slot

@@ -296,9 +296,9 @@ __device__ __noinline__ void mc_indirect(PathCtx &P, V org, V dir, Rng &rng, C3 
   mc_indirect_body<KINDS>(P, org, dir, rng, W);
 }
 
-// MonteCarlo_PathTrace, montecarlo.cpp:16-171
-template <uint32_t KINDS = KINDS_ALL>
-__device__ __noinline__ void mc_path(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
+// MonteCarlo_PathTrace, montecarlo.cpp:16-171 (DEFER: indirect sub-paths go to the mc_cont queue)
+template <uint32_t KINDS = KINDS_ALL, bool DEFER = false, bool HARD = false>
+__device__ __forceinline__ void mc_path(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
   const SceneView &S = *P.S;
   const Flags &F = *P.F;
   if (!F.monte_carlo) return;
@@ -316,8 +316,10 @@ __device__ __noinline__ void mc_path(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
     if (F.ambient) cb += ldc(S.ambient);
     V view = normalize(h.p - ray_start);
     double ct = dot(h.n, -view);
-    if (m.flags & (MF_DIFFUSE | MF_SPECULAR))
-      direct_illumination<KINDS>(S, F, h.p, h.n, ray_start, cb, m, ct, true, rng, P.cnt);
+    if (m.flags & (MF_DIFFUSE | MF_SPECULAR)) {
+      if (HARD) direct_illumination_hard<KINDS>(S, F, h.p, h.n, ray_start, cb, m, ct, true, P.cnt);
+      else direct_illumination<KINDS>(S, F, h.p, h.n, ray_start, cb, m, ct, true, rng, P.cnt);
+    }
     if (F.caustic && (m.flags & MF_DIFFUSE)) {
       V ex = reflective_bounce(h.n, view, ct);
       put_query(P, 1, h.p, h.n, ex, ct, h.mat, W * tw);
@@ -338,9 +340,37 @@ __device__ __noinline__ void mc_path(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
     if (rnd < pd) {
       C3 kd = ldc(m.kd);
       if (F.indirect) {
-        // IndirectIllumination(inMC): one sample continuing this path's stream
+        // IndirectIllumination(inMC): one sample continuing this path's stream. Queued (the
+        // path ends here, so its trace is this path's last work and its background term the
+        // last addition to the path's sum) and traced compacted in ind_cont_kernel.
         V s2 = diffuse_sample(h.n, ct, rng);
-        mc_indirect<KINDS>(P, h.p + s2 * kEps, s2, rng, W * ((kd * kd * tw) / pd));
+        C3 w2 = W * ((kd * kd * tw) / pd);
+        if (DEFER) {
+          V o2 = h.p + s2 * kEps;
+          uint64_t act = __ballot(1);
+          int lane = (int)(threadIdx.x & 63);
+          int leader = __ffsll((long long)act) - 1;
+          const uint32_t stripe = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) & (IND_QS - 1);
+          uint32_t qb = 0;
+          if (lane == leader) qb = atomicAdd(&P.A->mc_ncont[stripe * 32], (uint32_t)__popcll(act));
+          qb = (uint32_t)__shfl((int)qb, leader, 64);
+          IndCont &q = P.A->mc_cont[(size_t)stripe * P.A->mc_cap_s + qb +
+                                    (uint32_t)__popcll(act & ((1ull << lane) - 1ull))];
+          q.org[0] = o2.x; q.org[1] = o2.y; q.org[2] = o2.z;
+          q.hp[0] = s2.x; q.hp[1] = s2.y; q.hp[2] = s2.z;
+          q.w[0] = w2.r; q.w[1] = w2.g; q.w[2] = w2.b;
+          q.rkey = rng.key;
+          q.rctr = rng.ctr;
+          q.g = (uint32_t)P.g;
+          q.prim = P.prim;
+          q.pslot = P.pslot;
+          q.qslot = P.fixed[0] >= 0 ? (uint32_t)P.fixed[0] : 0xffffffffu;
+          q.mat = -1;
+          q.j = P.j;
+          P.fixed[0] = -2;  // the sub-path owns the global slot now
+        } else {
+          mc_indirect<KINDS>(P, h.p + s2 * kEps, s2, rng, w2);
+        }
         P.cnt.indirect++;
       } else if (F.fast_global) {
         V ex = reflective_bounce(h.n, view, ct);
@@ -533,40 +563,60 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void i
   path_stats(a, cnt);
 }
 
-// the queued indirect paths (shading of the first hit, then MonteCarlo_IndirectSample's loop
-// from iteration 1 on), one per thread: block b serves stripe b % IND_QS, striding over its fill
-// (the fills are known only on the device)
+// the queued indirect paths, one per thread: block b serves stripe b % IND_QS, striding over its
+// fill (the fills are known only on the device). At-hit entries (mat >= 0): shading of the
+// first hit, then MonteCarlo_IndirectSample's loop from iteration 1 on; ray entries
+// (mat == -1): the whole loop, its contribution added to the Monte Carlo path's base.
 template <uint32_t KINDS>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void ind_cont_kernel(RenderArgs a) {
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2)))
+void ind_cont_kernel(RenderArgs a, const IndCont *queue, const uint32_t *fill, uint32_t cap_s) {
   const uint32_t stripe = blockIdx.x % IND_QS, part = blockIdx.x / IND_QS;
   const uint32_t parts = gridDim.x / IND_QS;
-  const uint32_t n = min(a.ind_ncont[stripe * 32], a.ind_cap_s);
+  const uint32_t n = min(fill[stripe * 32], cap_s);
   Counts tot = {0, 0, 0, 0, 0, 0};
   const uint32_t rounds = (n + parts * blockDim.x - 1) / (parts * blockDim.x);
   for (uint32_t r = 0; r < rounds; r++) {
     uint32_t idx = (r * parts + part) * blockDim.x + threadIdx.x;
     if (idx >= n) continue;
-    const IndCont &q = a.ind_cont[(size_t)stripe * a.ind_cap_s + idx];
+    const IndCont &q = queue[(size_t)stripe * cap_s + idx];
     PathCtx P;
     path_init(P, a, q.g, q.prim, (int)q.pslot);
-    P.fixed[0] = q.qslot;
+    P.fixed[0] = (q.qslot == 0xffffffffu) ? -1 : (int64_t)q.qslot;
     Rng rng;
     rng.key = q.rkey;
     rng.ctr = q.rctr;
-    V org = ld3(q.org), dir = org;
     C3 tw = rgb(1, 1, 1), W = ldc(q.w);
-    Hit h;
-    h.p = ld3(q.hp);
-    h.n = ld3(q.hn);
-    h.t = 0.0;
-    h.mat = q.mat;
-    if (ind_shade<false>(P, h, org, dir, rng, W, tw))
-      for (int iter = 1; iter < a.F.max_monte_depth; iter++)
+    V org = ld3(q.org), dir = org;
+    bool go;
+    int iter0;
+    if (q.mat >= 0) {
+      Hit h;
+      h.p = ld3(q.hp);
+      h.n = ld3(q.hn);
+      h.t = 0.0;
+      h.mat = q.mat;
+      go = ind_shade<false>(P, h, org, dir, rng, W, tw);
+      iter0 = 1;
+    } else {
+      P.j = q.j;
+      dir = ld3(q.hp);
+      go = true;
+      iter0 = 0;
+    }
+    if (go)
+      for (int iter = iter0; iter < a.F.max_monte_depth; iter++)
         if (!ind_bounce<KINDS>(P, org, dir, rng, W, tw)) break;
     if (P.fixed[0] >= 0) put_none(a, 0, P.fixed[0]);
-    a.base[3 * (int64_t)q.g] = P.base.r;
-    a.base[3 * (int64_t)q.g + 1] = P.base.g;
-    a.base[3 * (int64_t)q.g + 2] = P.base.b;
+    double *bp = a.base + 3 * (int64_t)q.g;
+    if (q.mat >= 0) {
+      bp[0] = P.base.r;
+      bp[1] = P.base.g;
+      bp[2] = P.base.b;
+    } else {  // the sub-path's background term is the last addition to the path's sum
+      bp[0] = bp[0] + P.base.r;
+      bp[1] = bp[1] + P.base.g;
+      bp[2] = bp[2] + P.base.b;
+    }
     tot.shadow += P.cnt.shadow; tot.monte += P.cnt.monte; tot.trans += P.cnt.trans;
     tot.spec += P.cnt.spec; tot.indirect += P.cnt.indirect; tot.caustic += P.cnt.caustic;
   }
@@ -574,7 +624,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void i
 }
 
 // TransmissiveIllumination / SpecularIllumination sample (raytracer.cpp:47-109)
-template <uint32_t KINDS>
+template <uint32_t KINDS, bool DEFER, bool HARD>
 __global__ __launch_bounds__(128) void mc_kernel(RenderArgs a) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   Counts cnt = {0, 0, 0, 0, 0, 0};
@@ -599,7 +649,7 @@ __global__ __launch_bounds__(128) void mc_kernel(RenderArgs a) {
       V ex = transmissive_bounce(F.ir_air, n, view, ct, m.ir);
       C3 tw = (1.0 - R) * ldc(m.kt);
       V sb = F.distrib_trans ? specular_sample(ex, m.n, ct, rng) : ex;
-      mc_path<KINDS>(P, p + sb * kEps, sb, rng, tw / (double)sp.n_t);
+      mc_path<KINDS, DEFER, HARD>(P, p + sb * kEps, sb, rng, tw / (double)sp.n_t);
       P.cnt.trans++;
     } else {
       s -= sp.n_t;
@@ -607,7 +657,7 @@ __global__ __launch_bounds__(128) void mc_kernel(RenderArgs a) {
       V ex = reflective_bounce(n, view, ct);
       C3 tw = ldc(m.kt) * R + ldc(m.ks);
       V sb = F.distrib_spec ? specular_sample(ex, m.n, ct, rng) : ex;
-      mc_path<KINDS>(P, p + sb * kEps, sb, rng, tw / (double)sp.n_s);
+      mc_path<KINDS, DEFER, HARD>(P, p + sb * kEps, sb, rng, tw / (double)sp.n_s);
       P.cnt.spec++;
     }
     a.base[3 * g] = P.base.r;
@@ -1275,6 +1325,15 @@ void launch_ind(const RenderArgs &a, unsigned g, hipStream_t st) {
   else if (a.ind_waves == 4) ind_kernel<4, true, KINDS><<<g, 128, 0, st>>>(a);
   else ind_kernel<5, true, KINDS><<<g, 128, 0, st>>>(a);
 }
+void launch_cont(const RenderArgs &a, const IndCont *q, const uint32_t *fill, uint32_t cap_s,
+                 hipStream_t st) {
+  if ((a.S.kinds & ~KINDS_TRI_SPHERE) == 0)
+    ind_cont_kernel<KINDS_TRI_SPHERE><<<IND_QS * 32, 128, 0, st>>>(a, q, fill, cap_s);
+  else if ((a.S.kinds & ~KINDS_POLY) == 0)
+    ind_cont_kernel<KINDS_POLY><<<IND_QS * 32, 128, 0, st>>>(a, q, fill, cap_s);
+  else
+    ind_cont_kernel<KINDS_ALL><<<IND_QS * 32, 128, 0, st>>>(a, q, fill, cap_s);
+}
 void launch_path(const RenderArgs &a, hipStream_t st) {
   if (a.nprim > 0) slot0_kernel<<<nblk(a.nprim, 256), 256, 0, st>>>(a);
   if (a.total_ind > 0) {
@@ -1285,17 +1344,25 @@ void launch_path(const RenderArgs &a, hipStream_t st) {
     else if ((a.S.kinds & ~KINDS_POLY) == 0) launch_ind<KINDS_POLY>(a, g, st);
     else launch_ind<KINDS_ALL>(a, g, st);
     // continuations: 32 blocks per stripe stride over its fill
-    if (a.split_ind) {
-      if ((a.S.kinds & ~KINDS_TRI_SPHERE) == 0) ind_cont_kernel<KINDS_TRI_SPHERE><<<IND_QS * 32, 128, 0, st>>>(a);
-      else if ((a.S.kinds & ~KINDS_POLY) == 0) ind_cont_kernel<KINDS_POLY><<<IND_QS * 32, 128, 0, st>>>(a);
-      else ind_cont_kernel<KINDS_ALL><<<IND_QS * 32, 128, 0, st>>>(a);
-    }
+    if (a.split_ind) launch_cont(a, a.ind_cont, a.ind_ncont, a.ind_cap_s, st);
   }
   if (a.total_mc > 0) {
     unsigned g = nblk(a.total_mc, 128);
-    if ((a.S.kinds & ~KINDS_TRI_SPHERE) == 0) mc_kernel<KINDS_TRI_SPHERE><<<g, 128, 0, st>>>(a);
-    else if ((a.S.kinds & ~KINDS_POLY) == 0) mc_kernel<KINDS_POLY><<<g, 128, 0, st>>>(a);
-    else mc_kernel<KINDS_ALL><<<g, 128, 0, st>>>(a);
+    if (a.mc_cont) (void)hipMemsetAsync(a.mc_ncont, 0, IND_QS * 32 * sizeof(uint32_t), st);
+    if (a.mc_cont) {
+      if ((a.S.kinds & ~KINDS_TRI_SPHERE) == 0) {
+        if (a.S.hard_lights) mc_kernel<KINDS_TRI_SPHERE, true, true><<<g, 128, 0, st>>>(a);
+        else mc_kernel<KINDS_TRI_SPHERE, true, false><<<g, 128, 0, st>>>(a);
+      } else if ((a.S.kinds & ~KINDS_POLY) == 0) {
+        if (a.S.hard_lights) mc_kernel<KINDS_POLY, true, true><<<g, 128, 0, st>>>(a);
+        else mc_kernel<KINDS_POLY, true, false><<<g, 128, 0, st>>>(a);
+      } else {
+        mc_kernel<KINDS_ALL, true, false><<<g, 128, 0, st>>>(a);
+      }
+      launch_cont(a, a.mc_cont, a.mc_ncont, a.mc_cap_s, st);
+    } else {
+      mc_kernel<KINDS_ALL, false, false><<<g, 128, 0, st>>>(a);
+    }
   }
 }
 void launch_reduce(const RenderArgs &a, hipStream_t st) {

@@ -227,6 +227,7 @@ struct gi_ctx {
   int ind_waves = 3;              // indirect-path kernel occupancy target (waves per SIMD)
   DBuf ind_cont, ind_ncont;       // indirect paths that continue past their first bounce
   DBuf mc_cont, mc_ncont;         // Monte Carlo paths' indirect sub-paths
+  DBuf prim_rgb;                  // per-primary sums of the reduction
   bool split_ind = true;          // continuation queue for indirect paths (else one loop per lane)
   double ind_frac = 0.25;         // continuation queue size, as a fraction of its worst case
   // render scratch
@@ -950,6 +951,8 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     }
     a.rgbf = c->rgbf.as<float>();
     a.rgb8 = c->rgb8.as<uint8_t>();
+    HIPCHK(c, c->prim_rgb.ensure((size_t)nprim * 24));
+    a.prim_rgb = c->prim_rgb.as<double>();
     launch_reduce(a, c->stream);
     HIPCHK(c, hipGetLastError());
   }
@@ -1031,7 +1034,7 @@ void gi_destroy(gi_ctx *c) {
   DBuf *bufs[] = {&c->d_nodes, &c->d_elems, &c->d_shapes, &c->d_tris, &c->d_mats, &c->d_lights,
                   &c->d_lut, &c->d_stats, &c->spawn, &c->npaths, &c->path_off, &c->base,
                   &c->pixels, &c->rgbf, &c->rgb8, &c->gheap_d2, &c->gheap_idx, &c->qcount,
-                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont, &c->mc_cont, &c->mc_ncont, &c->fb_list, &c->fb_count, &c->fb_dense, &c->dk_q};
+                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont, &c->mc_cont, &c->mc_ncont, &c->prim_rgb, &c->fb_list, &c->fb_count, &c->fb_dense, &c->dk_q};
   for (DBuf *b : bufs) b->release();
   for (int l = 0; l < 2; l++) {
     c->qpos[l].release(); c->qshade[l].release(); c->qkey[l].release(); c->qout[l].release();

@@ -114,6 +114,7 @@ struct RenderArgs {
   uint32_t *qseg[2];          // [nprim + 1]: sorted appends of primary b are [qseg[b], qseg[b+1])
   uint32_t nq[2];
   double *base;         // [total_paths * 3]
+  double *prim_rgb;     // [nprim * 3] per-primary sums (reduce_prim_kernel -> reduce_kernel)
   const double *qout[2];       // k-NN contributions per slot
   float *rgbf;
   uint8_t *rgb8;

@@ -1054,6 +1054,78 @@ void launch_segments(const uint64_t *skeys, uint32_t n, uint32_t nprim, uint32_t
 // Per-pixel reduction: RenderImage's DOF average + ClampColor + box filter + SetPixelRGB
 // (render.cpp:130-135, 205-221; R2Image.cpp:205-208)
 // ---------------------------------------------------------------------------------------
+// Pass 1, one thread per primary sample b: c(b) = sum of b's path bases, then of its queries,
+// in the oracle's order (a sequential fp64 sum; the loads of each run are issued four at a
+// time so a lane has several lines in flight, the additions stay in order).
+__global__ __launch_bounds__(256) void reduce_prim_kernel(RenderArgs a) {
+  int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= a.nprim) return;
+  double c0 = 0, c1 = 0, c2 = 0;
+  {
+    uint32_t g = a.path_off[b];
+    const uint32_t p1 = a.path_off[b + 1];
+    const double *bs = a.base;
+    for (; g + 4 <= p1; g += 4) {
+      double v[12];
+#pragma unroll
+      for (int u = 0; u < 12; u++) v[u] = bs[3 * (int64_t)g + u];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        c0 += v[3 * u];
+        c1 += v[3 * u + 1];
+        c2 += v[3 * u + 2];
+      }
+    }
+    for (; g < p1; g++) {
+      c0 += bs[3 * (int64_t)g];
+      c1 += bs[3 * (int64_t)g + 1];
+      c2 += bs[3 * (int64_t)g + 2];
+    }
+  }
+  // each list in (primary, slot in primary, query in path) order: the primary's own query
+  // (slot b), its Monte Carlo paths' appends (sorted), then (global list) its indirect paths'
+  // queries (slots qind_base + t, in path order); empty slots skipped
+  for (int l = 0; l < 2; l++) {
+    if (!a.qout[l]) continue;
+    const uint64_t *qk = a.qkey[l];
+    const double *qo = a.qout[l];
+    auto add = [&](int64_t sl) {
+      if (qk[sl] == ~0ull) return;
+      c0 += qo[3 * sl];
+      c1 += qo[3 * sl + 1];
+      c2 += qo[3 * sl + 2];
+    };
+    add(b);
+    uint32_t q0 = a.qseg[l][b], q1 = a.qseg[l][b + 1];
+    for (uint32_t q = q0; q < q1; q++) add((int64_t)a.qapp[l] + a.sslot[l][q]);
+    if (l == 0) {
+      uint32_t t = a.ind_off[b];
+      const uint32_t t1 = a.ind_off[b + 1];
+      for (; t + 4 <= t1; t += 4) {
+        const int64_t s0 = a.qind_base + t;
+        uint64_t k[4];
+        double v[12];
+#pragma unroll
+        for (int u = 0; u < 4; u++) k[u] = qk[s0 + u];
+#pragma unroll
+        for (int u = 0; u < 12; u++) v[u] = qo[3 * s0 + u];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          if (k[u] != ~0ull) {
+            c0 += v[3 * u];
+            c1 += v[3 * u + 1];
+            c2 += v[3 * u + 2];
+          }
+      }
+      for (; t < t1; t++) add(a.qind_base + t);
+    }
+  }
+  a.prim_rgb[3 * b] = c0;
+  a.prim_rgb[3 * b + 1] = c1;
+  a.prim_rgb[3 * b + 2] = c2;
+}
+
+// Pass 2, one thread per output pixel
 __global__ __launch_bounds__(64) void reduce_kernel(RenderArgs a) {
   int pix = blockIdx.x * blockDim.x + threadIdx.x;
   if (pix >= a.npix) return;
@@ -1064,31 +1136,9 @@ __global__ __launch_bounds__(64) void reduce_kernel(RenderArgs a) {
     double s0 = 0, s1 = 0, s2 = 0;
     for (int k = 0; k < a.dof_test; k++) {
       int64_t b = ((int64_t)pix * af2 + sub) * a.dof_test + k;
-      uint32_t p0 = a.path_off[b], p1 = a.path_off[b + 1];
-      double c0 = 0, c1 = 0, c2 = 0;
-      for (uint32_t g = p0; g < p1; g++) {
-        c0 += a.base[3 * (int64_t)g];
-        c1 += a.base[3 * (int64_t)g + 1];
-        c2 += a.base[3 * (int64_t)g + 2];
-      }
-      // each list in (primary, slot in primary, query in path) order: the primary's own
-      // query (slot b), its Monte Carlo paths' appends (sorted), then (global list) its
-      // indirect paths' queries (slots qind_base + t, in path order); empty slots skipped
-      for (int l = 0; l < 2; l++) {
-        if (!a.qout[l]) continue;
-        auto add = [&](int64_t sl) {
-          if (a.qkey[l][sl] == ~0ull) return;
-          c0 += a.qout[l][3 * sl];
-          c1 += a.qout[l][3 * sl + 1];
-          c2 += a.qout[l][3 * sl + 2];
-        };
-        add(b);
-        uint32_t q0 = a.qseg[l][b], q1 = a.qseg[l][b + 1];
-        for (uint32_t q = q0; q < q1; q++) add((int64_t)a.qapp[l] + a.sslot[l][q]);
-        if (l == 0)
-          for (uint32_t t = a.ind_off[b]; t < a.ind_off[b + 1]; t++) add(a.qind_base + t);
-      }
-      s0 += c0; s1 += c1; s2 += c2;
+      s0 += a.prim_rgb[3 * b];
+      s1 += a.prim_rgb[3 * b + 1];
+      s2 += a.prim_rgb[3 * b + 2];
     }
     s0 /= a.dof_test; s1 /= a.dof_test; s2 /= a.dof_test;
     s0 = s0 < 0 ? 0 : (s0 > 1.0 ? 1.0 : s0);
@@ -1366,6 +1416,7 @@ void launch_path(const RenderArgs &a, hipStream_t st) {
   }
 }
 void launch_reduce(const RenderArgs &a, hipStream_t st) {
+  reduce_prim_kernel<<<nblk(a.nprim, 256), 256, 0, st>>>(a);
   reduce_kernel<<<nblk(a.npix, 64), 64, 0, st>>>(a);
 }
 void launch_knn(const KnnArgs &a, bool lds_heap, hipStream_t st) {

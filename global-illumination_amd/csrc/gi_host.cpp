@@ -236,6 +236,8 @@ struct gi_ctx {
   DBuf list_idx, list_d2, list_n;
   DBuf fb_list, fb_count, fb_dense;  // chunk k-NN fallback queries (striped, compacted)
   DBuf dk_q;                       // photon positions as queries (ensure_dk)
+  bool chunk_dk = true;            // chunk kernel (K <= 64): centre bound from the dk bounds (measured: fewer fallbacks)
+  bool chunk_fb_all = false;       // test knob: the lane-select chunk kernel hands every query to its fallback
   bool use_dk = true;              // wave k-NN kernel starts from per-photon K-th bounds
   uint64_t fb_total = 0;
   DBuf qseg[2];  // K-best lists of the query-per-wave k-NN path
@@ -642,8 +644,20 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
     k.fb_list = c->fb_list.as<uint32_t>();
     k.fb_count = c->fb_count.as<uint32_t>();
     k.fb_cap_s = cap_s;
+    // per-photon K-th distance bounds: the fallback's starting bound; the chunk kernel's centre
+    // bound uses them only with chunk_dk (else the exact d_K(c) gather)
+    const float *fb_dk = nullptr;
+    if (c->use_dk && k.mode != KNN_MODE_DK) {
+      int rc = ensure_dk(c, k);
+      if (rc) return rc;
+      fb_dk = k.map.dk;
+      if (!c->chunk_dk) k.map.dk = nullptr;
+    }
+    const int dbg0 = k.dbg;
+    if (c->chunk_fb_all && kind == 7) k.dbg |= 4;  // lane select skipped: all to the fallback
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     launch_knn_chunk(k, c->chunk_cap, kind - 5, c->stream);
+    k.dbg = dbg0;
     HIPCHK(c, hipGetLastError());
     uint32_t *dense = c->fb_dense.as<uint32_t>();
     launch_fb_compact(k.fb_list, k.fb_count, cap_s, dense, dense + nq, c->stream);
@@ -658,6 +672,7 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
       f.perm = dense;
       f.nq = nfb;
       f.q0 = 0;
+      f.map.dk = fb_dk;
       launch_knn_lane(f, c->lane_chunk, c->heap_arity, c->stream);
       HIPCHK(c, hipGetLastError());
     }
@@ -1021,6 +1036,8 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_IND_WAVES")) c->ind_waves = std::max(1, atoi(s));
   if (const char *s = getenv("GI_SPLIT_IND")) c->split_ind = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_DK")) c->use_dk = atoi(s) != 0;
+  if (const char *s = getenv("GI_CHUNK_DK")) c->chunk_dk = atoi(s) != 0;
+  if (const char *s = getenv("GI_CHUNK_FB_ALL")) c->chunk_fb_all = atoi(s) != 0;
   if (const char *s = getenv("GI_IND_FRAC")) c->ind_frac = std::min(1.0, std::max(1e-6, atof(s)));
   if (const char *s = getenv("GI_SORT_QUERIES")) c->sort_queries = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_KERNEL")) c->knn_kernel_kind = atoi(s);

@@ -580,6 +580,11 @@ __global__ __launch_bounds__(64) void knn_lane_kernel(KnnArgs a) {
   uint32_t visited = 0;
   int node = 1;
   bool live = valid && N > 0 && K > 0;
+  // first leaf (usually q's own): its photons p also give d_K(q) <= |q - p| + d_K(p)
+  // (KdView::dk, triangle inequality, as knn_wave_kernel's start), which caps lim from the
+  // second leaf on, so the rest of the walk prunes to about the K-neighbourhood
+  bool seed = a.map.dk != nullptr;
+  float sb = INFINITY, sd2 = 0.0f, sdk = INFINITY;
   while (__ballot(live)) {
     // walk to the next leaf within the bound
     int leaf = -1;
@@ -614,13 +619,32 @@ __global__ __launch_bounds__(64) void knn_lane_kernel(KnnArgs a) {
         float4 p[CH];
 #pragma unroll
         for (int u = 0; u < CH; u++) p[u] = pos[(ii + u < s1) ? ii + u : s1 - 1];
+        float dk[CH];
+        if (seed) {
+#pragma unroll
+          for (int u = 0; u < CH; u++) dk[u] = a.map.dk[(ii + u < s1) ? ii + u : s1 - 1];
+        }
 #pragma unroll
         for (int u = 0; u < CH; u++) {
           float dx = qp.x - p[u].x, dy = qp.y - p[u].y, dz = qp.z - p[u].z;
           float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
           uint64_t key = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)(uint32_t)(ii + u);
           if (ii + u < s1 && key < lim) heapn_accept<ARY>(h, size, K, key, lim);
+          if (seed) {
+            float v = sqrtf(d2) + dk[u];
+            if (v < sb) { sb = v; sd2 = d2; sdk = dk[u]; }
+          }
         }
+      }
+    }
+    if (seed && leaf >= 0) {
+      // the photon minimising |q - p| + d_K(p) is picked in f32; the bound is computed with
+      // its rounding margins in f64 for that photon (any photon gives a valid bound)
+      seed = false;
+      if (sdk < INFINITY) {
+        double U = (sqrt((double)sd2 * (1.0 + 1e-5)) + (double)sdk) * (1.0 + 1e-6) + 1e-12;
+        uint64_t ul = ((uint64_t)__float_as_uint(__double2float_ru(U * U * (1.0 + 1e-5))) + 1ull) << 32;
+        if (ul < lim) lim = ul;
       }
     }
     if (leaf >= 0) live = kd_next(nodes, node, qp.x, qp.y, qp.z);

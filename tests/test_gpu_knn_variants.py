@@ -8,7 +8,9 @@ exactly: the fp32 metric is shared, and only photons tied at the k-th distance m
 GI_KNN_KERNEL 5-7 = chunk kernels, 8 = the large-K chunk kernel (bitmask selection, bounds from
 per-photon K-th distances); GI_CHUNK_MINSUB sets how far an overflowing chunk is split
 (1 = down to single queries, 64 = straight to the per-lane fallback). GI_KNN_DK=0 turns off the
-wave kernel's start from per-photon K-th distance bounds (on by default).
+wave kernel's and the chunk fallback's start from per-photon K-th distance bounds (on by
+default); GI_CHUNK_DK=1 takes the chunk kernel's centre bound from them too; GI_CHUNK_FB_ALL=1
+sends every query of the lane-select chunk kernel to its per-lane fallback.
 It must also return its EstimateRadiance within rtol 1e-10 (fp64 sums in a different order).
 Leaf sizes are varied too, because the result set may not depend on the tree shape."""
 import os
@@ -41,6 +43,9 @@ VARIANTS = [
     {"GI_KNN_KERNEL": "7", "GI_LEAF_SIZE": "50"},
     {"GI_KNN_KERNEL": "7", "GI_CHUNK_MINSUB": "1"},
     {"GI_KNN_KERNEL": "7", "GI_CHUNK_MINSUB": "64"},
+    {"GI_KNN_KERNEL": "7", "GI_CHUNK_DK": "1"},
+    {"GI_KNN_KERNEL": "7", "GI_CHUNK_FB_ALL": "1"},
+    {"GI_KNN_KERNEL": "7", "GI_CHUNK_FB_ALL": "1", "GI_KNN_DK": "0"},
     {"GI_KNN_KERNEL": "8"},
     {"GI_KNN_KERNEL": "8", "GI_CHUNK_CAP_BIG": "384", "GI_LEAF_SIZE": "128"},
     {"GI_KNN_KERNEL": "8", "GI_CHUNK_MINSUB_BIG": "1"},

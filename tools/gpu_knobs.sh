@@ -11,7 +11,7 @@ for s in "${SET[@]}"; do
   i=$((i+1))
   echo "== $s"
   env $s timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/s$i -o run -- python3 bench.py --res ${RES:-512} --steps 1 --warmup 0 --no-cpu-baseline > $D/s$i.log 2>&1 || { tail -20 $D/s$i.log; exit 1; }
-  grep '^{' $D/s$i.log | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); g=d['roofline']['global']; c=d['roofline']['caustic_kernel']; print('value', d['value'], 'fb_frac', g['fallback_query_frac'], 'fb_ms', g['fallback_avg_ms'], 'glob_ms', g['avg_launch_ms'], 'caus_ms', c['avg_launch_ms'], 'caus_vis', round(c['visited_per_query'],1))"
+  grep '^{' $D/s$i.log | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); g=d['roofline']['global']; c=d['roofline']['caustic_kernel']; print('value', d['value'], 'fb_frac', g['fallback_query_frac'], 'fb_ms', g['fallback_avg_ms'], 'glob_ms', g['avg_launch_ms'], 'caus_ms', c['avg_launch_ms'], 'caus_fb', c['fallback_query_frac'], 'caus_fb_ms', c['fallback_avg_ms'], 'caus_vis', round(c['visited_per_query'],1))"
   python3 - $D/s$i/run_kernel_stats.csv <<'PY'
 import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))

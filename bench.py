@@ -189,7 +189,7 @@ def main():
         roofline = {"bound": "hbm", "achieved": g["achieved_GBps"], "peak": HBM_PEAK_GBPS,
                     "unit": "GB/s", "frac": round(g["achieved_GBps"] / HBM_PEAK_GBPS, 5),
                     "traffic": traffic,
-                    "kernel": "gi::knn_chunk_lane_kernel<3> + gi::knn_lane_kernel<8,4> fallback "
+                    "kernel": "gi::knn_chunk_lane_kernel<4> + gi::knn_lane_kernel<8,4> fallback "
                               "(global map k-NN + EstimateRadiance; avg_launch_ms = their sum)",
                     "bytes_per_unit": "16 B per photon returned (SURVEY.md 8(d))",
                     "global": g, "caustic_kernel": dict(c, kernel="gi::knn_wave_kernel<512> + knn_list_estimate_kernel")}

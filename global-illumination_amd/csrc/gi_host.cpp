@@ -214,7 +214,7 @@ struct gi_ctx {
   int chunk_cap = 256;            // chunk kernel: LDS candidate capacity per 64-query chunk
   int chunk_cap_big = 512;        // large-K chunk kernel: the same (384 or 512)
   int chunk_minsub_big = 64;      // large-K chunk kernel: overflowing chunks retried down to this (64: none, measured best)
-  int chunk_minsub = 64;          // chunk kernel: overflowing chunks retried down to this group size (64: no retry, measured best)
+  int chunk_minsub = 32;          // chunk kernel: overflowing chunks retried as halves (measured best with the dk bound)
   hipEvent_t ev2 = nullptr;       // chunk kernel / fallback split
   double fb_ms[2] = {0, 0};       // fallback time and queries per map (since the last reset)
   uint64_t fb_q[2] = {0, 0};

@@ -47,6 +47,10 @@ __device__ __forceinline__ double wmax(double v) {
   return v;
 }
 
+#ifndef CHUNK_EST_EB
+#define CHUNK_EST_EB 4         // photons per LDS/LUT round trip in the chunk estimate
+#endif
+
 // ascending bitonic sort of one float per lane across the wave
 __device__ __forceinline__ float wave_sort(float v, int lane) {
 #pragma unroll
@@ -456,7 +460,7 @@ __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, flo
       // photons in groups of EB: the LDS slot reads and direction-LUT loads of a group are
       // issued before its arithmetic (one memory round trip per group, not per photon); the
       // sums still run in photon order
-      constexpr int EB = 4;
+      constexpr int EB = CHUNK_EST_EB;
       for (int s0 = 0; s0 < num; s0 += EB) {
       float4 pg[EB];
       uint32_t eg[EB];
@@ -559,6 +563,9 @@ __device__ __forceinline__ void chunk_flush_stats(const KnnArgs &a, const ChunkP
 // ---------------------------------------------------------------------------------------------
 constexpr int LS_BR = 4;       // bracket photons resolved by the collect pass
 constexpr int LS_PASSES = 10;  // counting passes before a query goes to the fallback
+#ifndef LS_UNROLL
+#define LS_UNROLL 4            // candidates per LDS round trip in the counting / collect loops
+#endif
 
 // value-range bin of d2 in the bracket binning (lo, sc): monotone non-decreasing in d2, 0 at lo
 // (also for sc = inf), 15 at the bracket's top
@@ -597,9 +604,13 @@ void knn_chunk_lane_kernel(KnnArgs a) {
   __shared__ float4 cpos[CAPC];
   __shared__ uint32_t cidx[CAPC];
   __shared__ uint32_t crgbe[CAPC];
-  __shared__ uint32_t hist[256];
   __shared__ uint32_t stk[64];  // kd walk stack (walk_within)
-  __shared__ uint8_t sel[64 * 64];  // kept LDS slots, [s][lane] (K <= 64)
+  // kept LDS slots [s][lane] (K <= 64, u8) during the collect and the estimate; during the
+  // counting passes the same 4 KiB hold the lanes' bin counters [bin][lane] (u32), and during
+  // the bound phase the centre select's 256-bin histogram
+  __shared__ uint32_t selh[16 * 64];
+  uint8_t *sel = reinterpret_cast<uint8_t *>(selh);
+  uint32_t *hist = selh;
   const int lane = threadIdx.x;
   const int K = a.K;
   uint64_t st_q = 0, st_found = 0, st_vis = 0;
@@ -626,7 +637,7 @@ void knn_chunk_lane_kernel(KnnArgs a) {
     const bool act = valid && ((gm >> lane) & 1ull);
     if (P.on) P.t = clock64();
     ChunkGeom G;
-    // byte counters below: at most 255 candidates per chunk
+    // u8 slot lists below: at most 255 candidates per chunk
     chunk_bound_gather<CAPC>(a, lane, act, qp, CAPC - 1, cpos, cidx, crgbe, hist, stk, G, P);
     __syncthreads();
     if (G.overflow) continue;
@@ -655,21 +666,21 @@ void knn_chunk_lane_kernel(KnnArgs a) {
         if (P.on) P.c[8]++;
         const bool on = mode == 1;
         const float sc = 16.0f / (B - O);
-        uint64_t w0 = 0, w1 = 0;  // 16 bins x 8-bit counters
-#pragma unroll 4
+        // 16 bins per lane as LDS counters [bin][lane] (conflict-free, one ds_add per member)
+#pragma unroll
+        for (int b = 0; b < 16; b++) selh[b * 64 + lane] = 0u;
+#pragma unroll LS_UNROLL
         for (uint32_t s = 0; s < count; s++) {
           float d2 = metric(qx, qy, qz, cpos[s]);
           bool mem = on && d2 >= A && d2 <= B;
           uint32_t b = bin16(d2, O, sc);
-          uint64_t inc = mem ? (1ull << ((b & 7u) << 3)) : 0ull;
-          if (b & 8u) w1 += inc;
-          else w0 += inc;
+          if (mem) atomicAdd(&selh[b * 64 + lane], 1u);
         }
         if (on) {
           uint32_t before = 0, bs = 16, cb = 0;
 #pragma unroll
           for (int b = 0; b < 16; b++) {
-            uint32_t c = (uint32_t)(((b < 8) ? (w0 >> (8 * b)) : (w1 >> (8 * (b - 8)))) & 255ull);
+            uint32_t c = selh[b * 64 + lane];
             if (bs == 16) {
               if (before + c >= (uint32_t)need) { bs = (uint32_t)b; cb = c; }
               else before += c;
@@ -714,7 +725,7 @@ void knn_chunk_lane_kernel(KnnArgs a) {
 #pragma unroll
     for (int i = 0; i < LS_BR; i++) br[i] = ~0ull;
     const bool inb_on = col && need > 0;
-#pragma unroll 4
+#pragma unroll LS_UNROLL
     for (uint32_t s = 0; s < count; s++) {
       float d2 = metric(qx, qy, qz, cpos[s]);
       if (col && d2 < A) {

@@ -235,6 +235,8 @@ struct gi_ctx {
   DBuf qpos[2], qshade[2], qkey[2], qout[2];
   DBuf list_idx, list_d2, list_n;
   DBuf fb_list, fb_count, fb_dense;  // chunk k-NN fallback queries (striped, compacted)
+  DBuf fb_list2, fb_count2, fb_dense2;  // large-K chunk k-NN: second pass's fallback queries
+  bool chunk_big2 = true;            // large-K chunk k-NN: second chunk pass (1024 candidates)
   DBuf dk_q;                       // photon positions as queries (ensure_dk)
   bool chunk_dk = true;            // chunk kernel (K <= 64): centre bound from the dk bounds (measured: fewer fallbacks)
   bool chunk_fb_all = false;       // test knob: the lane-select chunk kernel hands every query to its fallback
@@ -606,10 +608,39 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
     HIPCHK(c, hipMemcpyAsync(&nfb, dense + nq, 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->fb_total += nfb;
-    if (nfb) {
+    uint32_t nfb2 = nfb;
+    if (nfb && c->chunk_big2) {
+      // second chunk pass with 1024 LDS candidates over the overflowing chunks' queries (the
+      // compacted list keeps each chunk's queries together, in Morton order); what overflows
+      // again goes to the query-per-wave kernel
+      int64_t chunks2 = ((int64_t)nfb + 63) / 64;
+      int64_t grid2 = knn_chunk_grid(nfb);
+      uint32_t cap2 = (uint32_t)(64 * ((chunks2 + grid2 - 1) / grid2) * ((grid2 + FB_QS - 1) / FB_QS));
+      HIPCHK(c, c->fb_list2.ensure((size_t)FB_QS * cap2 * 4));
+      HIPCHK(c, c->fb_dense2.ensure((size_t)nfb * 4 + 4));
+      HIPCHK(c, c->fb_count2.ensure(FB_QS * 32 * 4));
+      HIPCHK(c, hipMemsetAsync(c->fb_count2.p, 0, FB_QS * 32 * 4, c->stream));
+      KnnArgs s2 = k;
+      s2.perm = dense;
+      s2.nq = nfb;
+      s2.q0 = 0;
+      s2.fb_list = c->fb_list2.as<uint32_t>();
+      s2.fb_count = c->fb_count2.as<uint32_t>();
+      s2.fb_cap_s = cap2;
+      s2.dbg &= ~16;
+      if (!launch_knn_chunk_big(s2, 1024, c->stream))
+        return fail(c, GI_ERR_ARG, "k-NN launch: large-K chunk kernel unavailable");
+      HIPCHK(c, hipGetLastError());
+      dense = c->fb_dense2.as<uint32_t>();
+      launch_fb_compact(s2.fb_list, s2.fb_count, cap2, dense, dense + nfb, c->stream);
+      HIPCHK(c, hipGetLastError());
+      HIPCHK(c, hipMemcpyAsync(&nfb2, dense + nfb, 4, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    if (nfb2) {
       KnnArgs f = k;
       f.perm = dense;
-      f.nq = nfb;
+      f.nq = nfb2;
       f.q0 = 0;
       if (!launch_knn_wave(f, c->wave_cap_mul, c->stream))
         return fail(c, GI_ERR_ARG, "k-NN launch: unsupported estimate size for this kernel");
@@ -1037,6 +1068,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_SPLIT_IND")) c->split_ind = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_DK")) c->use_dk = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_DK")) c->chunk_dk = atoi(s) != 0;
+  if (const char *s = getenv("GI_CHUNK_BIG2")) c->chunk_big2 = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_FB_ALL")) c->chunk_fb_all = atoi(s) != 0;
   if (const char *s = getenv("GI_IND_FRAC")) c->ind_frac = std::min(1.0, std::max(1e-6, atof(s)));
   if (const char *s = getenv("GI_SORT_QUERIES")) c->sort_queries = atoi(s) != 0;
@@ -1051,7 +1083,7 @@ void gi_destroy(gi_ctx *c) {
   DBuf *bufs[] = {&c->d_nodes, &c->d_elems, &c->d_shapes, &c->d_tris, &c->d_mats, &c->d_lights,
                   &c->d_lut, &c->d_stats, &c->spawn, &c->npaths, &c->path_off, &c->base,
                   &c->pixels, &c->rgbf, &c->rgb8, &c->gheap_d2, &c->gheap_idx, &c->qcount,
-                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont, &c->mc_cont, &c->mc_ncont, &c->prim_rgb, &c->fb_list, &c->fb_count, &c->fb_dense, &c->dk_q};
+                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont, &c->mc_cont, &c->mc_ncont, &c->prim_rgb, &c->fb_list, &c->fb_count, &c->fb_dense, &c->fb_list2, &c->fb_count2, &c->fb_dense2, &c->dk_q};
   for (DBuf *b : bufs) b->release();
   for (int l = 0; l < 2; l++) {
     c->qpos[l].release(); c->qshade[l].release(); c->qkey[l].release(); c->qout[l].release();

@@ -1234,7 +1234,7 @@ unsigned knn_chunk_grid(int64_t nq) {
   return (unsigned)(chunks < (1 << 17) ? chunks : (1 << 17));
 }
 
-// large-K chunk kernel (needs a.map.dk); cap = LDS candidates per chunk (384 or 512)
+// large-K chunk kernel (needs a.map.dk); cap = LDS candidates per chunk (384, 512 or 1024)
 bool launch_knn_chunk_big(const KnnArgs &a, int cap, hipStream_t st) {
   if (a.nq == 0) return true;
   if (a.mode == KNN_MODE_LIST || a.mode == KNN_MODE_DK || !a.map.dk) return false;
@@ -1243,9 +1243,12 @@ bool launch_knn_chunk_big(const KnnArgs &a, int cap, hipStream_t st) {
   if (cap <= 384) {
     if (prof) knn_chunk_big_kernel<384, true><<<grid, 64, 0, st>>>(a);
     else knn_chunk_big_kernel<384, false><<<grid, 64, 0, st>>>(a);
-  } else {
+  } else if (cap <= 512) {
     if (prof) knn_chunk_big_kernel<512, true><<<grid, 64, 0, st>>>(a);
     else knn_chunk_big_kernel<512, false><<<grid, 64, 0, st>>>(a);
+  } else {
+    // second pass over the first pass's overflowing chunks: 32 KiB of LDS per wave
+    knn_chunk_big_kernel<1024, false><<<grid, 64, 0, st>>>(a);
   }
   return true;
 }

@@ -198,6 +198,9 @@ struct DevMap {
 struct gi_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;     // side stream: Monte Carlo paths beside the indirect paths
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  bool overlap_mc = true;
   std::string err;
   gi_params P;
   bool have_params = false;
@@ -933,7 +936,7 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
       }
       a.qcount = c->qcount.as<uint32_t>();
       HIPCHK(c, hipMemcpyAsync(c->qcount.p, qbase, 8, hipMemcpyHostToDevice, c->stream));
-      launch_path(a, c->stream);
+      launch_path(a, c->stream, c->overlap_mc ? c->stream2 : nullptr, c->ev_fork, c->ev_join);
       HIPCHK(c, hipGetLastError());
       HIPCHK(c, hipMemcpyAsync(nq, c->qcount.p, 8, hipMemcpyDeviceToHost, c->stream));
       uint32_t fills[IND_QS * 32];
@@ -1039,6 +1042,9 @@ int gi_create(gi_ctx **out, int dev) {
   if (hipSetDevice(dev) != hipSuccess) { delete c; return GI_ERR_HIP; }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return GI_ERR_HIP; }
   hipEventCreate(&c->ev0);
+  if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) c->stream2 = nullptr;
+  hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
+  hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
   hipEventCreate(&c->ev1);
   hipEventCreate(&c->ev2);
   std::vector<double> lut;
@@ -1069,6 +1075,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_KNN_DK")) c->use_dk = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_DK")) c->chunk_dk = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_BIG2")) c->chunk_big2 = atoi(s) != 0;
+  if (const char *s = getenv("GI_OVERLAP_MC")) c->overlap_mc = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_FB_ALL")) c->chunk_fb_all = atoi(s) != 0;
   if (const char *s = getenv("GI_IND_FRAC")) c->ind_frac = std::min(1.0, std::max(1e-6, atof(s)));
   if (const char *s = getenv("GI_SORT_QUERIES")) c->sort_queries = atoi(s) != 0;
@@ -1100,6 +1107,9 @@ void gi_destroy(gi_ctx *c) {
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
   if (c->ev2) hipEventDestroy(c->ev2);
+  if (c->ev_fork) hipEventDestroy(c->ev_fork);
+  if (c->ev_join) hipEventDestroy(c->ev_join);
+  if (c->stream2) hipStreamDestroy(c->stream2);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }

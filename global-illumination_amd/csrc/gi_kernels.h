@@ -175,6 +175,10 @@ __device__ __forceinline__ bool kd_next(const KdNode *nodes, int &node, float qx
   return true;
 }
 
+// pow behind a call: the estimates' specular and Gaussian-filter branches would otherwise inline
+// one fp64 pow per unrolled photon (code size, registers) for paths most scenes never take
+static __device__ __noinline__ double pow_call(double x, double y) { return pow(x, y); }
+
 // d-ary max-heap of u64 keys in LDS laid out [slot][lane] (stride 64): sift-down, Floyd build,
 // and accept (append unordered until K, heapify once, then replace the root)
 template <int ARY>
@@ -303,7 +307,8 @@ struct ScanTemp {
 hipError_t launch_scan(const uint32_t *in, uint32_t *out, int64_t n, ScanTemp &tmp,
                        hipStream_t st);
 void launch_primary(const RenderArgs &a, hipStream_t st);
-void launch_path(const RenderArgs &a, hipStream_t st);
+void launch_path(const RenderArgs &a, hipStream_t st, hipStream_t st2 = nullptr,
+                 hipEvent_t fork = nullptr, hipEvent_t join = nullptr);
 // float4 queries {x, y, z, 0} at the photons of a map (KNN_MODE_DK input)
 void launch_photon_queries(const float *pos4, int64_t n, float4 *q, hipStream_t st);
 // dense copy of the striped chunk fallback list; total length to *total

@@ -1384,7 +1384,37 @@ void launch_cont(const RenderArgs &a, const IndCont *q, const uint32_t *fill, ui
   else
     ind_cont_kernel<KINDS_ALL><<<IND_QS * 32, 128, 0, st>>>(a, q, fill, cap_s);
 }
-void launch_path(const RenderArgs &a, hipStream_t st) {
+// Path expansion of one batch. The Monte Carlo paths (mc_kernel: few, long, one wave per SIMD
+// by its registers) run on the side stream st2 when given, concurrently with the indirect paths
+// on st, so their waves share the CUs instead of running as a low-occupancy tail; st waits for
+// them before returning (fork/join events). The two kernels write disjoint path slots and
+// append queries through the same atomic counters.
+void launch_path(const RenderArgs &a, hipStream_t st, hipStream_t st2, hipEvent_t fork,
+                 hipEvent_t join) {
+  const bool side = st2 && fork && join && a.total_mc > 0;
+  hipStream_t ms = side ? st2 : st;
+  if (side) {
+    (void)hipEventRecord(fork, st);
+    (void)hipStreamWaitEvent(st2, fork, 0);
+  }
+  if (a.total_mc > 0) {
+    unsigned g = nblk(a.total_mc, 128);
+    if (a.mc_cont) (void)hipMemsetAsync(a.mc_ncont, 0, IND_QS * 32 * sizeof(uint32_t), ms);
+    if (a.mc_cont) {
+      if ((a.S.kinds & ~KINDS_TRI_SPHERE) == 0) {
+        if (a.S.hard_lights) mc_kernel<KINDS_TRI_SPHERE, true, true><<<g, 128, 0, ms>>>(a);
+        else mc_kernel<KINDS_TRI_SPHERE, true, false><<<g, 128, 0, ms>>>(a);
+      } else if ((a.S.kinds & ~KINDS_POLY) == 0) {
+        if (a.S.hard_lights) mc_kernel<KINDS_POLY, true, true><<<g, 128, 0, ms>>>(a);
+        else mc_kernel<KINDS_POLY, true, false><<<g, 128, 0, ms>>>(a);
+      } else {
+        mc_kernel<KINDS_ALL, true, false><<<g, 128, 0, ms>>>(a);
+      }
+      launch_cont(a, a.mc_cont, a.mc_ncont, a.mc_cap_s, ms);
+    } else {
+      mc_kernel<KINDS_ALL, false, false><<<g, 128, 0, ms>>>(a);
+    }
+  }
   if (a.nprim > 0) slot0_kernel<<<nblk(a.nprim, 256), 256, 0, st>>>(a);
   if (a.total_ind > 0) {
     unsigned g = nblk(a.total_ind, 128);
@@ -1396,23 +1426,9 @@ void launch_path(const RenderArgs &a, hipStream_t st) {
     // continuations: 32 blocks per stripe stride over its fill
     if (a.split_ind) launch_cont(a, a.ind_cont, a.ind_ncont, a.ind_cap_s, st);
   }
-  if (a.total_mc > 0) {
-    unsigned g = nblk(a.total_mc, 128);
-    if (a.mc_cont) (void)hipMemsetAsync(a.mc_ncont, 0, IND_QS * 32 * sizeof(uint32_t), st);
-    if (a.mc_cont) {
-      if ((a.S.kinds & ~KINDS_TRI_SPHERE) == 0) {
-        if (a.S.hard_lights) mc_kernel<KINDS_TRI_SPHERE, true, true><<<g, 128, 0, st>>>(a);
-        else mc_kernel<KINDS_TRI_SPHERE, true, false><<<g, 128, 0, st>>>(a);
-      } else if ((a.S.kinds & ~KINDS_POLY) == 0) {
-        if (a.S.hard_lights) mc_kernel<KINDS_POLY, true, true><<<g, 128, 0, st>>>(a);
-        else mc_kernel<KINDS_POLY, true, false><<<g, 128, 0, st>>>(a);
-      } else {
-        mc_kernel<KINDS_ALL, true, false><<<g, 128, 0, st>>>(a);
-      }
-      launch_cont(a, a.mc_cont, a.mc_ncont, a.mc_cap_s, st);
-    } else {
-      mc_kernel<KINDS_ALL, false, false><<<g, 128, 0, st>>>(a);
-    }
+  if (side) {
+    (void)hipEventRecord(join, st2);
+    (void)hipStreamWaitEvent(st, join, 0);
   }
 }
 void launch_reduce(const RenderArgs &a, hipStream_t st) {

@@ -208,10 +208,13 @@ __device__ __forceinline__ void wave_estimate(const KnnArgs &a, int64_t qi, floa
       double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
       double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
       bool spec = (m.flags & MF_SPECULAR) || (m.n < 0);
+      // without the specular term, ap * kd + 0 * ks == ap * kd up to the sign of a zero (for
+      // finite ks), and the sums start at +0, so dropping the 0 * ks products changes no result
+      const bool diff_only = !spec && isfinite(m.ks[0]) && isfinite(m.ks[1]) && isfinite(m.ks[2]);
       double c1 = 1.0, c2 = 1.0, tw = 0;
       if (a.filter == 1) c1 = 1.0 / (a.fk * sqrt(maxd2));
       else if (a.filter == 2) {
-        c1 = pow(2.7182818284590452354, -a.fb);
+        c1 = pow_call(2.7182818284590452354, -a.fb);
         c2 = 1.0 / (2.0 * maxd2);
       }
       for (int s = lane; s < num; s += 64) {
@@ -230,15 +233,21 @@ __device__ __forceinline__ void wave_estimate(const KnnArgs &a, int64_t qi, floa
         double ca = E0 * -ix + E1 * -iy + E2 * -iz;
         if (ca < 0) ca = 0;
         double ap = fabs(perp);
-        double pw = spec ? pow(ca, m.n) : 0.0;
-        p0 *= ap * m.kd[0] + pw * m.ks[0];
-        p1 *= ap * m.kd[1] + pw * m.ks[1];
-        p2 *= ap * m.kd[2] + pw * m.ks[2];
+        if (diff_only) {
+          p0 *= ap * m.kd[0];
+          p1 *= ap * m.kd[1];
+          p2 *= ap * m.kd[2];
+        } else {
+          double pw = spec ? pow_call(ca, m.n) : 0.0;
+          p0 *= ap * m.kd[0] + pw * m.ks[0];
+          p1 *= ap * m.kd[1] + pw * m.ks[1];
+          p2 *= ap * m.kd[2] + pw * m.ks[2];
+        }
         if (a.filter == 1) {
           double f = (1.0 - c1 * sqrt(d2));
           p0 *= f; p1 *= f; p2 *= f;
         } else if (a.filter == 2) {
-          double w = (1.0 - (1.0 - pow(c1, c2 * d2)) / (1.0 - c1));
+          double w = (1.0 - (1.0 - pow_call(c1, c2 * d2)) / (1.0 - c1));
           p0 *= w; p1 *= w; p2 *= w;
           tw += w;
         }
@@ -689,10 +698,13 @@ __global__ __launch_bounds__(64) void knn_lane_kernel(KnnArgs a) {
           double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
           double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
           bool spec = (m.flags & MF_SPECULAR) || (m.n < 0);
+          // without the specular term, ap * kd + 0 * ks == ap * kd up to the sign of a zero (for
+          // finite ks), and the sums start at +0, so dropping the 0 * ks products changes no result
+          const bool diff_only = !spec && isfinite(m.ks[0]) && isfinite(m.ks[1]) && isfinite(m.ks[2]);
           double c1 = 1.0, c2 = 1.0, tw = 0;
           if (a.filter == 1) c1 = 1.0 / (a.fk * sqrt(maxd2));
           else if (a.filter == 2) {
-            c1 = pow(2.7182818284590452354, -a.fb);
+            c1 = pow_call(2.7182818284590452354, -a.fb);
             c2 = 1.0 / (2.0 * maxd2);
           }
           for (int s = 0; s < num; s++) {
@@ -712,15 +724,21 @@ __global__ __launch_bounds__(64) void knn_lane_kernel(KnnArgs a) {
             double ca = E0 * -ix + E1 * -iy + E2 * -iz;
             if (ca < 0) ca = 0;
             double ap = fabs(perp);
-            double pw = spec ? pow(ca, m.n) : 0.0;
-            p0 *= ap * m.kd[0] + pw * m.ks[0];
-            p1 *= ap * m.kd[1] + pw * m.ks[1];
-            p2 *= ap * m.kd[2] + pw * m.ks[2];
+            if (diff_only) {
+              p0 *= ap * m.kd[0];
+              p1 *= ap * m.kd[1];
+              p2 *= ap * m.kd[2];
+            } else {
+              double pw = spec ? pow_call(ca, m.n) : 0.0;
+              p0 *= ap * m.kd[0] + pw * m.ks[0];
+              p1 *= ap * m.kd[1] + pw * m.ks[1];
+              p2 *= ap * m.kd[2] + pw * m.ks[2];
+            }
             if (a.filter == 1) {
               double f = (1.0 - c1 * sqrt(d2));
               p0 *= f; p1 *= f; p2 *= f;
             } else if (a.filter == 2) {
-              double w = (1.0 - (1.0 - pow(c1, c2 * d2)) / (1.0 - c1));
+              double w = (1.0 - (1.0 - pow_call(c1, c2 * d2)) / (1.0 - c1));
               p0 *= w; p1 *= w; p2 *= w;
               tw += w;
             }
@@ -908,10 +926,13 @@ __global__ __launch_bounds__(64) void knn_packet_kernel(KnnArgs a) {
           double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
           double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
           bool spec = (m.flags & MF_SPECULAR) || (m.n < 0);
+          // without the specular term, ap * kd + 0 * ks == ap * kd up to the sign of a zero (for
+          // finite ks), and the sums start at +0, so dropping the 0 * ks products changes no result
+          const bool diff_only = !spec && isfinite(m.ks[0]) && isfinite(m.ks[1]) && isfinite(m.ks[2]);
           double c1 = 1.0, c2 = 1.0, tw = 0;
           if (a.filter == 1) c1 = 1.0 / (a.fk * sqrt(maxd2));
           else if (a.filter == 2) {
-            c1 = pow(2.7182818284590452354, -a.fb);
+            c1 = pow_call(2.7182818284590452354, -a.fb);
             c2 = 1.0 / (2.0 * maxd2);
           }
           for (int s = 0; s < num; s++) {
@@ -931,15 +952,21 @@ __global__ __launch_bounds__(64) void knn_packet_kernel(KnnArgs a) {
             double ca = E0 * -ix + E1 * -iy + E2 * -iz;
             if (ca < 0) ca = 0;
             double ap = fabs(perp);
-            double pw = spec ? pow(ca, m.n) : 0.0;
-            p0 *= ap * m.kd[0] + pw * m.ks[0];
-            p1 *= ap * m.kd[1] + pw * m.ks[1];
-            p2 *= ap * m.kd[2] + pw * m.ks[2];
+            if (diff_only) {
+              p0 *= ap * m.kd[0];
+              p1 *= ap * m.kd[1];
+              p2 *= ap * m.kd[2];
+            } else {
+              double pw = spec ? pow_call(ca, m.n) : 0.0;
+              p0 *= ap * m.kd[0] + pw * m.ks[0];
+              p1 *= ap * m.kd[1] + pw * m.ks[1];
+              p2 *= ap * m.kd[2] + pw * m.ks[2];
+            }
             if (a.filter == 1) {
               double f = (1.0 - c1 * sqrt(d2));
               p0 *= f; p1 *= f; p2 *= f;
             } else if (a.filter == 2) {
-              double w = (1.0 - (1.0 - pow(c1, c2 * d2)) / (1.0 - c1));
+              double w = (1.0 - (1.0 - pow_call(c1, c2 * d2)) / (1.0 - c1));
               p0 *= w; p1 *= w; p2 *= w;
               tw += w;
             }

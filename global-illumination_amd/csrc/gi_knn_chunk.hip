@@ -451,10 +451,13 @@ __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, flo
       double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
       double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
       bool spec = (mt.flags & MF_SPECULAR) || (mt.n < 0);
+      // without the specular term, ap * kd + 0 * ks == ap * kd up to the sign of a zero (for
+      // finite ks), and the sums start at +0, so dropping the 0 * ks products changes no result
+      const bool diff_only = !spec && isfinite(mt.ks[0]) && isfinite(mt.ks[1]) && isfinite(mt.ks[2]);
       double c1 = 1.0, c2 = 1.0;
       if (a.filter == 1) c1 = 1.0 / (a.fk * sqrt(maxd2));
       else if (a.filter == 2) {
-        c1 = pow(2.7182818284590452354, -a.fb);
+        c1 = pow_call(2.7182818284590452354, -a.fb);
         c2 = 1.0 / (2.0 * maxd2);
       }
       // photons in groups of EB: the LDS slot reads and direction-LUT loads of a group are
@@ -492,15 +495,21 @@ __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, flo
         double ca = E0 * -ix + E1 * -iy + E2 * -iz;
         if (ca < 0) ca = 0;
         double ap = fabs(perp);
-        double pw = spec ? pow(ca, mt.n) : 0.0;
-        p0 *= ap * mt.kd[0] + pw * mt.ks[0];
-        p1 *= ap * mt.kd[1] + pw * mt.ks[1];
-        p2 *= ap * mt.kd[2] + pw * mt.ks[2];
+        if (diff_only) {
+          p0 *= ap * mt.kd[0];
+          p1 *= ap * mt.kd[1];
+          p2 *= ap * mt.kd[2];
+        } else {
+          double pw = spec ? pow_call(ca, mt.n) : 0.0;
+          p0 *= ap * mt.kd[0] + pw * mt.ks[0];
+          p1 *= ap * mt.kd[1] + pw * mt.ks[1];
+          p2 *= ap * mt.kd[2] + pw * mt.ks[2];
+        }
         if (a.filter == 1) {
           double f = (1.0 - c1 * sqrt(d2));
           p0 *= f; p1 *= f; p2 *= f;
         } else if (a.filter == 2) {
-          double w = (1.0 - (1.0 - pow(c1, c2 * d2)) / (1.0 - c1));
+          double w = (1.0 - (1.0 - pow_call(c1, c2 * d2)) / (1.0 - c1));
           p0 *= w; p1 *= w; p2 *= w;
           tw += w;
         }

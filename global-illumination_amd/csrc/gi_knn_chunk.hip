@@ -570,7 +570,10 @@ __device__ __forceinline__ void chunk_flush_stats(const KnnArgs &a, const ChunkP
 // ---------------------------------------------------------------------------------------------
 // lane select: one query per lane, counting passes over the LDS candidates
 // ---------------------------------------------------------------------------------------------
-constexpr int LS_BR = 4;       // bracket photons resolved by the collect pass
+constexpr int LS_BR = 4;       // bracket photons resolved by the collect pass (large-K kernel)
+#ifndef LS_BR_L
+#define LS_BR_L 12             // the same for the lane-select kernel (bracket kept in its LDS slot list; measured best)
+#endif
 constexpr int LS_PASSES = 10;  // counting passes before a query goes to the fallback
 #ifndef LS_UNROLL
 #define LS_UNROLL 4            // candidates per LDS round trip in the counting / collect loops
@@ -711,8 +714,10 @@ void knn_chunk_lane_kernel(KnnArgs a) {
             } else {
               A = nA;
               B = nB;
-              if (cb <= (uint32_t)LS_BR) mode = 2;
-              else if (!(B > A)) mode = 3;  // more than LS_BR photons tied at one d2
+              // the collect keeps the K - need photons below A at the front of the lane's
+              // slot list and the bracket's cb at its back: both must fit its 64 entries
+              if (cb <= (uint32_t)LS_BR_L && (uint32_t)(K - need) + cb <= 64u) mode = 2;
+              else if (!(B > A)) mode = 3;  // more than LS_BR_L photons tied at one d2
             }
           }
         }
@@ -727,12 +732,10 @@ void knn_chunk_lane_kernel(KnnArgs a) {
       if (P.on) P.c[9] += (uint64_t)__popcll(fbm);
     }
     const bool col = act && !fb && !(a.dbg & 4);
-    // collect: everything below A, and the bracket's photons into a small register buffer
-    int n = 0;
+    // collect: everything below A to the front of the lane's slot list (sel[n][lane]), the
+    // bracket's photons to its back (sel[63 - m][lane]); the bracket is then sorted in registers
+    int n = 0, m = 0;
     float km = 0.0f;
-    uint64_t br[LS_BR];
-#pragma unroll
-    for (int i = 0; i < LS_BR; i++) br[i] = ~0ull;
     const bool inb_on = col && need > 0;
 #pragma unroll LS_UNROLL
     for (uint32_t s = 0; s < count; s++) {
@@ -743,30 +746,34 @@ void knn_chunk_lane_kernel(KnnArgs a) {
         km = fmaxf(km, d2);
       }
       if (inb_on && d2 >= A && d2 <= B) {
-#pragma unroll
-        for (int i = LS_BR - 1; i > 0; i--) br[i] = br[i - 1];
-        br[0] = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)s;
+        sel[(63 - m) * 64 + lane] = (uint8_t)s;
+        m++;
       }
     }
     if (inb_on) {
       // sort the bracket by (d2, kd index) and keep `need` of it
-      uint64_t fk[LS_BR];
-      uint32_t sl[LS_BR];
+      uint64_t fk[LS_BR_L];
+      uint32_t sl[LS_BR_L];
 #pragma unroll
-      for (int i = 0; i < LS_BR; i++) {
-        sl[i] = (uint32_t)br[i];
-        fk[i] = (br[i] == ~0ull) ? ~0ull : ((br[i] & 0xffffffff00000000ull) | (uint64_t)cidx[sl[i] & 255u]);
+      for (int i = 0; i < LS_BR_L; i++) {
+        sl[i] = 0u;
+        fk[i] = ~0ull;
+        if (i < m) {
+          sl[i] = sel[(63 - i) * 64 + lane];
+          float d2 = metric(qx, qy, qz, cpos[sl[i]]);
+          fk[i] = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)cidx[sl[i]];
+        }
       }
 #pragma unroll
-      for (int i = 0; i < LS_BR; i++)
+      for (int i = 0; i < LS_BR_L; i++)
 #pragma unroll
-        for (int j = 0; j + 1 < LS_BR - i; j++)
+        for (int j = 0; j + 1 < LS_BR_L - i; j++)
           if (fk[j + 1] < fk[j]) {
             uint64_t t = fk[j]; fk[j] = fk[j + 1]; fk[j + 1] = t;
             uint32_t u = sl[j]; sl[j] = sl[j + 1]; sl[j + 1] = u;
           }
 #pragma unroll
-      for (int i = 0; i < LS_BR; i++)
+      for (int i = 0; i < LS_BR_L; i++)
         if (i < need) {
           sel[n * 64 + lane] = (uint8_t)sl[i];
           n++;

@@ -18,7 +18,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgi_amd.so")
+LIB_PATH = os.environ.get("GI_AMD_LIB") or os.path.join(_HERE, "libgi_amd.so")  # GI_AMD_LIB: experiment builds
 
 GI_OK, GI_ERR_ARG, GI_ERR_IO, GI_ERR_HIP, GI_ERR_STATE, GI_ERR_UNSUPPORTED, GI_ERR_ALLOC = range(7)
 DISK, CONE, GAUSS = 0, 1, 2

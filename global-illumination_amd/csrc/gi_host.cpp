@@ -240,6 +240,7 @@ struct gi_ctx {
   DBuf fb_list, fb_count, fb_dense;  // chunk k-NN fallback queries (striped, compacted)
   DBuf fb_list2, fb_count2, fb_dense2;  // large-K chunk k-NN: second pass's fallback queries
   bool chunk_big2 = true;            // large-K chunk k-NN: second chunk pass (1024 candidates)
+  int chunk_minsub_big2 = 64;        // ... its overflowing chunks retried down to this group size
   DBuf dk_q;                       // photon positions as queries (ensure_dk)
   bool chunk_dk = true;            // chunk kernel (K <= 64): centre bound from the dk bounds (measured: fewer fallbacks)
   bool chunk_fb_all = false;       // test knob: the lane-select chunk kernel hands every query to its fallback
@@ -631,6 +632,7 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
       s2.fb_count = c->fb_count2.as<uint32_t>();
       s2.fb_cap_s = cap2;
       s2.dbg &= ~16;
+      s2.chunk_minsub = c->chunk_minsub_big2;
       if (!launch_knn_chunk_big(s2, 1024, c->stream))
         return fail(c, GI_ERR_ARG, "k-NN launch: large-K chunk kernel unavailable");
       HIPCHK(c, hipGetLastError());
@@ -1075,6 +1077,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_KNN_DK")) c->use_dk = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_DK")) c->chunk_dk = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_BIG2")) c->chunk_big2 = atoi(s) != 0;
+  if (const char *s = getenv("GI_CHUNK_MINSUB_BIG2")) c->chunk_minsub_big2 = std::min(64, std::max(1, atoi(s)));
   if (const char *s = getenv("GI_OVERLAP_MC")) c->overlap_mc = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_FB_ALL")) c->chunk_fb_all = atoi(s) != 0;
   if (const char *s = getenv("GI_IND_FRAC")) c->ind_frac = std::min(1.0, std::max(1e-6, atof(s)));

@@ -175,12 +175,16 @@ __device__ __forceinline__ bool ray_box(V o, V d, const double *mn, const double
 
 // R3Intersects(ray, triangle) = plane (R3Isect.cpp:700-732) + R3Contains(triangle)
 // (R3Cont.cpp:491-512); edge planes precomputed on the host with the same arithmetic.
-GI_HD bool ray_tri(V o, V d, const DTri &tr, double &t, V &p) {
+// tmax: the caller's current closest t. A plane hit beyond it could not be taken by the caller
+// (R3SceneElement's t <= closest rule), so the containment tests are skipped: same result, less
+// fp64 work.
+GI_HD bool ray_tri(V o, V d, const DTri &tr, double &t, V &p, double tmax = INFINITY) {
   V n = ld3(tr.n);
   double denom = dot(n, d);
   if (isZero(denom)) return false;
   double s = -(dot(o, n) + tr.d) / denom;
   if (isNeg(s)) return false;
+  if (s > tmax) return false;
   V q = o + d * s;
   if (!box_contains(tr.bmin, tr.bmax, q)) return false;
   if (!isZero(q.x * n.x + q.y * n.y + q.z * n.z + tr.d)) return false;
@@ -194,7 +198,7 @@ GI_HD bool ray_tri(V o, V d, const DTri &tr, double &t, V &p) {
 }
 
 // R3Intersects(ray, sphere), R3Isect.cpp:975-1021
-GI_HD bool ray_sphere(V o, V d, V c, double r, double &t, V &p, V &nrm) {
+GI_HD bool ray_sphere(V o, V d, V c, double r, double &t, V &p, V &nrm, double tmax = INFINITY) {
   V v0 = c - o;
   double r2 = r * r;
   double d2 = v0.x * v0.x + v0.y * v0.y + v0.z * v0.z;
@@ -205,6 +209,7 @@ GI_HD bool ray_sphere(V o, V d, V c, double r, double &t, V &p, V &nrm) {
   if (isNeg(disc)) return false;
   double dd = sqrt(disc);
   t = inside ? v + dd : v - dd;
+  if (t > tmax) return false;  // beyond the caller's closest hit (see ray_tri)
   p = o + t * d;
   nrm = (p - c) / r;
   return true;
@@ -331,22 +336,22 @@ constexpr uint32_t KINDS_POLY = (1u << SK_TRI) | (1u << SK_SPHERE) | (1u << SK_M
 // R3TriangleArray) (R3Isect.cpp:800-833): min t over ALL triangles, t >= -1e-6 allowed (Q2).
 template <uint32_t KINDS = KINDS_ALL>
 __device__ __forceinline__ bool shape_intersect(const SceneView &S, const DShape &sh, V o, V d,
-                                             double &t, V &p, V &n) {
+                                             double &t, V &p, V &n, double tmax = INFINITY) {
   if (KINDS == KINDS_TRI_SPHERE) {
     if (sh.kind == SK_TRI) {
       const DTri &tr = S.tris[sh.tri_first];
-      if (!ray_tri(o, d, tr, t, p)) return false;
+      if (!ray_tri(o, d, tr, t, p, tmax)) return false;
       n = ld3(tr.n);
       return true;
     }
-    if (sh.kind == SK_SPHERE) return ray_sphere(o, d, ld3(sh.c), sh.r, t, p, n);
+    if (sh.kind == SK_SPHERE) return ray_sphere(o, d, ld3(sh.c), sh.r, t, p, n, tmax);
     return false;
   }
   if (!(KINDS & KIND_BIT(sh.kind))) return false;
   switch (sh.kind) {
     case SK_TRI: {
       const DTri &tr = S.tris[sh.tri_first];
-      if (!ray_tri(o, d, tr, t, p)) return false;
+      if (!ray_tri(o, d, tr, t, p, tmax)) return false;
       n = ld3(tr.n);
       return true;
     }
@@ -358,7 +363,7 @@ __device__ __forceinline__ bool shape_intersect(const SceneView &S, const DShape
         const DTri &tr = S.tris[sh.tri_first + i];
         double tt;
         V pp;
-        if (ray_tri(o, d, tr, tt, pp)) {
+        if (ray_tri(o, d, tr, tt, pp, tmax)) {  // a mesh hit beyond tmax is not taken either
           if (tt < mt) {
             found = true;
             p = pp;
@@ -371,7 +376,7 @@ __device__ __forceinline__ bool shape_intersect(const SceneView &S, const DShape
       return found;
     }
     case SK_SPHERE:
-      return ray_sphere(o, d, ld3(sh.c), sh.r, t, p, n);
+      return ray_sphere(o, d, ld3(sh.c), sh.r, t, p, n, tmax);
     case SK_BOX: {
       double tt;
       V nn;
@@ -455,7 +460,7 @@ __device__ __forceinline__ bool scene_intersect(const SceneView &S, V org, V dir
       for (int si = 0; si < el.shape_count; si++) {
         double t;
         V p, n;
-        if (shape_intersect<KINDS>(S, S.shapes[el.shape_first + si], lo, ldir, t, p, n)) {
+        if (shape_intersect<KINDS>(S, S.shapes[el.shape_first + si], lo, ldir, t, p, n, ec)) {
           if ((t >= 0.0) && (t <= ec)) {
             ep = p;
             en = n;

@@ -231,6 +231,7 @@ struct gi_ctx {
   DBuf ind_cont, ind_ncont;       // indirect paths that continue past their first bounce
   DBuf mc_cont, mc_ncont;         // Monte Carlo paths' indirect sub-paths
   DBuf prim_rgb;                  // per-primary sums of the reduction
+  DBuf ind_tab, mc_tab;           // path owner tables (owner of path 64k)
   bool split_ind = true;          // continuation queue for indirect paths (else one loop per lane)
   double ind_frac = 0.25;         // continuation queue size, as a fraction of its worst case
   // render scratch
@@ -894,6 +895,17 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     a.total_paths = total_paths;
     a.total_mc = totals[1];
     a.total_ind = totals[2];
+    // owner tables: the path kernels find their waves' primary sample in one load
+    if (a.total_ind > 0) {
+      HIPCHK(c, c->ind_tab.ensure(((size_t)a.total_ind / 64 + 2) * 4));
+      launch_owner_table(c->ind_off.as<uint32_t>(), nprim, c->ind_tab.as<uint32_t>(), c->stream);
+      a.ind_tab = c->ind_tab.as<uint32_t>();
+    }
+    if (a.total_mc > 0) {
+      HIPCHK(c, c->mc_tab.ensure(((size_t)a.total_mc / 64 + 2) * 4));
+      launch_owner_table(c->mc_off.as<uint32_t>(), nprim, c->mc_tab.as<uint32_t>(), c->stream);
+      a.mc_tab = c->mc_tab.as<uint32_t>();
+    }
     HIPCHK(c, c->base.ensure((size_t)total_paths * 24));
     a.base = c->base.as<double>();
     // continuation queue: stripe s takes the appends of waves w with w % IND_QS == s (<= 64
@@ -1093,7 +1105,7 @@ void gi_destroy(gi_ctx *c) {
   DBuf *bufs[] = {&c->d_nodes, &c->d_elems, &c->d_shapes, &c->d_tris, &c->d_mats, &c->d_lights,
                   &c->d_lut, &c->d_stats, &c->spawn, &c->npaths, &c->path_off, &c->base,
                   &c->pixels, &c->rgbf, &c->rgb8, &c->gheap_d2, &c->gheap_idx, &c->qcount,
-                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont, &c->mc_cont, &c->mc_ncont, &c->prim_rgb, &c->fb_list, &c->fb_count, &c->fb_dense, &c->fb_list2, &c->fb_count2, &c->fb_dense2, &c->dk_q};
+                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont, &c->mc_cont, &c->mc_ncont, &c->prim_rgb, &c->ind_tab, &c->mc_tab, &c->fb_list, &c->fb_count, &c->fb_dense, &c->fb_list2, &c->fb_count2, &c->fb_dense2, &c->dk_q};
   for (DBuf *b : bufs) b->release();
   for (int l = 0; l < 2; l++) {
     c->qpos[l].release(); c->qshade[l].release(); c->qkey[l].release(); c->qout[l].release();

@@ -86,6 +86,8 @@ struct RenderArgs {
   const uint32_t *path_off;  // [nprim + 1] exclusive scans of the three counts
   const uint32_t *mc_off;
   const uint32_t *ind_off;
+  const uint32_t *ind_tab;   // [total_ind / 64 + 1] owner of path 64k (owner_table_kernel)
+  const uint32_t *mc_tab;    // same for the Monte Carlo paths
   int64_t total_mc, total_ind;
   int32_t ind_waves;    // occupancy target of the indirect-path kernel (waves per SIMD)
   int32_t dbg;          // diagnostics: 1 = skip the indirect trace, 2 = skip diffuse sampling too
@@ -315,6 +317,7 @@ void launch_photon_queries(const float *pos4, int64_t n, float4 *q, hipStream_t 
 void launch_fb_compact(const uint32_t *list, const uint32_t *count, uint32_t cap_s, uint32_t *dense,
                        uint32_t *total, hipStream_t st);  // slot0 + indirect + Monte Carlo
 void launch_reduce(const RenderArgs &a, hipStream_t st);
+void launch_owner_table(const uint32_t *off, int64_t n, uint32_t *tab, hipStream_t st);
 void launch_segments(const uint64_t *skeys, uint32_t n, uint32_t nprim, uint32_t *seg,
                      hipStream_t st);
 void launch_knn(const KnnArgs &a, bool lds_heap, hipStream_t st);

@@ -409,15 +409,27 @@ __device__ __forceinline__ int64_t scan_owner(const uint32_t *off, int64_t n, in
   return lo;
 }
 
-// scan_owner for a whole wave: one binary search for the wave's first path, then each lane
-// steps forward (a wave's 64 consecutive paths span only a few primary samples)
+// scan_owner for a whole wave: the owner of the wave's first path, then each lane steps forward
+// (a wave's 64 consecutive paths span only a few primary samples). With an owner table
+// (tab[k] = owner of path 64k, owner_table_kernel) the first owner is one load; without it, a
+// binary search (19 dependent loads for 2^19 primaries).
 __device__ __forceinline__ int64_t wave_owner(const uint32_t *off, int64_t n, int64_t t,
-                                              int64_t total) {
+                                              int64_t total, const uint32_t *tab) {
   int64_t t0 = (int64_t)__builtin_amdgcn_readfirstlane((int)t);
   if (t0 > t) t0 = t;
-  int64_t p = scan_owner(off, n, t0 < total ? t0 : total - 1);
+  int64_t p;
+  if (tab) p = (int64_t)tab[t0 >> 6];
+  else p = scan_owner(off, n, t0 < total ? t0 : total - 1);
   while (p + 1 < n && (int64_t)off[p + 1] <= t) p++;
   return p;
+}
+
+// tab[k] = the primary owning path 64k of an exclusive scan off[0..n] (thread per primary)
+__global__ void owner_table_kernel(const uint32_t *off, int64_t n, uint32_t *tab) {
+  int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const uint32_t lo = off[p], hi = off[p + 1];
+  for (uint32_t k = (lo + 63) >> 6; (k << 6) < hi; k++) tab[k] = (uint32_t)p;
 }
 
 __device__ __forceinline__ void path_init(PathCtx &P, const RenderArgs &a, int64_t g, int64_t prim,
@@ -491,7 +503,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void i
   Counts cnt = {0, 0, 0, 0, 0, 0};
   bool queue = false;
   if (t < a.total_ind) {
-    int64_t pb = wave_owner(a.ind_off, a.nprim, t, a.total_ind);
+    int64_t pb = wave_owner(a.ind_off, a.nprim, t, a.total_ind, a.ind_tab);
     int s = (int)(t - a.ind_off[pb]);
     const Spawn &sp = a.spawn[pb];
     int pslot = 1 + sp.n_t + sp.n_s + s;
@@ -629,7 +641,7 @@ __global__ __launch_bounds__(128) void mc_kernel(RenderArgs a) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   Counts cnt = {0, 0, 0, 0, 0, 0};
   if (t < a.total_mc) {
-    int64_t pb = wave_owner(a.mc_off, a.nprim, t, a.total_mc);
+    int64_t pb = wave_owner(a.mc_off, a.nprim, t, a.total_mc, a.mc_tab);
     int s = (int)(t - a.mc_off[pb]);
     const Spawn &sp = a.spawn[pb];
     int64_t g = (int64_t)a.path_off[pb] + 1 + s;
@@ -1430,6 +1442,9 @@ void launch_path(const RenderArgs &a, hipStream_t st, hipStream_t st2, hipEvent_
     (void)hipEventRecord(join, st2);
     (void)hipStreamWaitEvent(st, join, 0);
   }
+}
+void launch_owner_table(const uint32_t *off, int64_t n, uint32_t *tab, hipStream_t st) {
+  if (n > 0) owner_table_kernel<<<nblk(n, 256), 256, 0, st>>>(off, n, tab);
 }
 void launch_reduce(const RenderArgs &a, hipStream_t st) {
   reduce_prim_kernel<<<nblk(a.nprim, 256), 256, 0, st>>>(a);

@@ -159,6 +159,40 @@ __global__ __launch_bounds__(256) void primary_kernel(RenderArgs a) {
   wave_add(&a.stats[ST_INDIRECT], c_ind);
 }
 
+// Out-of-line optics for the path kernels' glass/mirror branches (transcendental-heavy; inlined,
+// they set the register footprint: mc_kernel 294 -> 252 registers, 1 -> 2 waves per SIMD,
+// 2.5x faster; ind_cont_kernel 256 + scratch -> 168 at 3 waves per SIMD). The RNG state is
+// passed by value (a reference would put it in scratch); each sampler draws exactly two
+// numbers, so the caller advances its counter by 2.
+__device__ __noinline__ double reflection_coeff_nc(double ir_air, double ct, double ir_mat) {
+  return reflection_coeff(ir_air, ct, ir_mat);
+}
+__device__ __noinline__ V transmissive_bounce_nc(double ir_air, V n, V view, double ct, double ir_mat) {
+  return transmissive_bounce(ir_air, n, view, ct, ir_mat);
+}
+__device__ __noinline__ V specular_sample_nc(V ex, double nsh, double ct, uint64_t key, uint64_t ctr) {
+  Rng r;
+  r.key = key;
+  r.ctr = ctr;
+  return specular_sample(ex, nsh, ct, r);
+}
+__device__ __noinline__ V diffuse_sample_nc(V n, double ct, uint64_t key, uint64_t ctr) {
+  Rng r;
+  r.key = key;
+  r.ctr = ctr;
+  return diffuse_sample(n, ct, r);
+}
+__device__ __forceinline__ V specular_sample_call(V ex, double nsh, double ct, Rng &rng) {
+  V v = specular_sample_nc(ex, nsh, ct, rng.key, rng.ctr);
+  rng.ctr += 2;
+  return v;
+}
+__device__ __forceinline__ V diffuse_sample_call(V n, double ct, Rng &rng) {
+  V v = diffuse_sample_nc(n, ct, rng.key, rng.ctr);
+  rng.ctr += 2;
+  return v;
+}
+
 struct PathCtx {
   const SceneView *S;
   const Flags *F;
@@ -234,7 +268,7 @@ __device__ __forceinline__ bool ind_shade(PathCtx &P, const Hit &h, V &org, V &d
   V view = normalize(h.p - org);
   double ct = dot(h.n, -view);
   double R = 0;
-  if (!DIFFUSE_ONLY && F.fresnel && (m.flags & MF_TRANSPARENT)) R = reflection_coeff(F.ir_air, ct, m.ir);
+  if (!DIFFUSE_ONLY && F.fresnel && (m.flags & MF_TRANSPARENT)) R = reflection_coeff_nc(F.ir_air, ct, m.ir);
   double pd = m.max_kd, pt = m.max_kt;
   double ps = m.max_ks + R * pt;
   pt *= (1.0 - R);
@@ -250,13 +284,13 @@ __device__ __forceinline__ bool ind_shade(PathCtx &P, const Hit &h, V &org, V &d
   if (DIFFUSE_ONLY) return false;
   V sb;
   if (rnd < pd + pt) {
-    V ex = transmissive_bounce(F.ir_air, h.n, view, ct, m.ir);
-    sb = F.distrib_trans ? specular_sample(ex, m.n, ct, rng) : ex;
+    V ex = transmissive_bounce_nc(F.ir_air, h.n, view, ct, m.ir);
+    sb = F.distrib_trans ? specular_sample_call(ex, m.n, ct, rng) : ex;
     P.cnt.trans++;
     tw *= (1.0 - R) * ldc(m.kt) / pt;
   } else if (rnd < pd + pt + ps) {
     V ex = reflective_bounce(h.n, view, ct);
-    sb = F.distrib_spec ? specular_sample(ex, m.n, ct, rng) : ex;
+    sb = F.distrib_spec ? specular_sample_call(ex, m.n, ct, rng) : ex;
     P.cnt.spec++;
     tw *= (ldc(m.ks) + R * ldc(m.kt)) / ps;
   } else {
@@ -328,7 +362,7 @@ __device__ __forceinline__ void mc_path(PathCtx &P, V org, V dir, Rng &rng, C3 W
     P.base += W * (cb * tw);
     double R = 0;
     if (F.specular && F.transmissive && F.fresnel && (m.flags & MF_TRANSPARENT))
-      R = reflection_coeff(F.ir_air, ct, m.ir);
+      R = reflection_coeff_nc(F.ir_air, ct, m.ir);
     double pd = m.max_kd, pt = m.max_kt;
     double ps = m.max_ks + R * pt;
     pt *= (1.0 - R);
@@ -343,7 +377,7 @@ __device__ __forceinline__ void mc_path(PathCtx &P, V org, V dir, Rng &rng, C3 W
         // IndirectIllumination(inMC): one sample continuing this path's stream. Queued (the
         // path ends here, so its trace is this path's last work and its background term the
         // last addition to the path's sum) and traced compacted in ind_cont_kernel.
-        V s2 = diffuse_sample(h.n, ct, rng);
+        V s2 = diffuse_sample_call(h.n, ct, rng);
         C3 w2 = W * ((kd * kd * tw) / pd);
         if (DEFER) {
           V o2 = h.p + s2 * kEps;
@@ -380,14 +414,14 @@ __device__ __forceinline__ void mc_path(PathCtx &P, V org, V dir, Rng &rng, C3 W
       break;
     } else if (rnd < pd + pt) {
       if (!F.transmissive) break;
-      V ex = transmissive_bounce(F.ir_air, h.n, view, ct, m.ir);
-      sb = F.distrib_trans ? specular_sample(ex, m.n, ct, rng) : ex;
+      V ex = transmissive_bounce_nc(F.ir_air, h.n, view, ct, m.ir);
+      sb = F.distrib_trans ? specular_sample_call(ex, m.n, ct, rng) : ex;
       P.cnt.trans++;
       tw *= (1.0 - R) * ldc(m.kt) / pt;
     } else if (rnd < pd + pt + ps) {
       if (!F.specular) break;
       V ex = reflective_bounce(h.n, view, ct);
-      sb = F.distrib_spec ? specular_sample(ex, m.n, ct, rng) : ex;
+      sb = F.distrib_spec ? specular_sample_call(ex, m.n, ct, rng) : ex;
       P.cnt.spec++;
       tw *= (ldc(m.ks) + R * ldc(m.kt)) / ps;
     } else {
@@ -580,7 +614,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void i
 // first hit, then MonteCarlo_IndirectSample's loop from iteration 1 on; ray entries
 // (mat == -1): the whole loop, its contribution added to the Monte Carlo path's base.
 template <uint32_t KINDS>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2)))
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3)))
 void ind_cont_kernel(RenderArgs a, const IndCont *queue, const uint32_t *fill, uint32_t cap_s) {
   const uint32_t stripe = blockIdx.x % IND_QS, part = blockIdx.x / IND_QS;
   const uint32_t parts = gridDim.x / IND_QS;
@@ -658,9 +692,9 @@ __global__ __launch_bounds__(128) void mc_kernel(RenderArgs a) {
     Rng rng;
     if (s < sp.n_t) {
       rng.init(F.seed, KIND_TRANS, psample, (uint64_t)s);
-      V ex = transmissive_bounce(F.ir_air, n, view, ct, m.ir);
+      V ex = transmissive_bounce_nc(F.ir_air, n, view, ct, m.ir);
       C3 tw = (1.0 - R) * ldc(m.kt);
-      V sb = F.distrib_trans ? specular_sample(ex, m.n, ct, rng) : ex;
+      V sb = F.distrib_trans ? specular_sample_call(ex, m.n, ct, rng) : ex;
       mc_path<KINDS, DEFER, HARD>(P, p + sb * kEps, sb, rng, tw / (double)sp.n_t);
       P.cnt.trans++;
     } else {
@@ -668,7 +702,7 @@ __global__ __launch_bounds__(128) void mc_kernel(RenderArgs a) {
       rng.init(F.seed, KIND_SPEC, psample, (uint64_t)s);
       V ex = reflective_bounce(n, view, ct);
       C3 tw = ldc(m.kt) * R + ldc(m.ks);
-      V sb = F.distrib_spec ? specular_sample(ex, m.n, ct, rng) : ex;
+      V sb = F.distrib_spec ? specular_sample_call(ex, m.n, ct, rng) : ex;
       mc_path<KINDS, DEFER, HARD>(P, p + sb * kEps, sb, rng, tw / (double)sp.n_s);
       P.cnt.spec++;
     }

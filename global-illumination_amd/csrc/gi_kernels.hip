@@ -669,9 +669,12 @@ void ind_cont_kernel(RenderArgs a, const IndCont *queue, const uint32_t *fill, u
   path_stats(a, tot);
 }
 
+#ifndef MC_WPE
+#define MC_WPE 2  // mc_kernel occupancy target (waves per SIMD; 3 measured slower: spills)
+#endif
 // TransmissiveIllumination / SpecularIllumination sample (raytracer.cpp:47-109)
 template <uint32_t KINDS, bool DEFER, bool HARD>
-__global__ __launch_bounds__(128) void mc_kernel(RenderArgs a) {
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(MC_WPE))) void mc_kernel(RenderArgs a) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   Counts cnt = {0, 0, 0, 0, 0, 0};
   if (t < a.total_mc) {

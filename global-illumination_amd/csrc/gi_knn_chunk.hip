@@ -449,7 +449,6 @@ __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, flo
       uint32_t sign = meta & 3u;
       const DMaterial &mt = a.mats[meta >> 2];
       double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
-      double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
       bool spec = (mt.flags & MF_SPECULAR) || (mt.n < 0);
       // without the specular term, ap * kd + 0 * ks == ap * kd up to the sign of a zero (for
       // finite ks), and the sums start at +0, so dropping the 0 * ks products changes no result
@@ -464,6 +463,44 @@ __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, flo
       // issued before its arithmetic (one memory round trip per group, not per photon); the
       // sums still run in photon order
       constexpr int EB = CHUNK_EST_EB;
+      if (a.filter == 0 && diff_only) {
+        // the common case (disk filter, no specular term): neither d2 nor the exact bounce is
+        // needed, so only the direction code (cpos[slot].w) and the rgbe word are read
+        const float *cw = reinterpret_cast<const float *>(cpos) + 3;
+        const double kd0 = mt.kd[0], kd1 = mt.kd[1], kd2 = mt.kd[2];
+        for (int s0 = 0; s0 < num; s0 += EB) {
+          uint32_t eg[EB];
+          double lg[EB][3];
+#pragma unroll
+          for (int u = 0; u < EB; u++) {
+            uint32_t slot = slot_at(s0 + u < num ? s0 + u : s0);
+            eg[u] = crgbe[slot];
+            uint32_t dc = __float_as_uint(cw[4 * slot]) & 0xffffu;
+            lg[u][0] = a.lut[3 * dc];
+            lg[u][1] = a.lut[3 * dc + 1];
+            lg[u][2] = a.lut[3 * dc + 2];
+          }
+#pragma unroll
+          for (int u = 0; u < EB; u++) {
+            if (s0 + u >= num) break;
+            double ix = lg[u][0], iy = lg[u][1], iz = lg[u][2];
+            double perp = N0 * ix + N1 * iy + N2 * iz;
+            if ((sign == 2u && perp < 0) || (sign == 1u && perp > 0)) continue;
+            uint32_t e = eg[u];
+            uint32_t ee = e >> 24;
+            double inv = ee ? ldexp(1.0, (int)ee - 128 - 8) : 0.0;
+            double p0 = ee ? (double)(e & 255u) * inv : 0.0;
+            double p1 = ee ? (double)((e >> 8) & 255u) * inv : 0.0;
+            double p2 = ee ? (double)((e >> 16) & 255u) * inv : 0.0;
+            double ap = fabs(perp);
+            p0 *= ap * kd0;
+            p1 *= ap * kd1;
+            p2 *= ap * kd2;
+            o0 += p0; o1 += p1; o2 += p2;
+          }
+        }
+      } else {
+      const double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
       for (int s0 = 0; s0 < num; s0 += EB) {
       float4 pg[EB];
       uint32_t eg[EB];
@@ -514,6 +551,7 @@ __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, flo
           tw += w;
         }
         o0 += p0; o1 += p1; o2 += p2;
+      }
       }
       }
       bool ok = true;

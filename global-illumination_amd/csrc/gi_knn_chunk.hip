@@ -855,7 +855,9 @@ void knn_chunk_big_kernel(KnnArgs a) {
   __shared__ uint32_t crgbe[CAPC];
   __shared__ uint32_t hist[4];       // unused by the dk bound (chunk_bound_gather signature)
   __shared__ uint32_t stk[64];
-  __shared__ uint32_t selw[NW * 64];  // kept-candidate bitmask, [word][lane]
+  // kept-candidate bitmask [word][lane] during the collect and the estimate; during the counting
+  // passes the lanes' 16 bin counters [bin][lane]
+  __shared__ uint32_t selw[(NW > 16 ? NW : 16) * 64];
   const int lane = threadIdx.x;
   const int K = a.K;
   const int minsub = a.chunk_minsub > 0 ? a.chunk_minsub : 64;
@@ -904,25 +906,20 @@ void knn_chunk_big_kernel(KnnArgs a) {
       if (P.on) P.c[8]++;
       const bool on = mode == 1;
       const float sc = 16.0f / (B - O);
-      uint64_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+#pragma unroll
+      for (int b = 0; b < 16; b++) selw[b * 64 + lane] = 0u;
 #pragma unroll 4
       for (uint32_t s = 0; s < count; s++) {
         float d2 = metric(qx, qy, qz, cpos[s]);
         bool mem = on && d2 >= A && d2 <= B;
         uint32_t b = bin16(d2, O, sc);
-        uint64_t inc = mem ? (1ull << ((b & 3u) << 4)) : 0ull;
-        uint32_t g = b >> 2;
-        w0 += (g == 0) ? inc : 0ull;
-        w1 += (g == 1) ? inc : 0ull;
-        w2 += (g == 2) ? inc : 0ull;
-        w3 += (g == 3) ? inc : 0ull;
+        if (mem) atomicAdd(&selw[b * 64 + lane], 1u);
       }
       if (on) {
         uint32_t before = 0, bs = 16, cb = 0;
 #pragma unroll
         for (int b = 0; b < 16; b++) {
-          uint64_t w = (b < 4) ? w0 : (b < 8) ? w1 : (b < 12) ? w2 : w3;
-          uint32_t c = (uint32_t)((w >> (16 * (b & 3))) & 0xffffull);
+          uint32_t c = selw[b * 64 + lane];
           if (bs == 16) {
             if (before + c >= (uint32_t)need) { bs = (uint32_t)b; cb = c; }
             else before += c;

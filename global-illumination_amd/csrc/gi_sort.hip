@@ -23,13 +23,13 @@ __device__ __forceinline__ uint32_t spread10(uint32_t v) {
 }
 
 __global__ void morton_kernel(const float4 *q, int64_t n, float ox, float oy, float oz,
-                              float sx, float sy, float sz, uint32_t *keys, uint32_t *vals) {
+                              float sx, float sy, float sz, float cmax, uint32_t *keys, uint32_t *vals) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float4 p = q[i];
-  float fx = fminf(fmaxf((p.x - ox) * sx, 0.0f), 1023.0f);
-  float fy = fminf(fmaxf((p.y - oy) * sy, 0.0f), 1023.0f);
-  float fz = fminf(fmaxf((p.z - oz) * sz, 0.0f), 1023.0f);
+  float fx = fminf(fmaxf((p.x - ox) * sx, 0.0f), cmax);
+  float fy = fminf(fmaxf((p.y - oy) * sy, 0.0f), cmax);
+  float fz = fminf(fmaxf((p.z - oz) * sz, 0.0f), cmax);
   keys[i] = (spread10((uint32_t)fx) << 2) | (spread10((uint32_t)fy) << 1) | spread10((uint32_t)fz);
   vals[i] = (uint32_t)i;
 }
@@ -53,21 +53,24 @@ hipError_t morton_order(const float4 *q, int64_t n, const float bmin[3], const f
   if ((e = grow(s.k1, s.k1_cap, b4)) != hipSuccess) return e;
   if ((e = grow(s.v0, s.v0_cap, b4)) != hipSuccess) return e;
   if ((e = grow(s.v1, s.v1_cap, b4)) != hipSuccess) return e;
+  // cells per axis 2^bits (GI_MORTON_BITS, 8..10): the radix sort runs ceil(3 bits / 8) passes
+  static const int bits = getenv("GI_MORTON_BITS") ? std::min(10, std::max(8, atoi(getenv("GI_MORTON_BITS")))) : 10;
+  const float cmax = (float)((1 << bits) - 1);
   float sc[3];
   for (int i = 0; i < 3; i++) {
     float ext = bmax[i] - bmin[i];
-    sc[i] = ext > 0 ? 1023.0f / ext : 0.0f;
+    sc[i] = ext > 0 ? cmax / ext : 0.0f;
   }
   morton_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(
-      q, n, bmin[0], bmin[1], bmin[2], sc[0], sc[1], sc[2], (uint32_t *)s.k0, (uint32_t *)s.v0);
+      q, n, bmin[0], bmin[1], bmin[2], sc[0], sc[1], sc[2], cmax, (uint32_t *)s.k0, (uint32_t *)s.v0);
   size_t tb = 0;
   e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t *)s.k0, (uint32_t *)s.k1,
-                                         (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0, 30,
+                                         (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0, 3 * bits,
                                          st);
   if (e != hipSuccess) return e;
   if ((e = grow(s.tmp, s.tmp_cap, tb + 256)) != hipSuccess) return e;
   e = hipcub::DeviceRadixSort::SortPairs(s.tmp, tb, (const uint32_t *)s.k0, (uint32_t *)s.k1,
-                                         (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0, 30,
+                                         (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0, 3 * bits,
                                          st);
   if (e != hipSuccess) return e;
   *perm_out = (uint32_t *)s.v1;

@@ -195,12 +195,29 @@ struct DevMap {
 }  // namespace
 
 // =======================================================================================
+// Execution state of one photon map's k-NN launches (stream, timing events, scratch). One per
+// map, so the two maps' estimates can run concurrently on two streams during a render.
+struct MapExec {
+  hipStream_t st = nullptr;        // the ctx stream, or the side stream while maps overlap
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;  // launch / fallback split timing
+  SortScratch sorter;              // Morton order of the query list
+  DBuf list_idx, list_d2, list_n;  // K-best lists of the query-per-wave k-NN path
+  DBuf gheap_d2, gheap_idx;        // global-memory heaps (K > 64 per-lane kernel)
+  DBuf fb_list, fb_count, fb_dense;     // chunk k-NN fallback queries (striped, compacted)
+  DBuf fb_list2, fb_count2, fb_dense2;  // large-K chunk k-NN: second pass's fallback queries
+  DBuf dk_q;                       // photon positions as queries (ensure_dk)
+  uint64_t fb_total = 0;
+};
+
 struct gi_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;     // side stream: Monte Carlo paths beside the indirect paths
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;  // caustic k-NN on the side stream
   bool overlap_mc = true;
+  bool overlap_maps = true;         // caustic k-NN on the side stream beside the global k-NN
+  MapExec mx[2];
   std::string err;
   gi_params P;
   bool have_params = false;
@@ -218,7 +235,6 @@ struct gi_ctx {
   int chunk_cap_big = 512;        // large-K chunk kernel: the same (384 or 512)
   int chunk_minsub_big = 64;      // large-K chunk kernel: overflowing chunks retried down to this (64: none, measured best)
   int chunk_minsub = 32;          // chunk kernel: overflowing chunks retried as halves (measured best with the dk bound)
-  hipEvent_t ev2 = nullptr;       // chunk kernel / fallback split
   double fb_ms[2] = {0, 0};       // fallback time and queries per map (since the last reset)
   uint64_t fb_q[2] = {0, 0};
   int sel_slack = 64;
@@ -235,18 +251,13 @@ struct gi_ctx {
   bool split_ind = true;          // continuation queue for indirect paths (else one loop per lane)
   double ind_frac = 0.25;         // continuation queue size, as a fraction of its worst case
   // render scratch
-  DBuf spawn, npaths, path_off, nmc, mc_off, nind, ind_off, base, pixels, rgbf, rgb8, gheap_d2, gheap_idx, qcount, stats_bak;
+  DBuf spawn, npaths, path_off, nmc, mc_off, nind, ind_off, base, pixels, rgbf, rgb8, qcount, stats_bak;
   DBuf qpos[2], qshade[2], qkey[2], qout[2];
-  DBuf list_idx, list_d2, list_n;
-  DBuf fb_list, fb_count, fb_dense;  // chunk k-NN fallback queries (striped, compacted)
-  DBuf fb_list2, fb_count2, fb_dense2;  // large-K chunk k-NN: second pass's fallback queries
   bool chunk_big2 = true;            // large-K chunk k-NN: second chunk pass (1024 candidates)
   int chunk_minsub_big2 = 64;        // ... its overflowing chunks retried down to this group size
-  DBuf dk_q;                       // photon positions as queries (ensure_dk)
   bool chunk_dk = true;            // chunk kernel (K <= 64): centre bound from the dk bounds (measured: fewer fallbacks)
   bool chunk_fb_all = false;       // test knob: the lane-select chunk kernel hands every query to its fallback
   bool use_dk = true;              // wave k-NN kernel starts from per-photon K-th bounds
-  uint64_t fb_total = 0;
   DBuf qseg[2];  // K-best lists of the query-per-wave k-NN path
   size_t qcap_hint[2] = {0, 0};
   KeySortScratch keysort[2];
@@ -255,10 +266,8 @@ struct gi_ctx {
   // photon tracing scratch
   DBuf pcounts, poffs, pbuf;
   int64_t prim_per_batch = 1 << 19;  // denser query batches: fewer chunk k-NN overflows (measured best)
-  SortScratch sorter;
   bool sort_queries = true;
   float sbmin[3] = {0, 0, 0}, sbmax[3] = {1, 1, 1};
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
 #define HIPCHK(ctx, call)                                                        \
@@ -539,18 +548,19 @@ KnnArgs knn_args(gi_ctx *c, int mi) {
 // per map and (K, r). The wave kernel then starts each query from the bound of the photons in
 // its leaf instead of from r.
 int ensure_dk(gi_ctx *c, KnnArgs &k) {
+  MapExec &X = c->mx[k.stat_off ? 1 : 0];
   int mi = k.stat_off ? 1 : 0;
   DevMap &D = c->dmap[mi];
   if (!c->use_dk || D.n == 0 || k.K <= 0) return GI_OK;
   if (D.dk_k != k.K || D.dk_r2 != k.r2f) {
     D.dk_k = -1;
-    HIPCHK(c, c->dk_q.ensure((size_t)D.n * 16));
+    HIPCHK(c, X.dk_q.ensure((size_t)D.n * 16));
     HIPCHK(c, D.dk.ensure((size_t)D.n * 4));
-    launch_photon_queries(D.pos4.as<float>(), D.n, c->dk_q.as<float4>(), c->stream);
+    launch_photon_queries(D.pos4.as<float>(), D.n, X.dk_q.as<float4>(), X.st);
     KnnArgs d = k;
     d.mode = KNN_MODE_DK;
     d.map.dk = nullptr;
-    d.qpos = c->dk_q.as<float4>();
+    d.qpos = X.dk_q.as<float4>();
     d.qshade = nullptr;
     d.perm = nullptr;
     d.nq = D.n;
@@ -558,10 +568,10 @@ int ensure_dk(gi_ctx *c, KnnArgs &k) {
     d.out_dk = D.dk.as<float>();
     d.stats = nullptr;
     d.dbg = 0;
-    if (!launch_knn_wave(d, c->wave_cap_mul, c->stream))
+    if (!launch_knn_wave(d, c->wave_cap_mul, X.st))
       return fail(c, GI_ERR_ARG, "k-NN bound pass: unsupported estimate size");
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipStreamSynchronize(X.st));
     D.dk_k = k.K;
     D.dk_r2 = k.r2f;
   }
@@ -571,6 +581,7 @@ int ensure_dk(gi_ctx *c, KnnArgs &k) {
 
 // run a k-NN launch over nq queries (chunked when the heap lives in global scratch)
 int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
+  MapExec &X = c->mx[k.stat_off ? 1 : 0];
   // auto (-1): chunk kernel with lane select (+ per-lane fallback) for K <= 64, the per-lane
   // kernel for list mode, one query per wave beyond (measured)
   int kind = c->knn_kernel_kind;
@@ -591,28 +602,28 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
     int64_t chunks = (nq + 63) / 64;
     int64_t grid = knn_chunk_grid(nq);
     uint32_t cap_s = (uint32_t)(64 * ((chunks + grid - 1) / grid) * ((grid + FB_QS - 1) / FB_QS));
-    HIPCHK(c, c->fb_list.ensure((size_t)FB_QS * cap_s * 4));
-    HIPCHK(c, c->fb_dense.ensure((size_t)nq * 4 + 4));
-    HIPCHK(c, c->fb_count.ensure(FB_QS * 32 * 4));
-    HIPCHK(c, hipMemsetAsync(c->fb_count.p, 0, FB_QS * 32 * 4, c->stream));
+    HIPCHK(c, X.fb_list.ensure((size_t)FB_QS * cap_s * 4));
+    HIPCHK(c, X.fb_dense.ensure((size_t)nq * 4 + 4));
+    HIPCHK(c, X.fb_count.ensure(FB_QS * 32 * 4));
+    HIPCHK(c, hipMemsetAsync(X.fb_count.p, 0, FB_QS * 32 * 4, X.st));
     k.nq = nq;
     k.q0 = 0;
-    k.fb_list = c->fb_list.as<uint32_t>();
-    k.fb_count = c->fb_count.as<uint32_t>();
+    k.fb_list = X.fb_list.as<uint32_t>();
+    k.fb_count = X.fb_count.as<uint32_t>();
     k.fb_cap_s = cap_s;
     k.chunk_minsub = c->chunk_minsub_big;
-    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    if (!launch_knn_chunk_big(k, c->chunk_cap_big, c->stream))
+    HIPCHK(c, hipEventRecord(X.ev0, X.st));
+    if (!launch_knn_chunk_big(k, c->chunk_cap_big, X.st))
       return fail(c, GI_ERR_ARG, "k-NN launch: large-K chunk kernel unavailable");
     HIPCHK(c, hipGetLastError());
-    uint32_t *dense = c->fb_dense.as<uint32_t>();
-    launch_fb_compact(k.fb_list, k.fb_count, cap_s, dense, dense + nq, c->stream);
+    uint32_t *dense = X.fb_dense.as<uint32_t>();
+    launch_fb_compact(k.fb_list, k.fb_count, cap_s, dense, dense + nq, X.st);
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipEventRecord(c->ev2, c->stream));
+    HIPCHK(c, hipEventRecord(X.ev2, X.st));
     uint32_t nfb = 0;
-    HIPCHK(c, hipMemcpyAsync(&nfb, dense + nq, 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    c->fb_total += nfb;
+    HIPCHK(c, hipMemcpyAsync(&nfb, dense + nq, 4, hipMemcpyDeviceToHost, X.st));
+    HIPCHK(c, hipStreamSynchronize(X.st));
+    X.fb_total += nfb;
     uint32_t nfb2 = nfb;
     if (nfb && c->chunk_big2) {
       // second chunk pass with 1024 LDS candidates over the overflowing chunks' queries (the
@@ -621,43 +632,43 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
       int64_t chunks2 = ((int64_t)nfb + 63) / 64;
       int64_t grid2 = knn_chunk_grid(nfb);
       uint32_t cap2 = (uint32_t)(64 * ((chunks2 + grid2 - 1) / grid2) * ((grid2 + FB_QS - 1) / FB_QS));
-      HIPCHK(c, c->fb_list2.ensure((size_t)FB_QS * cap2 * 4));
-      HIPCHK(c, c->fb_dense2.ensure((size_t)nfb * 4 + 4));
-      HIPCHK(c, c->fb_count2.ensure(FB_QS * 32 * 4));
-      HIPCHK(c, hipMemsetAsync(c->fb_count2.p, 0, FB_QS * 32 * 4, c->stream));
+      HIPCHK(c, X.fb_list2.ensure((size_t)FB_QS * cap2 * 4));
+      HIPCHK(c, X.fb_dense2.ensure((size_t)nfb * 4 + 4));
+      HIPCHK(c, X.fb_count2.ensure(FB_QS * 32 * 4));
+      HIPCHK(c, hipMemsetAsync(X.fb_count2.p, 0, FB_QS * 32 * 4, X.st));
       KnnArgs s2 = k;
       s2.perm = dense;
       s2.nq = nfb;
       s2.q0 = 0;
-      s2.fb_list = c->fb_list2.as<uint32_t>();
-      s2.fb_count = c->fb_count2.as<uint32_t>();
+      s2.fb_list = X.fb_list2.as<uint32_t>();
+      s2.fb_count = X.fb_count2.as<uint32_t>();
       s2.fb_cap_s = cap2;
       s2.dbg &= ~16;
       s2.chunk_minsub = c->chunk_minsub_big2;
-      if (!launch_knn_chunk_big(s2, 1024, c->stream))
+      if (!launch_knn_chunk_big(s2, 1024, X.st))
         return fail(c, GI_ERR_ARG, "k-NN launch: large-K chunk kernel unavailable");
       HIPCHK(c, hipGetLastError());
-      dense = c->fb_dense2.as<uint32_t>();
-      launch_fb_compact(s2.fb_list, s2.fb_count, cap2, dense, dense + nfb, c->stream);
+      dense = X.fb_dense2.as<uint32_t>();
+      launch_fb_compact(s2.fb_list, s2.fb_count, cap2, dense, dense + nfb, X.st);
       HIPCHK(c, hipGetLastError());
-      HIPCHK(c, hipMemcpyAsync(&nfb2, dense + nfb, 4, hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(c, hipStreamSynchronize(c->stream));
+      HIPCHK(c, hipMemcpyAsync(&nfb2, dense + nfb, 4, hipMemcpyDeviceToHost, X.st));
+      HIPCHK(c, hipStreamSynchronize(X.st));
     }
     if (nfb2) {
       KnnArgs f = k;
       f.perm = dense;
       f.nq = nfb2;
       f.q0 = 0;
-      if (!launch_knn_wave(f, c->wave_cap_mul, c->stream))
+      if (!launch_knn_wave(f, c->wave_cap_mul, X.st))
         return fail(c, GI_ERR_ARG, "k-NN launch: unsupported estimate size for this kernel");
       HIPCHK(c, hipGetLastError());
     }
-    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipEventRecord(X.ev1, X.st));
     if (ms) {
-      HIPCHK(c, hipEventSynchronize(c->ev1));
+      HIPCHK(c, hipEventSynchronize(X.ev1));
       float t = 0, tf = 0;
-      HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
-      HIPCHK(c, hipEventElapsedTime(&tf, c->ev2, c->ev1));
+      HIPCHK(c, hipEventElapsedTime(&t, X.ev0, X.ev1));
+      HIPCHK(c, hipEventElapsedTime(&tf, X.ev2, X.ev1));
       *ms += t;
       int mi = k.stat_off ? 1 : 0;
       c->fb_ms[mi] += tf;
@@ -672,14 +683,14 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
     int64_t chunks = (nq + 63) / 64;
     int64_t grid = knn_chunk_grid(nq);
     uint32_t cap_s = (uint32_t)(64 * ((chunks + grid - 1) / grid) * ((grid + FB_QS - 1) / FB_QS));
-    HIPCHK(c, c->fb_list.ensure((size_t)FB_QS * cap_s * 4));
-    HIPCHK(c, c->fb_dense.ensure((size_t)nq * 4 + 4));
-    HIPCHK(c, c->fb_count.ensure(FB_QS * 32 * 4));
-    HIPCHK(c, hipMemsetAsync(c->fb_count.p, 0, FB_QS * 32 * 4, c->stream));
+    HIPCHK(c, X.fb_list.ensure((size_t)FB_QS * cap_s * 4));
+    HIPCHK(c, X.fb_dense.ensure((size_t)nq * 4 + 4));
+    HIPCHK(c, X.fb_count.ensure(FB_QS * 32 * 4));
+    HIPCHK(c, hipMemsetAsync(X.fb_count.p, 0, FB_QS * 32 * 4, X.st));
     k.nq = nq;
     k.q0 = 0;
-    k.fb_list = c->fb_list.as<uint32_t>();
-    k.fb_count = c->fb_count.as<uint32_t>();
+    k.fb_list = X.fb_list.as<uint32_t>();
+    k.fb_count = X.fb_count.as<uint32_t>();
     k.fb_cap_s = cap_s;
     // per-photon K-th distance bounds: the fallback's starting bound; the chunk kernel's centre
     // bound uses them only with chunk_dk (else the exact d_K(c) gather)
@@ -692,33 +703,33 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
     }
     const int dbg0 = k.dbg;
     if (c->chunk_fb_all && kind == 7) k.dbg |= 4;  // lane select skipped: all to the fallback
-    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    launch_knn_chunk(k, c->chunk_cap, kind - 5, c->stream);
+    HIPCHK(c, hipEventRecord(X.ev0, X.st));
+    launch_knn_chunk(k, c->chunk_cap, kind - 5, X.st);
     k.dbg = dbg0;
     HIPCHK(c, hipGetLastError());
-    uint32_t *dense = c->fb_dense.as<uint32_t>();
-    launch_fb_compact(k.fb_list, k.fb_count, cap_s, dense, dense + nq, c->stream);
+    uint32_t *dense = X.fb_dense.as<uint32_t>();
+    launch_fb_compact(k.fb_list, k.fb_count, cap_s, dense, dense + nq, X.st);
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipEventRecord(c->ev2, c->stream));
+    HIPCHK(c, hipEventRecord(X.ev2, X.st));
     uint32_t nfb = 0;
-    HIPCHK(c, hipMemcpyAsync(&nfb, dense + nq, 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    c->fb_total += nfb;
+    HIPCHK(c, hipMemcpyAsync(&nfb, dense + nq, 4, hipMemcpyDeviceToHost, X.st));
+    HIPCHK(c, hipStreamSynchronize(X.st));
+    X.fb_total += nfb;
     if (nfb) {
       KnnArgs f = k;
       f.perm = dense;
       f.nq = nfb;
       f.q0 = 0;
       f.map.dk = fb_dk;
-      launch_knn_lane(f, c->lane_chunk, c->heap_arity, c->stream);
+      launch_knn_lane(f, c->lane_chunk, c->heap_arity, X.st);
       HIPCHK(c, hipGetLastError());
     }
-    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipEventRecord(X.ev1, X.st));
     if (ms) {
-      HIPCHK(c, hipEventSynchronize(c->ev1));
+      HIPCHK(c, hipEventSynchronize(X.ev1));
       float t = 0, tf = 0;
-      HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
-      HIPCHK(c, hipEventElapsedTime(&tf, c->ev2, c->ev1));
+      HIPCHK(c, hipEventElapsedTime(&t, X.ev0, X.ev1));
+      HIPCHK(c, hipEventElapsedTime(&tf, X.ev2, X.ev1));
       *ms += t;
       int mi = k.stat_off ? 1 : 0;
       c->fb_ms[mi] += tf;
@@ -729,14 +740,14 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
   if (kind == 3 && (size_t)k.K * 512 <= 64 * 1024) {
     k.nq = nq;
     k.q0 = 0;
-    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    launch_knn_lane(k, c->lane_chunk, c->heap_arity, c->stream);
+    HIPCHK(c, hipEventRecord(X.ev0, X.st));
+    launch_knn_lane(k, c->lane_chunk, c->heap_arity, X.st);
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipEventRecord(X.ev1, X.st));
     if (ms) {
-      HIPCHK(c, hipEventSynchronize(c->ev1));
+      HIPCHK(c, hipEventSynchronize(X.ev1));
       float t = 0;
-      HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+      HIPCHK(c, hipEventElapsedTime(&t, X.ev0, X.ev1));
       *ms += t;
     }
     return GI_OK;
@@ -752,32 +763,32 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
         k.list_n = k.out_n;
       } else {
         size_t slots = (size_t)nq * (size_t)k.K;
-        HIPCHK(c, c->list_idx.ensure(slots * 4));
-        HIPCHK(c, c->list_d2.ensure(slots * 4));
-        HIPCHK(c, c->list_n.ensure((size_t)nq * 4));
-        k.list_idx = c->list_idx.as<int32_t>();
-        k.list_d2 = c->list_d2.as<float>();
-        k.list_n = c->list_n.as<int32_t>();
+        HIPCHK(c, X.list_idx.ensure(slots * 4));
+        HIPCHK(c, X.list_d2.ensure(slots * 4));
+        HIPCHK(c, X.list_n.ensure((size_t)nq * 4));
+        k.list_idx = X.list_idx.as<int32_t>();
+        k.list_d2 = X.list_d2.as<float>();
+        k.list_n = X.list_n.as<int32_t>();
       }
     }
     if (kind == 1) {
       int rc = ensure_dk(c, k);
       if (rc) return rc;
     }
-    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    HIPCHK(c, hipEventRecord(X.ev0, X.st));
     bool ok = true;
-    if (kind == 2) ok = launch_knn_packet(k, c->stream);
+    if (kind == 2) ok = launch_knn_packet(k, X.st);
     else if (kind == 4)
-      ok = launch_knn_group(k, c->group_lanes, c->stream) ||
-           launch_knn_wave(k, c->wave_cap_mul, c->stream);  // K too large for the groups
-    else ok = launch_knn_wave(k, c->wave_cap_mul, c->stream);
+      ok = launch_knn_group(k, c->group_lanes, X.st) ||
+           launch_knn_wave(k, c->wave_cap_mul, X.st);  // K too large for the groups
+    else ok = launch_knn_wave(k, c->wave_cap_mul, X.st);
     if (!ok) return fail(c, GI_ERR_ARG, "k-NN launch: unsupported estimate size for this kernel");
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipEventRecord(X.ev1, X.st));
     if (ms) {
-      HIPCHK(c, hipEventSynchronize(c->ev1));
+      HIPCHK(c, hipEventSynchronize(X.ev1));
       float t = 0;
-      HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+      HIPCHK(c, hipEventElapsedTime(&t, X.ev0, X.ev1));
       *ms += t;
     }
     return GI_OK;
@@ -791,19 +802,19 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
     a.q0 = s;
     if (!lds) {
       size_t slots = (size_t)((m + 63) / 64) * 64 * (size_t)k.K;
-      HIPCHK(c, c->gheap_d2.ensure(slots * 4));
-      HIPCHK(c, c->gheap_idx.ensure(slots * 4));
-      a.gheap_d2 = c->gheap_d2.as<float>();
-      a.gheap_idx = c->gheap_idx.as<int32_t>();
+      HIPCHK(c, X.gheap_d2.ensure(slots * 4));
+      HIPCHK(c, X.gheap_idx.ensure(slots * 4));
+      a.gheap_d2 = X.gheap_d2.as<float>();
+      a.gheap_idx = X.gheap_idx.as<int32_t>();
     }
-    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    launch_knn(a, lds, c->stream);
+    HIPCHK(c, hipEventRecord(X.ev0, X.st));
+    launch_knn(a, lds, X.st);
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipEventRecord(X.ev1, X.st));
     if (ms) {
-      HIPCHK(c, hipEventSynchronize(c->ev1));
+      HIPCHK(c, hipEventSynchronize(X.ev1));
       float t = 0;
-      HIPCHK(c, hipEventElapsedTime(&t, c->ev0, c->ev1));
+      HIPCHK(c, hipEventElapsedTime(&t, X.ev0, X.ev1));
       *ms += t;
     }
   }
@@ -813,6 +824,7 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
 // run the k-NN estimate of one query list into out[slot] (Morton-ordered launch)
 int knn_list(gi_ctx *c, int mi, const float4 *qpos, const QShade *qshade, int64_t nq,
              double *out, double *ms) {
+  MapExec &X = c->mx[mi];
   KnnArgs k = knn_args(c, mi);
   k.qpos = qpos;
   k.qshade = qshade;
@@ -820,11 +832,11 @@ int knn_list(gi_ctx *c, int mi, const float4 *qpos, const QShade *qshade, int64_
   k.nq = nq;
   if (c->sort_queries) {
     uint32_t *perm = nullptr;
-    HIPCHK(c, morton_order(qpos, nq, c->sbmin, c->sbmax, c->sorter, &perm, c->stream));
+    HIPCHK(c, morton_order(qpos, nq, c->sbmin, c->sbmax, X.sorter, &perm, X.st));
     k.perm = perm;
   }
   if (c->P.irradiance_cache && mi == GI_MAP_GLOBAL) {
-    launch_cached(k, c->stream);
+    launch_cached(k, X.st);
     HIPCHK(c, hipGetLastError());
     return GI_OK;
   }
@@ -975,6 +987,7 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     // deterministic slots (a primary's own query at slot b; indirect path t's at qind_base + t)
     // are already in (primary, slot-in-primary) order; only the Monte Carlo appends after
     // qbase[l] are key-sorted and indexed per primary (CSR over the sorted keys).
+    bool run[2] = {false, false};
     for (int l = 0; l < 2; l++) {
       a.nq[l] = nq[l];
       a.qapp[l] = qbase[l];
@@ -982,15 +995,48 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
       if (nq[l]) {
         HIPCHK(c, c->qout[l].ensure((size_t)nq[l] * 24));
         a.qout[l] = c->qout[l].as<double>();
-        if (!c->map_valid[l]) {
+        if (!c->map_valid[l])
           HIPCHK(c, hipMemsetAsync(c->qout[l].p, 0, (size_t)nq[l] * 24, c->stream));
-        } else {
-          int rc = knn_list(c, l, a.qpos[l], a.qshade[l], nq[l], c->qout[l].as<double>(),
-                            rs ? &knn_ms[l] : nullptr);
-          if (rc) return rc;
-          launches[l]++;
-        }
+        else
+          run[l] = true;
       }
+    }
+    // The two maps' estimates are independent (own query lists, maps and outputs): the caustic
+    // one runs in a worker thread on the side stream while this thread drives the global one,
+    // so each map's low-occupancy phases (fallbacks, second chunk pass) overlap the other's
+    // kernels. Each map has its own stream, events and scratch (MapExec).
+    const bool side = c->overlap_maps && c->stream2 && run[0] && run[1];
+    int rcm[2] = {GI_OK, GI_OK};
+    std::thread worker;
+    if (side) {
+      HIPCHK(c, hipEventRecord(c->ev_fork2, c->stream));
+      HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork2, 0));
+      c->mx[1].st = c->stream2;
+      worker = std::thread([&]() {
+        hipSetDevice(c->device);  // the current device is per host thread
+        rcm[1] = knn_list(c, 1, a.qpos[1], a.qshade[1], nq[1], c->qout[1].as<double>(),
+                          rs ? &knn_ms[1] : nullptr);
+      });
+    }
+    for (int l = 0; l < 2; l++) {
+      if (!run[l] || (side && l == 1)) continue;
+      rcm[l] = knn_list(c, l, a.qpos[l], a.qshade[l], nq[l], c->qout[l].as<double>(),
+                        rs ? &knn_ms[l] : nullptr);
+      if (rcm[l]) break;
+    }
+    if (side) {
+      worker.join();
+      c->mx[1].st = c->stream;
+      if (rcm[1] == GI_OK) {
+        HIPCHK(c, hipEventRecord(c->ev_join2, c->stream2));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join2, 0));
+      }
+    }
+    for (int l = 0; l < 2; l++) {
+      if (rcm[l]) return rcm[l];
+      if (run[l]) launches[l]++;
+    }
+    for (int l = 0; l < 2; l++) {
       HIPCHK(c, c->qseg[l].ensure((size_t)(nprim + 1) * 4));
       a.qseg[l] = c->qseg[l].as<uint32_t>();
       const int64_t napp = (int64_t)nq[l] - (int64_t)qbase[l];
@@ -1055,12 +1101,17 @@ int gi_create(gi_ctx **out, int dev) {
   gi_params_default(&c->P);
   if (hipSetDevice(dev) != hipSuccess) { delete c; return GI_ERR_HIP; }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return GI_ERR_HIP; }
-  hipEventCreate(&c->ev0);
   if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) c->stream2 = nullptr;
   hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
   hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
-  hipEventCreate(&c->ev1);
-  hipEventCreate(&c->ev2);
+  hipEventCreateWithFlags(&c->ev_fork2, hipEventDisableTiming);
+  hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming);
+  for (int m = 0; m < 2; m++) {
+    c->mx[m].st = c->stream;
+    hipEventCreate(&c->mx[m].ev0);
+    hipEventCreate(&c->mx[m].ev1);
+    hipEventCreate(&c->mx[m].ev2);
+  }
   std::vector<double> lut;
   build_lut(lut);
   if (upload(c->d_lut, lut.data(), lut.size() * 8, c->stream) != hipSuccess ||
@@ -1091,6 +1142,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_CHUNK_BIG2")) c->chunk_big2 = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_MINSUB_BIG2")) c->chunk_minsub_big2 = std::min(64, std::max(1, atoi(s)));
   if (const char *s = getenv("GI_OVERLAP_MC")) c->overlap_mc = atoi(s) != 0;
+  if (const char *s = getenv("GI_OVERLAP_MAPS")) c->overlap_maps = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_FB_ALL")) c->chunk_fb_all = atoi(s) != 0;
   if (const char *s = getenv("GI_IND_FRAC")) c->ind_frac = std::min(1.0, std::max(1e-6, atof(s)));
   if (const char *s = getenv("GI_SORT_QUERIES")) c->sort_queries = atoi(s) != 0;
@@ -1104,9 +1156,19 @@ void gi_destroy(gi_ctx *c) {
   hipSetDevice(c->device);
   DBuf *bufs[] = {&c->d_nodes, &c->d_elems, &c->d_shapes, &c->d_tris, &c->d_mats, &c->d_lights,
                   &c->d_lut, &c->d_stats, &c->spawn, &c->npaths, &c->path_off, &c->base,
-                  &c->pixels, &c->rgbf, &c->rgb8, &c->gheap_d2, &c->gheap_idx, &c->qcount,
-                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont, &c->mc_cont, &c->mc_ncont, &c->prim_rgb, &c->ind_tab, &c->mc_tab, &c->fb_list, &c->fb_count, &c->fb_dense, &c->fb_list2, &c->fb_count2, &c->fb_dense2, &c->dk_q};
+                  &c->pixels, &c->rgbf, &c->rgb8, &c->qcount,
+                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont, &c->mc_cont, &c->mc_ncont, &c->prim_rgb, &c->ind_tab, &c->mc_tab};
   for (DBuf *b : bufs) b->release();
+  for (int m = 0; m < 2; m++) {
+    MapExec &X = c->mx[m];
+    DBuf *xb[] = {&X.list_idx, &X.list_d2, &X.list_n, &X.gheap_d2, &X.gheap_idx, &X.fb_list, &X.fb_count,
+                  &X.fb_dense, &X.fb_list2, &X.fb_count2, &X.fb_dense2, &X.dk_q};
+    for (DBuf *b : xb) b->release();
+    sort_scratch_release(X.sorter);
+    if (X.ev0) hipEventDestroy(X.ev0);
+    if (X.ev1) hipEventDestroy(X.ev1);
+    if (X.ev2) hipEventDestroy(X.ev2);
+  }
   for (int l = 0; l < 2; l++) {
     c->qpos[l].release(); c->qshade[l].release(); c->qkey[l].release(); c->qout[l].release();
     sort_scratch_release(c->keysort[l]);
@@ -1118,11 +1180,9 @@ void gi_destroy(gi_ctx *c) {
     c->dmap[m].nodes.release();
     c->dmap[m].dk.release();
   }
-  sort_scratch_release(c->sorter);
-  if (c->ev0) hipEventDestroy(c->ev0);
-  if (c->ev1) hipEventDestroy(c->ev1);
-  if (c->ev2) hipEventDestroy(c->ev2);
   if (c->ev_fork) hipEventDestroy(c->ev_fork);
+  if (c->ev_fork2) hipEventDestroy(c->ev_fork2);
+  if (c->ev_join2) hipEventDestroy(c->ev_join2);
   if (c->ev_join) hipEventDestroy(c->ev_join);
   if (c->stream2) hipStreamDestroy(c->stream2);
   if (c->stream) hipStreamDestroy(c->stream);
@@ -1530,7 +1590,7 @@ int gi_knn_bench(gi_ctx *c, int map, int64_t n, const double *pts, const double 
       bmax[j] = std::max(bmax[j], qp[4 * i + j]);
     }
   uint32_t *perm = nullptr;
-  HIPCHK(c, morton_order(dq.as<float4>(), n, bmin, bmax, c->sorter, &perm, c->stream));
+  HIPCHK(c, morton_order(dq.as<float4>(), n, bmin, bmax, c->mx[0].sorter, &perm, c->stream));
   k.perm = perm;
   int saved = c->knn_kernel_kind;
   if (kernel >= 0) c->knn_kernel_kind = kernel;

@@ -358,8 +358,10 @@ __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, b
             int64_t ii = b + lane;
             bool take = false;
             float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+            uint32_t e = 0u;
             if (ii < s1) {
               p = pos[ii];
+              e = a.map.rgbe[ii];  // issued with the position: no second round trip per leaf
               take = gap2(p.x, p.y, p.z, p.x, p.y, p.z, bl, bh) <= U2;
             }
             uint64_t m = __ballot(take);
@@ -372,7 +374,7 @@ __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, b
               uint32_t off = count + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
               cpos[off] = p;
               cidx[off] = (uint32_t)ii;
-              crgbe[off] = a.map.rgbe[ii];
+              crgbe[off] = e;
             }
             count += nn;
           }

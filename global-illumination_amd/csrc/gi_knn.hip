@@ -217,6 +217,45 @@ __device__ __forceinline__ void wave_estimate(const KnnArgs &a, int64_t qi, floa
         c1 = pow_call(2.7182818284590452354, -a.fb);
         c2 = 1.0 / (2.0 * maxd2);
       }
+      if (a.filter == 0 && diff_only) {
+        // common case (disk filter, no specular term): the lane's photons s, s + 64, ... in
+        // groups of four, their list, direction-code, rgbe and LUT loads in flight together;
+        // each lane still sums its photons in increasing s
+        for (int s0 = lane; s0 < num; s0 += 256) {
+          uint32_t ids[4], ee[4], dcs[4];
+          double lx[4], ly[4], lz[4];
+#pragma unroll
+          for (int u = 0; u < 4; u++) ids[u] = fetch_id(s0 + 64 * u < num ? s0 + 64 * u : s0);
+#pragma unroll
+          for (int u = 0; u < 4; u++) {
+            dcs[u] = __float_as_uint(a.map.pos4[4 * (int64_t)ids[u] + 3]) & 0xffffu;
+            ee[u] = a.map.rgbe[ids[u]];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; u++) {
+            lx[u] = a.lut[3 * dcs[u]];
+            ly[u] = a.lut[3 * dcs[u] + 1];
+            lz[u] = a.lut[3 * dcs[u] + 2];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; u++) {
+            if (s0 + 64 * u >= num) break;
+            double perp = N0 * lx[u] + N1 * ly[u] + N2 * lz[u];
+            if ((sign == 2u && perp < 0) || (sign == 1u && perp > 0)) continue;
+            uint32_t e = ee[u];
+            uint32_t x = e >> 24;
+            double inv = x ? ldexp(1.0, (int)x - 128 - 8) : 0.0;
+            double p0 = x ? (double)(e & 255u) * inv : 0.0;
+            double p1 = x ? (double)((e >> 8) & 255u) * inv : 0.0;
+            double p2 = x ? (double)((e >> 16) & 255u) * inv : 0.0;
+            double ap = fabs(perp);
+            p0 *= ap * m.kd[0];
+            p1 *= ap * m.kd[1];
+            p2 *= ap * m.kd[2];
+            o0 += p0; o1 += p1; o2 += p2;
+          }
+        }
+      } else
       for (int s = lane; s < num; s += 64) {
         uint32_t id = fetch_id(s);
         double d2 = (double)fetch_d2(s);

@@ -1,8 +1,6 @@
 """The oracle restatement checked against what the reference itself left behind and against
 independent invariants:
-  * gallery/figures/fig_5a.png (pointlight1.scn, direct lighting from one point light; RNG
-    independent) -- rendered by the reference author; the bulk of the image must match
-    exactly (see tests/golden/README.md for why not all of it);
+  * (the reference's own rendered figures pin the shading: tests/test_cpu_gallery.py);
   * RGBE codec and direction table known answers (graphics_utils.cpp:50-77,
     photon_utils.cpp:253-272);
   * the kd-tree FindClosestQuick restatement equals a brute-force k-NN."""
@@ -13,7 +11,6 @@ import pytest
 
 import oracle_lib
 import synth
-from pngio import read_png
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden")
@@ -53,24 +50,11 @@ def test_kdtree_equals_bruteforce(k, r):
         dx = (qf[0] - P[:, 0]).astype(np.float32)
         dy = (qf[1] - P[:, 1]).astype(np.float32)
         dz = (qf[2] - P[:, 2]).astype(np.float32)
+        # the restatement's metric is fmaf(dz, dz, fmaf(dy, dy, dx * dx)) in fp32; the exact
+        # fp64 sum of the fp32 products rounded once to fp32 equals it except on rare last-ulp
+        # ties, which the rtol below absorbs (the k-NN *set* is checked exactly on the GPU)
         d = (dx * dx).astype(np.float64) + (dy.astype(np.float64) * dy) + (dz.astype(np.float64) * dz)
-        # fp32 fma metric: compare on the float rounding of the exact fp64 sum of products
-        df = np.array([np.float32(np.fma(z, z, np.fma(y, y, np.float32(x * x))))
-                       if hasattr(np, "fma") else np.float32(v)
-                       for x, y, z, v in zip(dx, dy, dz, d)], dtype=np.float32) \
-            if False else d.astype(np.float32)
+        df = d.astype(np.float32)
         sel = np.sort(df[df <= r2])[:k]
         assert nf[i] == len(sel)
         np.testing.assert_allclose(d2[i, :nf[i]], sel, rtol=1e-6)
-
-
-def test_gallery_fig5a_pointlight_direct():
-    """fig_5a = pointlight1.scn, one blue point light, direct lighting only."""
-    gal = read_png(os.path.join(GOLD, "fig_5a.png"))[..., :3].astype(int)
-    rgb, _ = oracle_lib.render([os.path.join(SCN, "pointlight1.scn"), "/tmp/x.png",
-                                "-resolution", "512", "512", "-aa", "0", "-no_indirect",
-                                "-no_caustic", "-threads", "8"], 512, 512)
-    ours = rgb[::-1].astype(int)  # bottom-up rows -> file order
-    d = np.abs(ours - gal).max(-1)
-    assert (d == 0).mean() >= 0.89
-    assert (d <= 1).mean() >= 0.90

@@ -13,31 +13,9 @@ import pytest
 import gi_amd
 import gi_dist
 import oracle_lib
+from gpu_util import compare, run_gpu, scene
 
 pytestmark = pytest.mark.gpu
-INP = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "scenes")
-
-
-def scene(name):
-    return os.path.join(INP, name)
-
-
-def run_gpu(renderer, args):
-    p, sc, _out, w, h, aa, real = gi_amd.ParseArgs(args)
-    renderer.set_params(p)
-    renderer.ReadScene(sc, real)
-    pst = None
-    if p.indirect_illum or p.caustic_illum or p.direct_photon_illum:
-        pst = renderer.MapPhotons()
-    rgb, st = renderer.RenderImage(aa, w, h)
-    return rgb, st, pst
-
-
-def compare(a, b, exact_frac, le1_frac, mean_tol):
-    d = np.abs(a.astype(int) - b.astype(int))
-    assert (d.max(-1) == 0).mean() >= exact_frac, (d.max(-1) == 0).mean()
-    assert (d.max(-1) <= 1).mean() >= le1_frac, (d.max(-1) <= 1).mean()
-    assert abs(a.astype(float).mean() - b.astype(float).mean()) <= mean_tol
 
 
 @pytest.mark.parametrize("name,extra", [

@@ -231,18 +231,13 @@ struct gi_ctx {
   bool map_valid[2] = {false, false};
   int leaf_size[2] = {64, 256};  // photons per kd leaf, per map (global, caustic)
   int wave_cap_mul = 1;
-  int chunk_cap = 256;            // chunk kernel: LDS candidate capacity per 64-query chunk
   int chunk_cap_big = 512;        // large-K chunk kernel: the same (384 or 512)
   int chunk_minsub_big = 64;      // large-K chunk kernel: overflowing chunks retried down to this (64: none, measured best)
   int chunk_minsub = 32;          // chunk kernel: overflowing chunks retried as halves (measured best with the dk bound)
   double fb_ms[2] = {0, 0};       // fallback time and queries per map (since the last reset)
   uint64_t fb_q[2] = {0, 0};
   int sel_slack = 64;
-  bool force_gheap = false;
   int knn_qpl = 1;
-  int lane_chunk = 8;             // per-lane kernel: photon loads in flight per lane
-  int group_lanes = 16;           // group kernel: lanes per query
-  int heap_arity = 4;             // per-lane kernel: d-ary heap
   int ind_waves = 3;              // indirect-path kernel occupancy target (waves per SIMD)
   DBuf ind_cont, ind_ncont;       // indirect paths that continue past their first bounce
   DBuf mc_cont, mc_ncont;         // Monte Carlo paths' indirect sub-paths
@@ -261,7 +256,7 @@ struct gi_ctx {
   DBuf qseg[2];  // K-best lists of the query-per-wave k-NN path
   size_t qcap_hint[2] = {0, 0};
   KeySortScratch keysort[2];
-  int knn_kernel_kind = -1;  // -1 auto, 0 per-lane heap, 1 query per wave, 2 packet
+  int knn_kernel_kind = -1;  // -1 auto; run_knn lists the kinds
   DBuf scan_lvl[8], scan_out[8];
   // photon tracing scratch
   DBuf pcounts, poffs, pbuf;
@@ -582,19 +577,21 @@ int ensure_dk(gi_ctx *c, KnnArgs &k) {
 // run a k-NN launch over nq queries (chunked when the heap lives in global scratch)
 int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
   MapExec &X = c->mx[k.stat_off ? 1 : 0];
-  // auto (-1): chunk kernel with lane select (+ per-lane fallback) for K <= 64, the per-lane
-  // kernel for list mode, one query per wave beyond (measured)
+  // Kernel choice (GI_KNN_KERNEL overrides; -1 = auto):
+  //   7  chunk kernel with lane select + per-lane fallback (K <= 64, estimates): the default
+  //   3  per-lane kernel, LDS heaps (K <= 128; list mode)
+  //   8  large-K chunk kernel + query-per-wave fallback (K > 64, estimates; needs dk bounds)
+  //   1  query-per-wave kernel (K + 64 <= 1024)
+  //   0  per-lane kernel with global-memory heaps (any K)
   int kind = c->knn_kernel_kind;
-  int auto_kind = (k.K <= 64) ? (k.mode == KNN_MODE_LIST ? 3 : 7)
-                              : ((k.mode == KNN_MODE_LIST || !c->use_dk) ? 1 : 8);
+  const bool list = k.mode == KNN_MODE_LIST, dkm = k.mode == KNN_MODE_DK;
+  int auto_kind = (k.K <= 64) ? (list ? 3 : 7) : ((list || !c->use_dk) ? 1 : 8);
   if (kind < 0) kind = auto_kind;
-  // an override that cannot serve this map's K (or list mode) falls back to the automatic one
-  if (kind == 8 && (k.mode == KNN_MODE_LIST || k.mode == KNN_MODE_DK || k.K + 64 > 1024 || !c->use_dk))
-    kind = auto_kind == 8 ? 1 : auto_kind;
-  if (((kind >= 5 && kind <= 7) && (k.K > 64 || k.mode == KNN_MODE_LIST)) || (kind == 3 && k.K > 128) ||
-      (kind == 0 && k.K > 64))
-    kind = auto_kind;
-  if (kind == 2 && (int64_t)k.K * 64 * 8 > 80 * 1024) kind = 1;
+  // an override that cannot serve this launch falls back to the automatic choice
+  if (kind == 7 && (k.K > 64 || list)) kind = auto_kind;
+  if (kind == 8 && (list || dkm || k.K + 64 > 1024 || !c->use_dk)) kind = auto_kind == 8 ? 1 : auto_kind;
+  if (kind == 3 && (size_t)k.K * 512 > 64 * 1024) kind = auto_kind;
+  if (kind == 1 && k.K + 64 > 1024) kind = 0;
   if (kind == 8) {
     // large-K chunk kernel, then the query-per-wave kernel on what it hands over
     int rc = ensure_dk(c, k);
@@ -676,7 +673,7 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
     }
     return GI_OK;
   }
-  if ((kind >= 5 && kind <= 7) && k.K <= 64 && k.mode != KNN_MODE_LIST) {
+  if (kind == 7) {
     // chunk kernel, then the per-lane kernel on the chunks that overflowed its LDS gather
     // striped fallback list (gi_knn_chunk.hip to_fallback): block b -> stripe b % FB_QS, at most
     // 64 queries per chunk, ceil(chunks / grid) chunks per block
@@ -702,9 +699,9 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
       if (!c->chunk_dk) k.map.dk = nullptr;
     }
     const int dbg0 = k.dbg;
-    if (c->chunk_fb_all && kind == 7) k.dbg |= 4;  // lane select skipped: all to the fallback
+    if (c->chunk_fb_all) k.dbg |= 4;  // lane select skipped: all to the fallback
     HIPCHK(c, hipEventRecord(X.ev0, X.st));
-    launch_knn_chunk(k, c->chunk_cap, kind - 5, X.st);
+    launch_knn_chunk(k, X.st);
     k.dbg = dbg0;
     HIPCHK(c, hipGetLastError());
     uint32_t *dense = X.fb_dense.as<uint32_t>();
@@ -721,7 +718,7 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
       f.nq = nfb;
       f.q0 = 0;
       f.map.dk = fb_dk;
-      launch_knn_lane(f, c->lane_chunk, c->heap_arity, X.st);
+      launch_knn_lane(f, X.st);
       HIPCHK(c, hipGetLastError());
     }
     HIPCHK(c, hipEventRecord(X.ev1, X.st));
@@ -737,11 +734,11 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
     }
     return GI_OK;
   }
-  if (kind == 3 && (size_t)k.K * 512 <= 64 * 1024) {
+  if (kind == 3) {
     k.nq = nq;
     k.q0 = 0;
     HIPCHK(c, hipEventRecord(X.ev0, X.st));
-    launch_knn_lane(k, c->lane_chunk, c->heap_arity, X.st);
+    launch_knn_lane(k, X.st);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(X.ev1, X.st));
     if (ms) {
@@ -752,37 +749,29 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
     }
     return GI_OK;
   }
-  if ((kind == 1 && k.K + 64 <= 1024) || kind == 2 || kind == 4) {
+  if (kind == 1) {
+    // one query per wave; the search writes per-query K-best lists in list / DK mode (and when
+    // the estimate is not fused into it), a second kernel estimates from them
     k.nq = nq;
     k.q0 = 0;
-    if (kind == 1 || kind == 4) {
-      // search writes per-query K-best lists, a second kernel estimates from them
-      if (k.mode == KNN_MODE_LIST) {
-        k.list_idx = k.out_idx;
-        k.list_d2 = k.out_d2;
-        k.list_n = k.out_n;
-      } else {
-        size_t slots = (size_t)nq * (size_t)k.K;
-        HIPCHK(c, X.list_idx.ensure(slots * 4));
-        HIPCHK(c, X.list_d2.ensure(slots * 4));
-        HIPCHK(c, X.list_n.ensure((size_t)nq * 4));
-        k.list_idx = X.list_idx.as<int32_t>();
-        k.list_d2 = X.list_d2.as<float>();
-        k.list_n = X.list_n.as<int32_t>();
-      }
+    if (k.mode == KNN_MODE_LIST) {
+      k.list_idx = k.out_idx;
+      k.list_d2 = k.out_d2;
+      k.list_n = k.out_n;
+    } else {
+      size_t slots = (size_t)nq * (size_t)k.K;
+      HIPCHK(c, X.list_idx.ensure(slots * 4));
+      HIPCHK(c, X.list_d2.ensure(slots * 4));
+      HIPCHK(c, X.list_n.ensure((size_t)nq * 4));
+      k.list_idx = X.list_idx.as<int32_t>();
+      k.list_d2 = X.list_d2.as<float>();
+      k.list_n = X.list_n.as<int32_t>();
     }
-    if (kind == 1) {
-      int rc = ensure_dk(c, k);
-      if (rc) return rc;
-    }
+    int rc = ensure_dk(c, k);
+    if (rc) return rc;
     HIPCHK(c, hipEventRecord(X.ev0, X.st));
-    bool ok = true;
-    if (kind == 2) ok = launch_knn_packet(k, X.st);
-    else if (kind == 4)
-      ok = launch_knn_group(k, c->group_lanes, X.st) ||
-           launch_knn_wave(k, c->wave_cap_mul, X.st);  // K too large for the groups
-    else ok = launch_knn_wave(k, c->wave_cap_mul, X.st);
-    if (!ok) return fail(c, GI_ERR_ARG, "k-NN launch: unsupported estimate size for this kernel");
+    if (!launch_knn_wave(k, c->wave_cap_mul, X.st))
+      return fail(c, GI_ERR_ARG, "k-NN launch: unsupported estimate size for this kernel");
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(X.ev1, X.st));
     if (ms) {
@@ -793,14 +782,14 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
     }
     return GI_OK;
   }
-  bool lds = k.K <= 64 && !c->force_gheap;
-  const int64_t CH = lds ? nq : (int64_t)(1 << 20);
+  // kind 0: per-lane heaps in global scratch, launched in slices of 2^20 queries
+  const int64_t CH = (int64_t)(1 << 20);
   for (int64_t s = 0; s < nq; s += CH) {
     int64_t m = std::min(CH, nq - s);
     KnnArgs a = k;
     a.nq = m;
     a.q0 = s;
-    if (!lds) {
+    {
       size_t slots = (size_t)((m + 63) / 64) * 64 * (size_t)k.K;
       HIPCHK(c, X.gheap_d2.ensure(slots * 4));
       HIPCHK(c, X.gheap_idx.ensure(slots * 4));
@@ -808,7 +797,7 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
       a.gheap_idx = X.gheap_idx.as<int32_t>();
     }
     HIPCHK(c, hipEventRecord(X.ev0, X.st));
-    launch_knn(a, lds, X.st);
+    launch_knn(a, X.st);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(X.ev1, X.st));
     if (ms) {
@@ -1126,15 +1115,9 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_LEAF_SIZE_C")) c->leaf_size[1] = std::max(1, atoi(s));
   if (const char *s = getenv("GI_WAVE_CAP_MUL")) c->wave_cap_mul = std::max(1, atoi(s));
   if (const char *s = getenv("GI_SEL_SLACK")) c->sel_slack = std::max(1, atoi(s));
-  if (const char *s = getenv("GI_CHUNK_CAP")) c->chunk_cap = std::max(64, atoi(s));
   if (const char *s = getenv("GI_CHUNK_CAP_BIG")) c->chunk_cap_big = atoi(s) <= 384 ? 384 : 512;
   if (const char *s = getenv("GI_CHUNK_MINSUB_BIG")) c->chunk_minsub_big = std::min(64, std::max(1, atoi(s)));
   if (const char *s = getenv("GI_CHUNK_MINSUB")) c->chunk_minsub = std::min(64, std::max(1, atoi(s)));
-  if (const char *s = getenv("GI_KNN_GHEAP")) c->force_gheap = atoi(s) != 0;
-  if (const char *s = getenv("GI_KNN_QPL")) c->knn_qpl = std::max(1, atoi(s));
-  if (const char *s = getenv("GI_LANE_CHUNK")) c->lane_chunk = std::max(1, atoi(s));
-  if (const char *s = getenv("GI_GROUP_LANES")) c->group_lanes = std::max(1, atoi(s));
-  if (const char *s = getenv("GI_HEAP_ARITY")) c->heap_arity = std::max(2, atoi(s));
   if (const char *s = getenv("GI_IND_WAVES")) c->ind_waves = std::max(1, atoi(s));
   if (const char *s = getenv("GI_SPLIT_IND")) c->split_ind = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_DK")) c->use_dk = atoi(s) != 0;

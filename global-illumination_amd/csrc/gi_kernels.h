@@ -320,14 +320,14 @@ void launch_reduce(const RenderArgs &a, hipStream_t st);
 void launch_owner_table(const uint32_t *off, int64_t n, uint32_t *tab, hipStream_t st);
 void launch_segments(const uint64_t *skeys, uint32_t n, uint32_t nprim, uint32_t *seg,
                      hipStream_t st);
-void launch_knn(const KnnArgs &a, bool lds_heap, hipStream_t st);
+// generic per-lane kernel with its heaps in global scratch (any K; used beyond the LDS kernels)
+void launch_knn(const KnnArgs &a, hipStream_t st);
 bool launch_knn_wave(const KnnArgs &a, int cap_mul, hipStream_t st);
-bool launch_knn_packet(const KnnArgs &a, hipStream_t st);
-bool launch_knn_lane(const KnnArgs &a, int chunk, int arity, hipStream_t st);
-bool launch_knn_group(const KnnArgs &a, int lanes, hipStream_t st);
-bool launch_knn_chunk(const KnnArgs &a, int cap, int variant, hipStream_t st);  // 0 wave, 1 heaps, 2 lane select
+bool launch_knn_lane(const KnnArgs &a, hipStream_t st);
+bool launch_knn_chunk(const KnnArgs &a, hipStream_t st);  // K <= 64, lane select
+bool launch_knn_chunk_big(const KnnArgs &a, int cap, hipStream_t st);  // K > 64, needs a.map.dk
+// blocks of the chunk kernels (one 64-query chunk each, grid-stride)
 unsigned knn_chunk_grid(int64_t nq);
-bool launch_knn_chunk_big(const KnnArgs &a, int cap, hipStream_t st);  // K > 64, needs a.map.dk  // blocks of the chunk kernels (one 64-query chunk each, grid-stride)
 void launch_list_estimate(const KnnArgs &a, hipStream_t st);
 void launch_cached(const KnnArgs &a, hipStream_t st);
 void launch_photons(const PhotonArgs &a, bool emit, hipStream_t st);

@@ -847,17 +847,13 @@ __device__ __forceinline__ int knn_search(const KdView &M, float qx, float qy, f
 // the previous query p all lie within d_K(p) + |q - p| of q (triangle inequality), so
 // d_K(q)^2 <= (d_K(p) + |q - p|)^2. A 1e-5 relative margin covers the fp32 metric's
 // rounding; the bound only prunes, the result set is unchanged.
-template <bool LDS_HEAP>
+// The heaps live in global scratch, so any K works: this is the path for estimate sizes beyond
+// the LDS kernels (K + 64 > 1024 photons per query-per-wave candidate buffer).
 __global__ __launch_bounds__(64) void knn_kernel(KnnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   int lane = threadIdx.x;
   uint64_t nfound_total = 0, visited_total = 0, nq_done = 0;
   HeapRef h;
-  if (LDS_HEAP) {
-    h.d2 = reinterpret_cast<float *>(smem) + lane;
-    h.idx = reinterpret_cast<int32_t *>(smem + (size_t)a.K * 64 * sizeof(float)) + lane;
-    h.stride = 64;
-  } else {
+  {
     int64_t t = (int64_t)blockIdx.x * 64 + lane;
     h.d2 = a.gheap_d2 + t;
     h.idx = a.gheap_idx + t;
@@ -1487,14 +1483,9 @@ void launch_reduce(const RenderArgs &a, hipStream_t st) {
   reduce_prim_kernel<<<nblk(a.nprim, 256), 256, 0, st>>>(a);
   reduce_kernel<<<nblk(a.npix, 64), 64, 0, st>>>(a);
 }
-void launch_knn(const KnnArgs &a, bool lds_heap, hipStream_t st) {
+void launch_knn(const KnnArgs &a, hipStream_t st) {
   if (a.nq == 0) return;
-  if (lds_heap) {
-    size_t sm = (size_t)a.K * 64 * (sizeof(float) + sizeof(int32_t));
-    knn_kernel<true><<<nblk(a.nq, 64 * a.qpl), 64, sm, st>>>(a);
-  } else {
-    knn_kernel<false><<<nblk(a.nq, 64 * a.qpl), 64, 0, st>>>(a);
-  }
+  knn_kernel<<<nblk(a.nq, 64 * a.qpl), 64, 0, st>>>(a);
 }
 void launch_cached(const KnnArgs &a, hipStream_t st) {
   if (a.nq == 0) return;

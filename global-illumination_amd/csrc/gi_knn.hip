@@ -857,245 +857,13 @@ __global__ __launch_bounds__(64) void knn_lane_kernel(KnnArgs a) {
   }
 }
 
-bool launch_knn_lane(const KnnArgs &a, int chunk, int arity, hipStream_t st) {
+// 8 photon loads in flight per lane and a 4-ary heap: the measured best
+bool launch_knn_lane(const KnnArgs &a, hipStream_t st) {
   if (a.nq == 0) return true;
   size_t lds = (size_t)(a.K > 0 ? a.K : 1) * 64 * sizeof(uint64_t);
   if (lds > 64 * 1024) return false;
   unsigned grid = (unsigned)((a.nq + 63) / 64);
-  if (arity <= 2) {
-    if (chunk <= 4) knn_lane_kernel<4, 2><<<grid, 64, lds, st>>>(a);
-    else knn_lane_kernel<8, 2><<<grid, 64, lds, st>>>(a);
-  } else if (arity <= 4) {
-    if (chunk <= 4) knn_lane_kernel<4, 4><<<grid, 64, lds, st>>>(a);
-    else knn_lane_kernel<8, 4><<<grid, 64, lds, st>>>(a);
-  } else {
-    if (chunk <= 4) knn_lane_kernel<4, 8><<<grid, 64, lds, st>>>(a);
-    else knn_lane_kernel<8, 8><<<grid, 64, lds, st>>>(a);
-  }
-  return true;
-}
-
-// ---------------------------------------------------------------------------------------
-// Packet k-NN: 64 spatially adjacent queries (Morton order) per wave share ONE wave-uniform
-// traversal of the kd-tree, so each node and leaf fetch serves 64 queries. Every lane keeps
-// its own exact max-heap of the K best keys (d2 bits << 32 | photon index) in LDS laid out
-// [slot][lane] (8-B stride across lanes: conflict-free ds_read/write_b64).
-//
-// Exactness: a subtree is skipped only if, for EVERY lane, the query lies on the visited side
-// of the split and diff^2 > that lane's current bound (the single-query rule of
-// R3Kdtree.cpp:740-751 applied per lane), so each lane's result is the same K smallest
-// (d2, index) pairs with d2 <= r2 as the per-query search.
-// Visit order: at each node the packet descends first into the side holding the majority
-// of its queries (recomputed identically on the way up, which makes the walk stackless).
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ float rlane(float v, int j) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
-}
-
-__global__ __launch_bounds__(64) void knn_packet_kernel(KnnArgs a) {
-  extern __shared__ uint64_t hs[];
-  const int lane = threadIdx.x;
-  uint64_t *h = hs + lane;
-  const KdNode *nodes = reinterpret_cast<const KdNode *>(a.map.nodes);
-  const float4 *pos = reinterpret_cast<const float4 *>(a.map.pos4);
-  const int L = a.map.nleaves;
-  const int64_t N = a.map.n;
-  const int K = a.K;
-  const int64_t q = (int64_t)blockIdx.x * 64 + lane;
-  bool valid = q < a.nq;
-  int64_t qi = 0;
-  float4 qp = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (valid) {
-    int64_t qg = a.q0 + q;
-    qi = a.perm ? (int64_t)a.perm[qg] : qg;
-    qp = a.qpos[qi];
-    valid = __float_as_uint(qp.w) != QMETA_NONE;
-  }
-  int size = 0;
-  uint64_t thr = valid ? ((uint64_t)__float_as_uint(a.r2f) << 32) + 0x100000000ull : 0ull;
-  float pr = valid ? a.r2f : -1.0f;  // prune bound: d2 of the current threshold
-  const uint64_t vmask = __ballot(valid);
-  const int nvalid = __popcll(vmask);
-  uint32_t visited = 0;
-  if (N > 0 && K > 0) {
-    int node = 1;
-    while (true) {
-      KdNode nd = nodes[node];
-      bool need = valid && kd_box_d2(nd.lo, nd.hi, qp.x, qp.y, qp.z) <= pr;
-      if (__ballot(need)) {
-        if (node < L) {
-          // descend: the side holding the majority of the packet first
-          float qa = kd_axis_q(__float_as_int(nd.hi.w), qp.x, qp.y, qp.z);
-          int nr = __popcll(__ballot(valid && qa - nd.lo.w >= 0.0f));
-          node = 2 * node + ((2 * nr > nvalid) ? 1 : 0);
-          continue;
-        }
-        int leaf = node - L;
-        int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
-        visited += (uint32_t)(s1 - s0);
-        for (int64_t b = s0; b < s1; b += 64) {
-          int cnt = (int)((s1 - b) < 64 ? (s1 - b) : 64);
-          float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (lane < cnt) p = pos[b + lane];
-          if (!need) continue;
-          for (int j = 0; j < cnt; j++) {
-            float px = rlane(p.x, j), py = rlane(p.y, j), pz = rlane(p.z, j);
-            float dx = qp.x - px, dy = qp.y - py, dz = qp.z - pz;
-            float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
-            if (d2 <= pr) {
-              uint64_t key = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)(uint32_t)(b + j);
-              if (key < thr) {
-                heapn_accept<4>(h, size, K, key, thr);
-                if (size == K) pr = __uint_as_float((uint32_t)(thr >> 32));
-              }
-            }
-          }
-        }
-      }
-      // backtrack: first-visited child whose sibling is unvisited (majority rule recomputed)
-      while (node != 1) {
-        const KdNode &pn = nodes[node >> 1];
-        float qa = kd_axis_q(__float_as_int(pn.hi.w), qp.x, qp.y, qp.z);
-        int nr = __popcll(__ballot(valid && qa - pn.lo.w >= 0.0f));
-        int first = (2 * nr > nvalid) ? 1 : 0;
-        if ((node & 1) == first) break;
-        node >>= 1;
-      }
-      if (node == 1) break;
-      node ^= 1;
-    }
-  }
-  int num = size;
-  if (valid) {
-    if (a.mode == KNN_MODE_LIST) {
-      for (int s = 0; s < K; s++) {
-        bool v = s < num;
-        uint64_t key = v ? h[s * 64] : 0ull;
-        a.out_idx[qi * K + s] = v ? (int32_t)(uint32_t)key : -1;
-        a.out_d2[qi * K + s] = v ? __uint_as_float((uint32_t)(key >> 32)) : -1.0f;
-      }
-      a.out_n[qi] = num;
-    } else {
-      double o0 = 0, o1 = 0, o2 = 0;
-      double maxd2 = kEps;
-      if (num > 0) {
-        // max-heap root = K-th distance (photon_utils.cpp:108-111); r_max^2 if fewer (Q4)
-        maxd2 = (num < K) ? a.rmax * a.rmax : (double)__uint_as_float((uint32_t)(h[0] >> 32));
-        if (num == K && maxd2 < kEps) maxd2 = kEps;
-        if (a.mode == KNN_MODE_IRRADIANCE) {
-          // EstimateIrradiance, photon_utils.cpp:209-246
-          for (int s = 0; s < num; s++) {
-            uint32_t e = a.map.rgbe[(uint32_t)h[s * 64]];
-            uint32_t ex = e >> 24;
-            if (ex) {
-              double inv = ldexp(1.0, (int)ex - 128 - 8);
-              o0 += (double)(e & 255u) * inv;
-              o1 += (double)((e >> 8) & 255u) * inv;
-              o2 += (double)((e >> 16) & 255u) * inv;
-            }
-          }
-          double den = kPi * maxd2;
-          o0 /= den; o1 /= den; o2 /= den;
-        } else {
-          // EstimateRadiance, photon_utils.cpp:113-158
-          const QShade &sh = a.qshade[qi];
-          uint32_t meta = __float_as_uint(qp.w);
-          uint32_t sign = meta & 3u;
-          const DMaterial &m = a.mats[meta >> 2];
-          double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
-          double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
-          bool spec = (m.flags & MF_SPECULAR) || (m.n < 0);
-          // without the specular term, ap * kd + 0 * ks == ap * kd up to the sign of a zero (for
-          // finite ks), and the sums start at +0, so dropping the 0 * ks products changes no result
-          const bool diff_only = !spec && isfinite(m.ks[0]) && isfinite(m.ks[1]) && isfinite(m.ks[2]);
-          double c1 = 1.0, c2 = 1.0, tw = 0;
-          if (a.filter == 1) c1 = 1.0 / (a.fk * sqrt(maxd2));
-          else if (a.filter == 2) {
-            c1 = pow_call(2.7182818284590452354, -a.fb);
-            c2 = 1.0 / (2.0 * maxd2);
-          }
-          for (int s = 0; s < num; s++) {
-            uint64_t key = h[s * 64];
-            uint32_t id = (uint32_t)key;
-            double d2 = (double)__uint_as_float((uint32_t)(key >> 32));
-            uint32_t dcode = __float_as_uint(a.map.pos4[4 * (int64_t)id + 3]) & 0xffffu;
-            double ix = a.lut[3 * dcode], iy = a.lut[3 * dcode + 1], iz = a.lut[3 * dcode + 2];
-            double perp = N0 * ix + N1 * iy + N2 * iz;
-            if ((sign == 2u && perp < 0) || (sign == 1u && perp > 0)) continue;
-            uint32_t e = a.map.rgbe[id];
-            uint32_t ee = e >> 24;
-            double inv = ee ? ldexp(1.0, (int)ee - 128 - 8) : 0.0;
-            double p0 = ee ? (double)(e & 255u) * inv : 0.0;
-            double p1 = ee ? (double)((e >> 8) & 255u) * inv : 0.0;
-            double p2 = ee ? (double)((e >> 16) & 255u) * inv : 0.0;
-            double ca = E0 * -ix + E1 * -iy + E2 * -iz;
-            if (ca < 0) ca = 0;
-            double ap = fabs(perp);
-            if (diff_only) {
-              p0 *= ap * m.kd[0];
-              p1 *= ap * m.kd[1];
-              p2 *= ap * m.kd[2];
-            } else {
-              double pw = spec ? pow_call(ca, m.n) : 0.0;
-              p0 *= ap * m.kd[0] + pw * m.ks[0];
-              p1 *= ap * m.kd[1] + pw * m.ks[1];
-              p2 *= ap * m.kd[2] + pw * m.ks[2];
-            }
-            if (a.filter == 1) {
-              double f = (1.0 - c1 * sqrt(d2));
-              p0 *= f; p1 *= f; p2 *= f;
-            } else if (a.filter == 2) {
-              double w = (1.0 - (1.0 - pow_call(c1, c2 * d2)) / (1.0 - c1));
-              p0 *= w; p1 *= w; p2 *= w;
-              tw += w;
-            }
-            o0 += p0; o1 += p1; o2 += p2;
-          }
-          bool ok = true;
-          if (a.filter == 0 && maxd2 > 0) {
-            double den = kPi * maxd2;
-            o0 /= den; o1 /= den; o2 /= den;
-          } else if (a.filter == 1 && maxd2 > 0) {
-            double den = (1.0 - 2.0 / 3.0 / a.fk) * kPi * maxd2;
-            o0 /= den; o1 /= den; o2 /= den;
-          } else if (a.filter == 2 && tw > 0 && maxd2 > 0) {
-            double sc = a.fa * (num / tw) / (kPi * maxd2);
-            o0 *= sc; o1 *= sc; o2 *= sc;
-          } else {
-            ok = false;
-          }
-          if (ok) {
-            o0 *= sh.w[0]; o1 *= sh.w[1]; o2 *= sh.w[2];
-          } else {
-            o0 = o1 = o2 = 0;
-          }
-        }
-      }
-      a.out[3 * qi] = o0;
-      a.out[3 * qi + 1] = o1;
-      a.out[3 * qi + 2] = o2;
-      if (a.out_n) a.out_n[qi] = num;
-      if (a.out_maxd2) a.out_maxd2[qi] = (num > 0) ? (float)maxd2 : 0.0f;
-    }
-  }
-  if (a.stats) {
-    uint64_t nq_done = valid ? 1 : 0, found = valid ? (uint64_t)num : 0,
-             vis = valid ? (uint64_t)visited : 0;
-    wave_add(&a.stats[ST_KNN + a.stat_off], nq_done);
-    wave_add(&a.stats[ST_KNN_PHOTONS + a.stat_off], found);
-    wave_add(&a.stats[ST_KNN_VISITED + a.stat_off], vis);
-  }
-}
-
-bool launch_knn_packet(const KnnArgs &a, hipStream_t st) {
-  if (a.nq == 0) return true;
-  size_t lds = (size_t)(a.K > 0 ? a.K : 1) * 64 * sizeof(uint64_t);
-  if (lds > 160 * 1024) return false;
-  if (lds > 64 * 1024)
-    hipFuncSetAttribute((const void *)knn_packet_kernel,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  unsigned grid = (unsigned)((a.nq + 63) / 64);
-  knn_packet_kernel<<<grid, 64, lds, st>>>(a);
+  knn_lane_kernel<8, 4><<<grid, 64, lds, st>>>(a);
   return true;
 }
 
@@ -1106,20 +874,12 @@ void launch_list_estimate(const KnnArgs &a, hipStream_t st) {
 }
 
 template <bool PROF, bool FUSE>
-bool wave_launch(const KnnArgs &a, int need, int lb, unsigned grid, hipStream_t st) {
-  if (lb <= 1) {
-    if (need <= 128) knn_wave_kernel<128, 1, PROF, FUSE><<<grid, 64, 0, st>>>(a);
-    else if (need <= 256) knn_wave_kernel<256, 1, PROF, FUSE><<<grid, 64, 0, st>>>(a);
-    else if (need <= 512) knn_wave_kernel<512, 1, PROF, FUSE><<<grid, 64, 0, st>>>(a);
-    else if (need <= 1024) knn_wave_kernel<1024, 1, PROF, FUSE><<<grid, 64, 0, st>>>(a);
-    else return false;
-  } else {
-    if (need <= 128) knn_wave_kernel<128, 8, PROF, FUSE><<<grid, 64, 0, st>>>(a);
-    else if (need <= 256) knn_wave_kernel<256, 8, PROF, FUSE><<<grid, 64, 0, st>>>(a);
-    else if (need <= 512) knn_wave_kernel<512, 8, PROF, FUSE><<<grid, 64, 0, st>>>(a);
-    else if (need <= 1024) knn_wave_kernel<1024, 8, PROF, FUSE><<<grid, 64, 0, st>>>(a);
-    else return false;
-  }
+bool wave_launch(const KnnArgs &a, int need, unsigned grid, hipStream_t st) {
+  if (need <= 128) knn_wave_kernel<128, 1, PROF, FUSE><<<grid, 64, 0, st>>>(a);
+  else if (need <= 256) knn_wave_kernel<256, 1, PROF, FUSE><<<grid, 64, 0, st>>>(a);
+  else if (need <= 512) knn_wave_kernel<512, 1, PROF, FUSE><<<grid, 64, 0, st>>>(a);
+  else if (need <= 1024) knn_wave_kernel<1024, 1, PROF, FUSE><<<grid, 64, 0, st>>>(a);
+  else return false;
   return true;
 }
 
@@ -1127,19 +887,17 @@ bool launch_knn_wave(const KnnArgs &a, int cap_mul, hipStream_t st) {
   if (a.nq == 0) return true;
   int need = (a.K + 64) * cap_mul;
   int64_t grid = a.nq < (1 << 16) ? a.nq : (1 << 16);
-  // photon batches of 64 prefetched per leaf (GI_WAVE_LB: 1 or 8); GI_KNN_DBG & 16 selects the
-  // instance with phase cycle counters
-  static const int lb = getenv("GI_WAVE_LB") ? atoi(getenv("GI_WAVE_LB")) : 1;
+  // GI_KNN_DBG & 16 selects the instance with phase cycle counters
   // the estimate fused into the search (GI_WAVE_FUSE=0: lists + knn_list_estimate_kernel)
   static const bool fuse = getenv("GI_WAVE_FUSE") ? atoi(getenv("GI_WAVE_FUSE")) != 0 : true;
   const bool est = a.mode != KNN_MODE_LIST && a.mode != KNN_MODE_DK;
   bool ok;
   if (est && fuse) {
-    ok = (a.dbg & 16) ? wave_launch<true, true>(a, need, lb, (unsigned)grid, st)
-                      : wave_launch<false, true>(a, need, lb, (unsigned)grid, st);
+    ok = (a.dbg & 16) ? wave_launch<true, true>(a, need, (unsigned)grid, st)
+                      : wave_launch<false, true>(a, need, (unsigned)grid, st);
   } else {
-    ok = (a.dbg & 16) ? wave_launch<true, false>(a, need, lb, (unsigned)grid, st)
-                      : wave_launch<false, false>(a, need, lb, (unsigned)grid, st);
+    ok = (a.dbg & 16) ? wave_launch<true, false>(a, need, (unsigned)grid, st)
+                      : wave_launch<false, false>(a, need, (unsigned)grid, st);
   }
   if (!ok) return false;
   if (est && !fuse) knn_list_estimate_kernel<<<(unsigned)grid, 64, 0, st>>>(a);

@@ -10,14 +10,11 @@
 //      inequality), and every photon of its K-NN lies within U of B.
 //   2. gather: one wave-uniform kd traversal (box-to-box pruning) copies every photon within U
 //      of B into LDS (position, dir bits, rgbe, index), ballot-compacted.
-//   3. select, two variants:
-//      - lane select (knn_chunk_lane_kernel, default): lane j owns query j. Counting passes
-//        over the LDS candidates (every read is an LDS broadcast) narrow a d2 bracket with 16
-//        value-range bins each, until the K-th key's bracket holds <= 4 photons; a collect
-//        pass then keeps everything below the bracket and sorts the bracket by (d2, index).
-//        No cross-lane operations, no LDS atomics, all 64 queries advance together.
-//      - wave select (knn_chunk_kernel): one query at a time, 64 lanes compute its candidate
-//        keys and a wave-wide value-range bucket select keeps the K best.
+//   3. lane select (knn_chunk_lane_kernel): lane j owns query j. Counting passes over the LDS
+//      candidates (every read is an LDS broadcast) narrow a d2 bracket with 16 value-range bins
+//      each, until the K-th key's bracket holds few photons; a collect pass then keeps
+//      everything below the bracket and sorts the bracket by (d2, index). All 64 queries
+//      advance together.
 //   4. estimate: each lane estimates its own query from the LDS-staged photons it kept.
 // There is no per-query traversal and no per-query heap. The only global traffic per query is
 // its record and the LUT rows of the photons it keeps. Chunks whose gather exceeds the LDS
@@ -1034,234 +1031,6 @@ void knn_chunk_big_kernel(KnnArgs a) {
   chunk_flush_stats(a, P, st_q, st_found, st_vis);
 }
 
-// ---------------------------------------------------------------------------------------------
-// wave select: one query at a time across the wave
-// ---------------------------------------------------------------------------------------------
-template <int CAPC, int WPE>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE)))
-void knn_chunk_kernel(KnnArgs a) {
-  constexpr int PER = CAPC / 64;
-  using SlotT = typename std::conditional<(CAPC <= 256), uint8_t, uint16_t>::type;
-  __shared__ float4 cpos[CAPC];
-  __shared__ uint32_t cidx[CAPC];
-  __shared__ uint32_t crgbe[CAPC];
-  __shared__ uint32_t hist[256];
-  __shared__ uint32_t stk[64];  // kd walk stack (walk_within)
-  __shared__ SlotT sel[64 * 64];      // kept LDS slots per query of the chunk (K <= 64)
-  __shared__ float smax[64];          // per query: K-th d2
-  __shared__ int snum[64];
-  const int lane = threadIdx.x;
-  const int K = a.K;
-  uint64_t st_q = 0, st_found = 0, st_vis = 0;
-  ChunkProf P;
-  P.on = (a.dbg & 16) != 0;
-  P.t = 0;
-  for (int i = 0; i < 10; i++) P.c[i] = 0;
-  for (int64_t chunk = blockIdx.x; chunk * 64 < a.nq; chunk += gridDim.x) {
-    bool valid;
-    int64_t qi;
-    float4 qp;
-    chunk_load_query(a, chunk, lane, valid, qi, qp);
-    uint64_t vmask = __ballot(valid);
-    if (vmask == 0) continue;
-    if (P.on) P.t = clock64();
-    ChunkGeom G;
-    chunk_bound_gather<CAPC>(a, lane, valid, qp, CAPC, cpos, cidx, crgbe, hist, stk, G, P);
-    if (G.overflow) {
-      to_fallback(a, vmask, valid, qi, lane);
-      __syncthreads();
-      continue;
-    }
-    __syncthreads();
-    const uint32_t count = G.count;
-    // ---- 3. each query of the chunk against the LDS candidates
-    for (int j = 0; j < 64; j++) {
-      if (!((vmask >> j) & 1ull)) continue;
-      if (a.dbg & 4) {
-        if (lane == 0) { snum[j] = 0; smax[j] = 0.0f; }
-        continue;
-      }
-      float qx = __shfl(qp.x, j, 64), qy = __shfl(qp.y, j, 64), qz = __shfl(qp.z, j, 64);
-      float lim2 = query_lim2(a, G, qx, qy, qz);
-      // key = d2 bits << 32 | LDS slot; ~0 = not a candidate (beyond the bound or past count)
-      uint64_t key[PER];
-      uint32_t nvalid = 0;
-      float mn = INFINITY, mx = -INFINITY;
-#pragma unroll
-      for (int u = 0; u < PER; u++) {
-        uint32_t s = (uint32_t)(u * 64 + lane);
-        key[u] = ~0ull;
-        if (s < count) {
-          float d2 = metric(qx, qy, qz, cpos[s]);
-          if (d2 <= lim2) {
-            key[u] = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)s;
-            mn = fminf(mn, d2);
-            mx = fmaxf(mx, d2);
-          }
-        }
-        nvalid += (uint32_t)__popcll(__ballot(key[u] != ~0ull));
-      }
-      if (nvalid > (uint32_t)K && !(a.dbg & 1)) wave_select_k<PER>(key, K, mn, mx, hist, cidx, lane);
-      int num = (int)(nvalid > (uint32_t)K ? (uint32_t)K : nvalid);
-      // record the kept slots of query j (order: slot-major, then lane) and its K-th d2
-      float km = 0.0f;
-      uint32_t base = 0;
-#pragma unroll
-      for (int u = 0; u < PER; u++) {
-        bool kp = key[u] != ~0ull;
-        uint64_t bm = __ballot(kp);
-        if (kp) {
-          sel[j * 64 + base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull))] =
-              (SlotT)(uint32_t)key[u];
-          km = fmaxf(km, __uint_as_float((uint32_t)(key[u] >> 32)));
-        }
-        base += (uint32_t)__popcll(bm);
-      }
-      km = wmaxf(km);
-      if (lane == 0) {
-        snum[j] = num;
-        smax[j] = km;
-      }
-    }
-    __syncthreads();
-    P.lap(2);
-    if (valid) {
-      int num = snum[lane];
-      if (!(a.dbg & 2))
-        chunk_estimate(a, qi, qp, num, smax[lane], cpos, crgbe,
-                       [&](int s) { return (uint32_t)sel[lane * 64 + s]; });
-      st_q += 1;
-      st_found += (uint64_t)num;
-      st_vis += count;
-    }
-    __syncthreads();
-    P.lap(3);
-  }
-  chunk_flush_stats(a, P, st_q, st_found, st_vis);
-}
-
-// ---------------------------------------------------------------------------------------------
-// per-lane heaps over centre-sorted candidates (experiment, slower; kept for comparison)
-// ---------------------------------------------------------------------------------------------
-// ascending bitonic sort of PER*64 u64 keys held as key[u] at index u*64 + lane
-template <int PER>
-__device__ __forceinline__ void wave_bitonic_sort(uint64_t (&k)[PER], int lane) {
-  constexpr int N = PER * 64;
-#pragma unroll
-  for (int size = 2; size <= N; size <<= 1) {
-#pragma unroll
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      if (stride >= 64) {
-        const int us = stride >> 6;
-#pragma unroll
-        for (int u = 0; u < PER; u++) {
-          int pu = u ^ us;
-          if (pu <= u) continue;
-          bool asc = (((u * 64 + lane) & size) == 0);
-          uint64_t x = k[u], y = k[pu];
-          if ((x > y) == asc) { k[u] = y; k[pu] = x; }
-        }
-      } else {
-#pragma unroll
-        for (int u = 0; u < PER; u++) {
-          bool asc = (((u * 64 + lane) & size) == 0);
-          uint64_t o = (uint64_t)__shfl_xor((long long)k[u], stride, 64);
-          bool lower = (lane & stride) == 0;
-          k[u] = (lower == asc) ? (k[u] < o ? k[u] : o) : (k[u] > o ? k[u] : o);
-        }
-      }
-    }
-  }
-}
-
-template <int CAPC>
-__global__ __launch_bounds__(64) void knn_chunk_heap_kernel(KnnArgs a) {
-  constexpr int PER = CAPC / 64;
-  __shared__ float4 cpos[CAPC];
-  __shared__ uint32_t cidx[CAPC];
-  __shared__ uint32_t crgbe[CAPC];
-  __shared__ uint32_t hist[256];
-  __shared__ uint32_t stk[64];  // kd walk stack (walk_within)
-  __shared__ uint16_t ord[CAPC];      // candidate slots sorted by distance to the chunk centre
-  extern __shared__ uint64_t hsm[];   // per-lane 4-ary heaps [K][64]
-  uint64_t *h = hsm + threadIdx.x;
-  const int lane = threadIdx.x;
-  const int K = a.K;
-  uint64_t st_q = 0, st_found = 0, st_vis = 0;
-  ChunkProf P;
-  P.on = false;
-  P.t = 0;
-  for (int i = 0; i < 10; i++) P.c[i] = 0;
-  for (int64_t chunk = blockIdx.x; chunk * 64 < a.nq; chunk += gridDim.x) {
-    bool valid;
-    int64_t qi;
-    float4 qp;
-    chunk_load_query(a, chunk, lane, valid, qi, qp);
-    uint64_t vmask = __ballot(valid);
-    if (vmask == 0) continue;
-    ChunkGeom G;
-    chunk_bound_gather<CAPC>(a, lane, valid, qp, CAPC, cpos, cidx, crgbe, hist, stk, G, P);
-    if (G.overflow) {
-      to_fallback(a, vmask, valid, qi, lane);
-      __syncthreads();
-      continue;
-    }
-    __syncthreads();
-    const uint32_t count = G.count;
-    // ---- 3. sort the candidates by distance to c, then every lane scans them for its own
-    //         query into its LDS heap: all lanes read the same candidate (LDS broadcast), and
-    //         near-first order keeps replacements rare after the Floyd-built fill
-    {
-      uint64_t kc[PER];
-#pragma unroll
-      for (int u = 0; u < PER; u++) {
-        uint32_t s = (uint32_t)(u * 64 + lane);
-        kc[u] = ~0ull;
-        if (s < count) {
-          float dd = metric(G.cx, G.cy, G.cz, cpos[s]);
-          kc[u] = ((uint64_t)__float_as_uint(dd) << 32) | (uint64_t)s;
-        }
-      }
-      wave_bitonic_sort<PER>(kc, lane);
-#pragma unroll
-      for (int u = 0; u < PER; u++) {
-        uint32_t i = (uint32_t)(u * 64 + lane);
-        if (i < count) ord[i] = (uint16_t)(uint32_t)kc[u];
-      }
-    }
-    __syncthreads();
-    int size = 0;
-    if (!(a.dbg & 4)) {
-      float lim2 = valid ? query_lim2(a, G, qp.x, qp.y, qp.z) : 0.0f;
-      uint64_t lim = valid ? (((uint64_t)__float_as_uint(lim2) + 1ull) << 32) : 0ull;
-      for (uint32_t i = 0; i < count; i++) {
-        uint32_t slot = ord[i];
-        float d2 = metric(qp.x, qp.y, qp.z, cpos[slot]);
-        uint64_t key = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)cidx[slot];
-        if (key < lim) heapn_accept<4>(h, size, K, key, lim);
-      }
-    }
-    // ---- 4. estimate from the lane's heap (kd indices mapped back to their LDS slots)
-    if (valid && !(a.dbg & 2)) {
-      float km = size ? __uint_as_float((uint32_t)(h[0] >> 32)) : 0.0f;
-      chunk_estimate(a, qi, qp, size, km, cpos, crgbe, [&](int s) {
-        uint32_t id = (uint32_t)h[s * 64];
-        uint32_t slot = 0;
-        for (uint32_t t = 0; t < count; t++)
-          if (cidx[t] == id) { slot = t; break; }
-        return slot;
-      });
-    }
-    if (valid) {
-      st_q += 1;
-      st_found += (uint64_t)size;
-      st_vis += count;
-    }
-    __syncthreads();
-  }
-  chunk_flush_stats(a, P, st_q, st_found, st_vis);
-}
-
 // dense copy of the striped fallback list: block b copies stripe b % FB_QS after the fills of
 // the stripes before it
 __global__ __launch_bounds__(256) void fb_compact_kernel(const uint32_t *list, const uint32_t *count,
@@ -1306,31 +1075,13 @@ bool launch_knn_chunk_big(const KnnArgs &a, int cap, hipStream_t st) {
   return true;
 }
 
-// variant: 0 wave select, 1 per-lane heaps, 2 lane select
-bool launch_knn_chunk(const KnnArgs &a, int cap, int variant, hipStream_t st) {
+// lane-select chunk kernel (K <= 64), 4 waves per SIMD (3 and 2 measured +4 % and +40 %)
+bool launch_knn_chunk(const KnnArgs &a, hipStream_t st) {
   if (a.nq == 0) return true;
   if (a.mode == KNN_MODE_LIST || a.K > 64) return false;
   unsigned grid = knn_chunk_grid(a.nq);
-  static const int wpe = getenv("GI_CHUNK_WPE") ? atoi(getenv("GI_CHUNK_WPE")) : 4;
-  if (variant == 1) {
-    size_t lds = (size_t)a.K * 64 * sizeof(uint64_t);
-    if (cap <= 256) knn_chunk_heap_kernel<256><<<grid, 64, lds, st>>>(a);
-    else knn_chunk_heap_kernel<512><<<grid, 64, lds, st>>>(a);
-    return true;
-  }
-  if (variant == 2) {
-    if (a.dbg & 16) knn_chunk_lane_kernel<3, true><<<grid, 64, 0, st>>>(a);
-    else if (wpe >= 4) knn_chunk_lane_kernel<4, false><<<grid, 64, 0, st>>>(a);
-    else if (wpe == 3) knn_chunk_lane_kernel<3, false><<<grid, 64, 0, st>>>(a);
-    else knn_chunk_lane_kernel<2, false><<<grid, 64, 0, st>>>(a);
-    return true;
-  }
-  if (cap <= 256) {
-    if (wpe >= 4) knn_chunk_kernel<256, 4><<<grid, 64, 0, st>>>(a);
-    else if (wpe == 3) knn_chunk_kernel<256, 3><<<grid, 64, 0, st>>>(a);
-    else knn_chunk_kernel<256, 2><<<grid, 64, 0, st>>>(a);
-  } else if (cap <= 512) knn_chunk_kernel<512, 2><<<grid, 64, 0, st>>>(a);
-  else knn_chunk_kernel<1024, 1><<<grid, 64, 0, st>>>(a);
+  if (a.dbg & 16) knn_chunk_lane_kernel<3, true><<<grid, 64, 0, st>>>(a);
+  else knn_chunk_lane_kernel<4, false><<<grid, 64, 0, st>>>(a);
   return true;
 }
 

@@ -188,7 +188,7 @@ int gi_knn_batch(gi_ctx *ctx, int map, int64_t n, const double *points, int k, d
                  int32_t *idx_out, float *d2_out, int32_t *nfound);
 /* Diagnostics: time the k-NN estimate kernel over n resident queries (Morton-ordered as in
  * rendering; mode 0 radiance, 1 irradiance, 2 list) for `iters` launches with the given
- * kernel (-1 = default, 0 per-lane, 1 query-per-wave, 2 packet). Uses the context's
+ * kernel (-1 = default; else a GI_KNN_KERNEL kind of gi_host.cpp run_knn). Uses the context's
  * estimate size / distance / filter for `map`. Outputs average ms per launch and the
  * photons found / visited per query. No reference counterpart (measurement only). */
 int gi_knn_bench(gi_ctx *ctx, int map, int64_t n, const double *points, const double *normals,

@@ -1,18 +1,16 @@
-"""Every k-NN kernel variant against the oracle (R3Kdtree::FindClosestQuick, R3Kdtree.cpp:
-688-848; EstimateRadiance photon_utils.cpp:72-162).
+"""Every k-NN kernel the render and the test seams launch, against the oracle
+(R3Kdtree::FindClosestQuick, R3Kdtree.cpp:688-848; EstimateRadiance photon_utils.cpp:72-162).
 
-The variants are chosen when a context is created (gi_host.cpp tuning environment):
-GI_KNN_KERNEL 0 = per-lane LDS heap, 1 = query per wave, 2 = packet, 3 = per-lane with
-batched inserts, 4 = L-lane groups (GI_GROUP_LANES). Each must return the oracle's k-NN sets
-exactly: the fp32 metric is shared, and only photons tied at the k-th distance may differ.
-GI_KNN_KERNEL 5-7 = chunk kernels, 8 = the large-K chunk kernel (bitmask selection, bounds from
-per-photon K-th distances); GI_CHUNK_MINSUB sets how far an overflowing chunk is split
-(1 = down to single queries, 64 = straight to the per-lane fallback). GI_KNN_DK=0 turns off the
-wave kernel's and the chunk fallback's start from per-photon K-th distance bounds (on by
-default); GI_CHUNK_DK=1 takes the chunk kernel's centre bound from them too; GI_CHUNK_FB_ALL=1
-sends every query of the lane-select chunk kernel to its per-lane fallback.
-It must also return its EstimateRadiance within rtol 1e-10 (fp64 sums in a different order).
-Leaf sizes are varied too, because the result set may not depend on the tree shape."""
+The kernel is chosen when a context is created (gi_host.cpp run_knn): GI_KNN_KERNEL 7 = chunk
+kernel with lane select + per-lane fallback (the K <= 64 default), 3 = per-lane kernel (list
+mode), 8 = large-K chunk kernel + query-per-wave fallback (the K > 64 default), 1 = query per
+wave, 0 = per-lane with global-memory heaps (any K). GI_CHUNK_MINSUB sets how far an
+overflowing chunk is split (1 = down to single queries, 64 = straight to the fallback);
+GI_KNN_DK=0 turns off the start from per-photon K-th distance bounds; GI_CHUNK_FB_ALL=1 sends
+every query of the chunk kernel to its fallback. Each must return the oracle's k-NN sets exactly
+(the fp32 metric is shared; only photons tied at the k-th distance may differ) and its
+EstimateRadiance within rtol 1e-10 (fp64 sums in a different order). Leaf sizes are varied
+too, because the result set may not depend on the tree shape."""
 import os
 
 import numpy as np
@@ -29,27 +27,15 @@ VARIANTS = [
     {"GI_KNN_KERNEL": "0", "GI_LEAF_SIZE": "16"},
     {"GI_KNN_KERNEL": "1", "GI_LEAF_SIZE": "512"},
     {"GI_KNN_KERNEL": "1", "GI_KNN_DK": "0"},
-    {"GI_KNN_KERNEL": "2"},
-    {"GI_KNN_KERNEL": "3", "GI_LANE_CHUNK": "4"},
-    {"GI_KNN_KERNEL": "3", "GI_LANE_CHUNK": "16", "GI_LEAF_SIZE": "32"},
-    {"GI_KNN_KERNEL": "4", "GI_GROUP_LANES": "8"},
-    {"GI_KNN_KERNEL": "4", "GI_GROUP_LANES": "16", "GI_SEL_SLACK": "1"},
-    {"GI_KNN_KERNEL": "4", "GI_GROUP_LANES": "32", "GI_LEAF_SIZE": "128"},
-    {"GI_KNN_KERNEL": "5"},
-    {"GI_KNN_KERNEL": "5", "GI_CHUNK_CAP": "256", "GI_LEAF_SIZE": "50"},
-    {"GI_KNN_KERNEL": "6"},
-    {"GI_KNN_KERNEL": "6", "GI_CHUNK_CAP": "256"},
+    {"GI_KNN_KERNEL": "3", "GI_LEAF_SIZE": "32"},
     {"GI_KNN_KERNEL": "7"},
     {"GI_KNN_KERNEL": "7", "GI_LEAF_SIZE": "50"},
     {"GI_KNN_KERNEL": "7", "GI_CHUNK_MINSUB": "1"},
-    {"GI_KNN_KERNEL": "7", "GI_CHUNK_MINSUB": "64"},
-    {"GI_KNN_KERNEL": "7", "GI_CHUNK_DK": "1"},
-    {"GI_KNN_KERNEL": "7", "GI_CHUNK_FB_ALL": "1"},
+    {"GI_KNN_KERNEL": "7", "GI_CHUNK_DK": "0"},
     {"GI_KNN_KERNEL": "7", "GI_CHUNK_FB_ALL": "1", "GI_KNN_DK": "0"},
     {"GI_KNN_KERNEL": "8"},
     {"GI_KNN_KERNEL": "8", "GI_CHUNK_CAP_BIG": "384", "GI_LEAF_SIZE": "128"},
     {"GI_KNN_KERNEL": "8", "GI_CHUNK_MINSUB_BIG": "1"},
-    {"GI_KNN_KERNEL": "8", "GI_CHUNK_MINSUB_BIG": "64"},
 ]
 
 

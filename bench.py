@@ -25,7 +25,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "global-illumination_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
-SCENE = os.path.join(ROOT, "tests", "scenes", "cornell.scn")
+SCENES = os.path.join(ROOT, "tests", "scenes")
 HBM_PEAK_GBPS = 8000.0
 BYTES_PER_PHOTON = 16   # compulsory photon record gather
 BYTES_PER_SAMPLE = 12   # f32 RGB pixel write
@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--caustic-photons", type=int, default=1000000)
     ap.add_argument("--tile", type=int, default=16)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--scene", default="cornell.scn", help="scene under tests/scenes (C2: cornell)")
+    ap.add_argument("--extra", default="", help="extra reference flags, e.g. '-dof 4 12.2 0.025'")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-res", type=int, default=8, help="CPU baseline sample: res x res px")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -76,14 +78,14 @@ def cpu_baseline(a):
     identical per-sample workload)."""
     import oracle_lib
     threads = a.cpu_threads or min(16, os.cpu_count() or 1)
-    args = [SCENE, "/tmp/cpu.png", "-resolution", str(a.cpu_res), str(a.cpu_res), "-aa",
-            str(a.aa), "-global", str(a.global_photons), "-caustic", str(a.caustic_photons),
-            "-threads", str(threads), "-seed", str(a.seed)]
+    args = [os.path.join(SCENES, a.scene), "/tmp/cpu.png", "-resolution", str(a.cpu_res),
+            str(a.cpu_res), "-aa", str(a.aa), "-global", str(a.global_photons), "-caustic",
+            str(a.caustic_photons), "-threads", str(threads), "-seed", str(a.seed)] + a.extra.split()
     _, st = oracle_lib.render(args, a.cpu_res, a.cpu_res)
     samples = a.cpu_res * a.cpu_res * 4 ** a.aa
     return {"value": samples / st["render_s"] / 1e6, "unit": "Mpixel-samples/s",
             "cores": threads, "kind": "port",
-            "sample": f"cornell.scn {a.cpu_res}x{a.cpu_res} aa={a.aa} ({samples} pixel-samples), "
+            "sample": f"{a.scene} {a.cpu_res}x{a.cpu_res} aa={a.aa} ({samples} pixel-samples), "
                       f"{a.global_photons}+{a.caustic_photons} photons; render {st['render_s']:.2f} s, "
                       f"photon map {st['trace_s'] + st['kd_s']:.2f} s on {threads} threads"}
 
@@ -103,9 +105,9 @@ def main():
         dist.init_process_group(backend=backend)
     import gi_amd
 
-    args = [SCENE, "/tmp/bench.png", "-resolution", str(a.res), str(a.res), "-aa", str(a.aa),
-            "-global", str(a.global_photons), "-caustic", str(a.caustic_photons),
-            "-seed", str(a.seed)]
+    args = [os.path.join(SCENES, a.scene), "/tmp/bench.png", "-resolution", str(a.res),
+            str(a.res), "-aa", str(a.aa), "-global", str(a.global_photons), "-caustic",
+            str(a.caustic_photons), "-seed", str(a.seed)] + a.extra.split()
     p, sc, _o, w, h, aa, real = gi_amd.ParseArgs(args)
     r = gi_amd.Renderer(local, p)
     r.ReadScene(sc, real)
@@ -202,8 +204,8 @@ def main():
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_per_step, 2),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": "f64 (shading/geometry), f32 (photon positions)", "data": "synthetic",
-            "config": {"workload": f"cornell.scn {w}x{h} aa={aa} "
-                                   f"{a.global_photons}+{a.caustic_photons} photons",
+            "config": {"workload": f"{a.scene} {w}x{h} aa={aa} "
+                                   f"{a.global_photons}+{a.caustic_photons} photons {a.extra}".strip(),
                        "pixel_samples_per_frame": samples_per_frame,
                        "parallelism": f"tiles{a.tile}x{a.tile} % {world}",
                        "photon_map_s": round(photon_s, 3),

@@ -112,6 +112,7 @@ struct SceneView {
   const DElement *elems;
   const DShape *shapes;
   const DTri *tris;
+  const DBvhNode *bvh;
   const DMaterial *mats;
   const DLight *lights;
   int32_t nnodes, nelems, nlights;
@@ -324,6 +325,62 @@ GI_HD bool ray_cylinder(V o, V R, V p1, V p2, double radius, double &t_out, V &p
   return true;
 }
 
+// Slab test of a ray against a BVH node box for parameters in [-2e-6, bound] (a mesh hit may
+// have t in [-1e-6, 0), Q2). inv = 1 / direction per axis (+-inf on a zero component: the slab
+// then spans everything or nothing). The boxes carry a margin (gi_layout.h DBvhNode), so the
+// test is conservative for every triangle hit R3Intersects(ray, R3TriangleArray) can report.
+__device__ __forceinline__ bool bvh_box(const DBvhNode &b, V o, V inv, double bound) {
+  double t0 = -2.0e-6, t1 = bound;
+  double ta = (b.lo[0] - o.x) * inv.x, tb = (b.hi[0] - o.x) * inv.x;
+  t0 = fmax(t0, fmin(ta, tb));
+  t1 = fmin(t1, fmax(ta, tb));
+  ta = (b.lo[1] - o.y) * inv.y; tb = (b.hi[1] - o.y) * inv.y;
+  t0 = fmax(t0, fmin(ta, tb));
+  t1 = fmin(t1, fmax(ta, tb));
+  ta = (b.lo[2] - o.z) * inv.z; tb = (b.hi[2] - o.z) * inv.z;
+  t0 = fmax(t0, fmin(ta, tb));
+  t1 = fmin(t1, fmax(ta, tb));
+  return t0 <= t1;
+}
+
+// R3Intersects(ray, R3TriangleArray) (R3Isect.cpp:800-833) through the mesh's BVH: the same
+// minimum t over every triangle ray_tri accepts (t >= -1e-6, Q2), the same tie rule as the
+// file-order loop (equal t: lowest triangle index), visiting only boxes the ray meets below the
+// current minimum. Stackless pre-order walk with skip links.
+__device__ __noinline__ bool ray_mesh_bvh(const SceneView &S, const DShape &sh, V o, V d, double &t,
+                                          V &p, V &n, double tmax) {
+  const DBvhNode *B = S.bvh + sh.bvh_first;
+  const DTri *T = S.tris + sh.tri_first;
+  const V inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+  bool found = false;
+  double mt = 3.40282346638528859811704183484516925440e+38;  // FLT_MAX, as the linear loop
+  int32_t midx = 0x7fffffff;
+  const int end = B[0].skip;
+  int i = 0;
+  while (i < end) {
+    const DBvhNode &nd = B[i];
+    if (!bvh_box(nd, o, inv, fmin(mt, tmax))) {
+      i = nd.skip;
+      continue;
+    }
+    for (int k = 0; k < nd.tri_count; k++) {
+      const DTri &tr = T[nd.tri_first + k];
+      double tt;
+      V pp;
+      if (ray_tri(o, d, tr, tt, pp, tmax) && (tt < mt || (tt == mt && tr.idx < midx))) {
+        found = true;
+        p = pp;
+        n = ld3(tr.n);
+        mt = tt;
+        midx = tr.idx;
+      }
+    }
+    i++;
+  }
+  t = mt;
+  return found;
+}
+
 // shape kinds a kernel instance is compiled for (KINDS template argument): the host launches
 // the smallest instance covering SceneView::kinds, so scenes of triangles and spheres do not
 // carry the mesh/box/cylinder code (registers and instruction cache) through their hot loops
@@ -357,6 +414,7 @@ __device__ __forceinline__ bool shape_intersect(const SceneView &S, const DShape
     }
     case SK_MESH: {
       if (!ray_box(o, d, sh.bmin, sh.bmax, nullptr, nullptr)) return false;
+      if (sh.bvh_first >= 0) return ray_mesh_bvh(S, sh, o, d, t, p, n, tmax);
       bool found = false;
       double mt = 3.40282346638528859811704183484516925440e+38;  // FLT_MAX
       for (int i = 0; i < sh.tri_count; i++) {

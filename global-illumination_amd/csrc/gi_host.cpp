@@ -224,7 +224,7 @@ struct gi_ctx {
   bool have_scene = false;
   HostScene scene;
   // device scene
-  DBuf d_nodes, d_elems, d_shapes, d_tris, d_mats, d_lights, d_lut, d_stats;
+  DBuf d_nodes, d_elems, d_shapes, d_tris, d_bvh, d_mats, d_lights, d_lut, d_stats;
   // photon maps
   HostMap hmap[2];
   DevMap dmap[2];
@@ -309,6 +309,7 @@ SceneView make_view(gi_ctx *c) {
   S.elems = c->d_elems.as<DElement>();
   S.shapes = c->d_shapes.as<DShape>();
   S.tris = c->d_tris.as<DTri>();
+  S.bvh = c->d_bvh.as<DBvhNode>();
   S.mats = c->d_mats.as<DMaterial>();
   S.lights = c->d_lights.as<DLight>();
   S.nnodes = (int)H.nodes.size();
@@ -1137,7 +1138,7 @@ int gi_create(gi_ctx **out, int dev) {
 void gi_destroy(gi_ctx *c) {
   if (!c) return;
   hipSetDevice(c->device);
-  DBuf *bufs[] = {&c->d_nodes, &c->d_elems, &c->d_shapes, &c->d_tris, &c->d_mats, &c->d_lights,
+  DBuf *bufs[] = {&c->d_nodes, &c->d_elems, &c->d_shapes, &c->d_tris, &c->d_bvh, &c->d_mats, &c->d_lights,
                   &c->d_lut, &c->d_stats, &c->spawn, &c->npaths, &c->path_off, &c->base,
                   &c->pixels, &c->rgbf, &c->rgb8, &c->qcount,
                   &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont, &c->mc_cont, &c->mc_ncont, &c->prim_rgb, &c->ind_tab, &c->mc_tab};
@@ -1192,6 +1193,7 @@ int gi_read_scene(gi_ctx *c, const char *path, int real) {
   HIPCHK(c, upload(c->d_elems, H.elems.data(), H.elems.size() * sizeof(DElement), c->stream));
   HIPCHK(c, upload(c->d_shapes, H.shapes.data(), H.shapes.size() * sizeof(DShape), c->stream));
   HIPCHK(c, upload(c->d_tris, H.tris.data(), H.tris.size() * sizeof(DTri), c->stream));
+  HIPCHK(c, upload(c->d_bvh, H.bvh.data(), H.bvh.size() * sizeof(DBvhNode), c->stream));
   HIPCHK(c, upload(c->d_mats, H.mats.data(), H.mats.size() * sizeof(DMaterial), c->stream));
   HIPCHK(c, upload(c->d_lights, H.lights.data(), H.lights.size() * sizeof(DLight), c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -7,6 +7,7 @@
 //   DElement[] elements in (node pre-order, element order); material + shape range + bbox
 //   DShape[]   shapes in element order; triangles / meshes index into DTri[]
 //   DTri[]     triangles with precomputed plane and edge planes (R3Cont.cpp:491-512)
+//   DBvhNode[] per-mesh linearised BVHs over the mesh's triangles (see DBvhNode)
 // Everything geometric is fp64 (RNScalar is double; the 1e-6 tolerances of RNScalar.h:225-316
 // need it). Photon maps are fp32 (see DESIGN.md "Data layout").
 #pragma once
@@ -27,13 +28,31 @@ struct DTri {
   double ev[3][3];   // edge-plane normals  normalize(n x e_i)
   double ed[3];      // edge-plane offsets
   double bmin[3], bmax[3];
+  int32_t idx;       // index within its mesh in file order (BVH leaves reorder the triangles;
+                     // ties of the mesh's minimum t go to the lowest idx, R3Isect.cpp:813-829)
+  int32_t pad;
+};
+
+// Linearised BVH of one mesh (R3TriangleArray) in depth-first pre-order: node i's first child is
+// i + 1, and `skip` is the node after its subtree (the root's skip = the node count), so a walk
+// needs no stack: descend to i + 1 when the ray meets the box, else jump to skip. Leaves hold
+// triangles [tri_first, tri_first + tri_count) relative to the mesh's first triangle. Boxes are
+// the union of the triangles' boxes widened by a margin larger than the 1e-6 containment
+// tolerances of R3Contains(triangle) (R3Cont.cpp:491-512), so no triangle R3Intersects(ray,
+// R3TriangleArray) would report is ever culled.
+struct DBvhNode {
+  double lo[3], hi[3];
+  int32_t skip;
+  int32_t tri_first;   // leaf: first triangle (mesh-relative); internal: -1
+  int32_t tri_count;   // leaf: triangle count; internal: 0
+  int32_t pad;
 };
 
 struct DShape {
   int32_t kind;
   int32_t tri_first;   // SK_TRI: triangle index; SK_MESH: first triangle
   int32_t tri_count;   // SK_MESH: number of triangles
-  int32_t pad;
+  int32_t bvh_first;   // SK_MESH: root of its DBvhNode tree, -1 = no tree (small meshes)
   double c[3];         // sphere / circle centre
   double n[3];         // circle normal
   double r;            // radius

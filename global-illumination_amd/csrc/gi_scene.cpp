@@ -7,6 +7,7 @@
 #include "gi_scene.h"
 #include <array>
 #include <cfloat>
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -507,6 +508,67 @@ static void xform_box(const double *T, const Bx &b, Bx &out) {
   }
 }
 
+// ---- per-mesh BVH (DBvhNode, gi_layout.h) ----------------------------------------------
+// Top-down median split of the triangle centroids along the longest axis of their box, leaves of
+// at most BVH_LEAF triangles, nodes emitted in pre-order with skip links. Box margin: the
+// containment tolerances of a triangle hit are 1e-6 per coordinate (R3Cont.cpp:491-512), so a
+// reported hit point lies within 1e-6 of its triangle's box; 1e-5 + 1e-9 |x| keeps every such
+// point strictly inside its node boxes, with room for the slab test's rounding.
+constexpr int BVH_LEAF = 4;
+constexpr int BVH_MIN_TRIS = 16;  // smaller meshes keep the linear loop
+
+static int bvh_rec(std::vector<DTri> &t, int a, int b, std::vector<DBvhNode> &out) {
+  int id = (int)out.size();
+  out.push_back(DBvhNode());
+  DBvhNode nd;
+  memset(&nd, 0, sizeof nd);
+  Bx box, cb;
+  for (int i = a; i < b; i++) {
+    box.add(t[i].bmin);
+    box.add(t[i].bmax);
+    double c[3];
+    for (int k = 0; k < 3; k++) c[k] = (t[i].bmin[k] + t[i].bmax[k]) * 0.5;
+    cb.add(c);
+  }
+  for (int k = 0; k < 3; k++) {
+    nd.lo[k] = box.mn[k] - (1e-5 + 1e-9 * fabs(box.mn[k]));
+    nd.hi[k] = box.mx[k] + (1e-5 + 1e-9 * fabs(box.mx[k]));
+  }
+  if (b - a <= BVH_LEAF) {
+    nd.tri_first = a;
+    nd.tri_count = b - a;
+    nd.skip = id + 1;
+    out[id] = nd;
+    return id;
+  }
+  int axis = 0;
+  double ext = cb.mx[0] - cb.mn[0];
+  for (int k = 1; k < 3; k++)
+    if (cb.mx[k] - cb.mn[k] > ext) { axis = k; ext = cb.mx[k] - cb.mn[k]; }
+  int mid = (a + b) / 2;
+  std::nth_element(t.begin() + a, t.begin() + mid, t.begin() + b, [axis](const DTri &x, const DTri &y) {
+    double cx = x.bmin[axis] + x.bmax[axis], cy = y.bmin[axis] + y.bmax[axis];
+    return cx < cy || (cx == cy && x.idx < y.idx);
+  });
+  nd.tri_first = -1;
+  nd.tri_count = 0;
+  bvh_rec(t, a, mid, out);
+  bvh_rec(t, mid, b, out);
+  nd.skip = (int)out.size();
+  out[id] = nd;
+  return id;
+}
+
+// reorders `tris` into leaf order and appends the mesh's nodes; returns the root index, or -1
+static int build_mesh_bvh(std::vector<DTri> &tris, std::vector<DBvhNode> &all) {
+  if ((int)tris.size() < BVH_MIN_TRIS) return -1;
+  std::vector<DBvhNode> nodes;
+  bvh_rec(tris, 0, (int)tris.size(), nodes);
+  int base = (int)all.size();
+  all.insert(all.end(), nodes.begin(), nodes.end());  // skip links are relative to the root
+  return base;
+}
+
 // pre-order flatten; returns the node's bbox in parent coordinates (R3SceneNode::UpdateBBox)
 static Bx flatten(Graph &G, int gi_idx, int parent, HostScene &S) {
   GNode &g = G.nodes[gi_idx];
@@ -531,10 +593,14 @@ static Bx flatten(Graph &G, int gi_idx, int parent, HostScene &S) {
     for (auto &s : e.shapes) {
       shape_box(s);
       DShape ds = s.s;
+      ds.bvh_first = -1;
       if (s.s.kind == SK_TRI || s.s.kind == SK_MESH) {
+        std::vector<DTri> tris = s.tris;
+        for (size_t i = 0; i < tris.size(); i++) tris[i].idx = (int32_t)i;
+        if (s.s.kind == SK_MESH) ds.bvh_first = build_mesh_bvh(tris, S.bvh);
         ds.tri_first = (int)S.tris.size();
-        ds.tri_count = (int)s.tris.size();
-        S.tris.insert(S.tris.end(), s.tris.begin(), s.tris.end());
+        ds.tri_count = (int)tris.size();
+        S.tris.insert(S.tris.end(), tris.begin(), tris.end());
       }
       if (s.s.kind == SK_CONE) S.unsupported_shapes = true;
       S.shapes.push_back(ds);

@@ -11,6 +11,7 @@ struct HostScene {
   std::vector<DElement> elems;
   std::vector<DShape> shapes;
   std::vector<DTri> tris;
+  std::vector<DBvhNode> bvh;  // per-mesh BVHs (DShape::bvh_first)
   std::vector<DMaterial> mats;
   std::vector<DLight> lights;
   // camera (R3Camera: eye + triad, R3Triad.cpp:72-79); xfov = yfov (Q5)

@@ -222,3 +222,55 @@ def test_large_map_properties(renderer, name, extra, goal_g, goal_c):
         assert nf[i] == k
         np.testing.assert_allclose(np.sort(d2[i]), np.sort(dd)[:k], rtol=1e-5)
         assert (dd[idx[i]] <= kth * (1 + 1e-5)).all()
+
+
+def _off_triangles(path):
+    with open(path) as f:
+        toks = [t for line in f for t in line.split("#")[0].split()]
+    assert toks[0] == "OFF"
+    nv, nf = int(toks[1]), int(toks[2])
+    v = np.array(toks[4:4 + 3 * nv], dtype=float).reshape(nv, 3)
+    pos, tris = 4 + 3 * nv, []
+    for _ in range(nf):
+        k = int(toks[pos])
+        tris.append([int(x) for x in toks[pos + 1:pos + 1 + k]])
+        pos += 1 + k
+    return v, np.array(tris)
+
+
+@pytest.mark.parametrize("kind", ["surface", "edges", "outside"])
+def test_mesh_bvh_matches_linear_loop(renderer, kind):
+    """The device walks each mesh of >= 16 triangles through its BVH (gi_device.h ray_mesh_bvh);
+    the result must be R3Intersects(ray, R3TriangleArray)'s linear loop exactly: Q2 self-hits
+    from rays leaving the surface (whole mesh missed), rays through shared edges and vertices
+    (equal-t ties go to the lowest triangle index), and rays from outside."""
+    rng = np.random.default_rng({"surface": 1, "edges": 2, "outside": 3}[kind])
+    v, f = _off_triangles(scene("teapot.off"))
+    renderer.ReadScene(scene("teapot.scn"))
+    n = 6000
+    tri = f[rng.integers(0, len(f), n)]
+    a, b, c = v[tri[:, 0]], v[tri[:, 1]], v[tri[:, 2]]
+    if kind == "surface":
+        u = rng.random((n, 2))
+        m = u.sum(1) > 1
+        u[m] = 1 - u[m]
+        org = a + u[:, :1] * (b - a) + u[:, 1:] * (c - a)
+        d = rng.normal(size=(n, 3))
+    elif kind == "edges":
+        w = rng.random((n, 1))
+        tgt = np.where(rng.random((n, 1)) < 0.5, a + w * (b - a), a)  # on an edge or a vertex
+        org = tgt + rng.normal(size=(n, 3)) * 3.0
+        d = tgt - org
+    else:
+        tgt = a + rng.random((n, 1)) * (b - a)
+        org = rng.normal(size=(n, 3)) * 10.0
+        d = tgt - org
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    gh, gt, gp, gn, gm = renderer.Intersects(org, d)
+    oh, ot, op, on, om = oracle_lib.intersect(scene("teapot.scn"), org, d)
+    np.testing.assert_array_equal(gh, oh)
+    both = gh == 1
+    assert both.sum() > (0.05 if kind == "surface" else 0.5) * n
+    np.testing.assert_array_equal(gt[both], ot[both])
+    np.testing.assert_array_equal(gn[both], on[both])
+    np.testing.assert_array_equal(gp[both], op[both])

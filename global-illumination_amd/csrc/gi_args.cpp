@@ -2,7 +2,7 @@
 // image output.
 //   gi_params_default   defaults of photonmap.cpp:27-106
 //   gi_parse_args       ParseArgs, utils/io_utils.cpp:16-212 (same flags, clamps, messages;
-//                       extension: -seed S)
+//                       extensions: -seed S, -gpus N)
 //   gi_write_image      R2Image::Write: .png (bottom-up rows, R2Image.cpp:1430) / .ppm
 #include <cstdio>
 #include <cstdlib>
@@ -140,6 +140,7 @@ int gi_parse_args(int argc, char **argv, gi_params *P, const char **scene, const
         if (*h < 0) *h *= -1;
       }
       else if (!strcmp(a, "-seed") && need(1)) P->seed = strtoull(next(), nullptr, 10);
+      else if (!strcmp(a, "-gpus") && need(1)) P->gpus = atoi(next());
       else return bad(a);
       argv++;
       argc--;

@@ -5,6 +5,8 @@
 // wavefront launches; host code only sequences kernels, runs the adaptive photon-emission
 // bookkeeping and builds the kd-tree (kd build on the GPU is SURVEY.md §8(f) row f1).
 #include <hip/hip_runtime.h>
+#include <dlfcn.h>
+#include <rccl/rccl.h>
 #include <algorithm>
 #include <cfloat>
 #include <chrono>
@@ -12,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -195,6 +198,40 @@ struct DevMap {
 }  // namespace
 
 // =======================================================================================
+// RCCL, opened at run time by multi-device contexts only (gi_create_devices with distinct
+// devices): the single-device library carries no RCCL dependency, and a torch process that
+// loads it keeps its own copy.
+struct Rccl {
+  bool tried = false, ok = false;
+  ncclResult_t (*commInitAll)(ncclComm_t *, int, const int *) = nullptr;
+  ncclResult_t (*commDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*groupStart)() = nullptr;
+  ncclResult_t (*groupEnd)() = nullptr;
+  ncclResult_t (*send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  const char *(*errString)(ncclResult_t) = nullptr;
+  bool load() {
+    static std::mutex mu;
+    std::lock_guard<std::mutex> g(mu);
+    if (tried) return ok;
+    tried = true;
+    void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return false;
+    commInitAll = (decltype(commInitAll))dlsym(h, "ncclCommInitAll");
+    commDestroy = (decltype(commDestroy))dlsym(h, "ncclCommDestroy");
+    groupStart = (decltype(groupStart))dlsym(h, "ncclGroupStart");
+    groupEnd = (decltype(groupEnd))dlsym(h, "ncclGroupEnd");
+    send = (decltype(send))dlsym(h, "ncclSend");
+    recv = (decltype(recv))dlsym(h, "ncclRecv");
+    errString = (decltype(errString))dlsym(h, "ncclGetErrorString");
+    ok = commInitAll && commDestroy && groupStart && groupEnd && send && recv && errString;
+    return ok;
+  }
+};
+Rccl g_rccl;
+
+// =======================================================================================
 // Execution state of one photon map's k-NN launches (stream, timing events, scratch). One per
 // map, so the two maps' estimates can run concurrently on two streams during a render.
 struct MapExec {
@@ -211,6 +248,14 @@ struct MapExec {
 
 struct gi_ctx {
   int device = 0;
+  // Device set (gi_create_devices): this context drives the first device and forwards every
+  // call to one context per further device. Output tiles t go to device t % ndev; photon
+  // emission ranges are split across the devices; the maps are built once and replicated.
+  std::vector<gi_ctx *> peers;
+  std::vector<ncclComm_t> comms;     // [ndev] RCCL communicators (distinct devices), else empty
+  DBuf pack;                         // this device's shard pixels, packed for the gather
+  std::vector<DBuf> recv, peer_pix;  // first device: each peer's packed pixels and pixel list
+  std::mutex err_mu;                 // err is written by the map worker threads too
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;     // side stream: Monte Carlo paths beside the indirect paths
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -265,20 +310,25 @@ struct gi_ctx {
   float sbmin[3] = {0, 0, 0}, sbmax[3] = {1, 1, 1};
 };
 
-#define HIPCHK(ctx, call)                                                        \
-  do {                                                                           \
-    hipError_t _e = (call);                                                      \
-    if (_e != hipSuccess) {                                                      \
-      (ctx)->err = std::string("HIP error: ") + hipGetErrorString(_e) + " at " + \
-                   __FILE__ + ":" + std::to_string(__LINE__);                    \
-      return GI_ERR_HIP;                                                         \
-    }                                                                            \
+static void set_err(gi_ctx *c, const std::string &msg) {
+  std::lock_guard<std::mutex> g(c->err_mu);
+  c->err = msg;
+}
+
+#define HIPCHK(ctx, call)                                                                   \
+  do {                                                                                      \
+    hipError_t _e = (call);                                                                 \
+    if (_e != hipSuccess) {                                                                 \
+      set_err((ctx), std::string("HIP error: ") + hipGetErrorString(_e) + " at " + __FILE__ + \
+                         ":" + std::to_string(__LINE__));                                   \
+      return GI_ERR_HIP;                                                                    \
+    }                                                                                       \
   } while (0)
 
 namespace {
 
 int fail(gi_ctx *c, int code, const std::string &msg) {
-  c->err = msg;
+  set_err(c, msg);
   return code;
 }
 
@@ -428,9 +478,10 @@ double light_power(const HostScene &S, const DLight &L) {
   return (L.color[0] + L.color[1] + L.color[2]) * area * flux;
 }
 
-// trace photons [e0, e0+n) of one light and append the stored ones (emission order)
-int trace_batch(gi_ctx *c, int caustic, int light, int64_t e0, int64_t n,
-                std::vector<gi_photon> &out) {
+// trace photons [e0, e0+n) of one light on this context's device and append the stored ones
+// (emission order)
+int trace_batch_dev(gi_ctx *c, int caustic, int light, int64_t e0, int64_t n,
+                    std::vector<gi_photon> &out) {
   const int64_t CH = 1 << 22;
   for (int64_t s = 0; s < n; s += CH) {
     int64_t m = std::min(CH, n - s);
@@ -465,6 +516,57 @@ int trace_batch(gi_ctx *c, int caustic, int light, int64_t e0, int64_t n,
                              hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
+  return GI_OK;
+}
+
+// Run fn(k, ctx_k) for every device of the set on its own host thread (k = 0 is this context);
+// returns the first failure, with that device's message copied into c->err.
+template <typename Fn>
+int on_devices(gi_ctx *c, Fn fn) {
+  const int nd = 1 + (int)c->peers.size();
+  if (nd == 1) return fn(0, c);
+  std::vector<int> rc(nd, GI_OK);
+  std::vector<std::thread> th;
+  for (int k = 0; k < nd; k++) {
+    gi_ctx *d = k ? c->peers[k - 1] : c;
+    th.emplace_back([&, k, d]() {
+      if (hipSetDevice(d->device) != hipSuccess) {
+        rc[k] = fail(d, GI_ERR_HIP, "hipSetDevice failed");
+        return;
+      }
+      try {
+        rc[k] = fn(k, d);
+      } catch (const std::bad_alloc &) {
+        rc[k] = fail(d, GI_ERR_ALLOC, "host allocation failed");
+      } catch (...) {
+        rc[k] = fail(d, GI_ERR_HIP, "unexpected exception");
+      }
+    });
+  }
+  for (auto &t : th) t.join();
+  hipSetDevice(c->device);
+  for (int k = 0; k < nd; k++)
+    if (rc[k] != GI_OK) {
+      if (k) set_err(c, "device " + std::to_string(c->peers[k - 1]->device) + ": " + c->peers[k - 1]->err);
+      return rc[k];
+    }
+  return GI_OK;
+}
+
+// trace photons [e0, e0+n) of one light: on a device set the range is cut into one contiguous
+// piece per device (the RNG is keyed by emission index, so the concatenation in device order
+// is the one-device result photon for photon)
+int trace_batch(gi_ctx *c, int caustic, int light, int64_t e0, int64_t n,
+                std::vector<gi_photon> &out) {
+  const int nd = 1 + (int)c->peers.size();
+  if (nd == 1 || n < 4096 * (int64_t)nd) return trace_batch_dev(c, caustic, light, e0, n, out);
+  std::vector<std::vector<gi_photon>> part(nd);
+  int rc = on_devices(c, [&](int k, gi_ctx *d) -> int {
+    int64_t a = e0 + n * k / nd, b = e0 + n * (k + 1) / nd;
+    return trace_batch_dev(d, caustic, light, a, b - a, part[k]);
+  });
+  if (rc) return rc;
+  for (auto &p : part) out.insert(out.end(), p.begin(), p.end());
   return GI_OK;
 }
 
@@ -1003,9 +1105,18 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
       HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork2, 0));
       c->mx[1].st = c->stream2;
       worker = std::thread([&]() {
-        hipSetDevice(c->device);  // the current device is per host thread
-        rcm[1] = knn_list(c, 1, a.qpos[1], a.qshade[1], nq[1], c->qout[1].as<double>(),
-                          rs ? &knn_ms[1] : nullptr);
+        if (hipSetDevice(c->device) != hipSuccess) {  // the current device is per host thread
+          rcm[1] = fail(c, GI_ERR_HIP, "k-NN worker: hipSetDevice failed");
+          return;
+        }
+        try {
+          rcm[1] = knn_list(c, 1, a.qpos[1], a.qshade[1], nq[1], c->qout[1].as<double>(),
+                            rs ? &knn_ms[1] : nullptr);
+        } catch (const std::bad_alloc &) {
+          rcm[1] = fail(c, GI_ERR_ALLOC, "k-NN worker: host allocation failed");
+        } catch (...) {
+          rcm[1] = fail(c, GI_ERR_HIP, "k-NN worker: unexpected exception");
+        }
       });
     }
     for (int l = 0; l < 2; l++) {
@@ -1065,6 +1176,40 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     }
   }
   return GI_OK;
+}
+
+int upload_scene(gi_ctx *c) {
+  HostScene &H = c->scene;
+  HIPCHK(c, upload(c->d_nodes, H.nodes.data(), H.nodes.size() * sizeof(DNode), c->stream));
+  HIPCHK(c, upload(c->d_elems, H.elems.data(), H.elems.size() * sizeof(DElement), c->stream));
+  HIPCHK(c, upload(c->d_shapes, H.shapes.data(), H.shapes.size() * sizeof(DShape), c->stream));
+  HIPCHK(c, upload(c->d_tris, H.tris.data(), H.tris.size() * sizeof(DTri), c->stream));
+  HIPCHK(c, upload(c->d_bvh, H.bvh.data(), H.bvh.size() * sizeof(DBvhNode), c->stream));
+  HIPCHK(c, upload(c->d_mats, H.mats.data(), H.mats.size() * sizeof(DMaterial), c->stream));
+  HIPCHK(c, upload(c->d_lights, H.lights.data(), H.lights.size() * sizeof(DLight), c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->have_scene = true;
+  c->map_valid[0] = c->map_valid[1] = false;
+  for (int i = 0; i < 3; i++) {
+    c->sbmin[i] = (float)H.bmin[i];
+    c->sbmax[i] = (float)H.bmax[i];
+  }
+  return GI_OK;
+}
+
+// the first device's photon maps (host copies + kd trees) and parameters onto the others
+int replicate_maps(gi_ctx *c) {
+  if (c->peers.empty()) return GI_OK;
+  return on_devices(c, [&](int k, gi_ctx *d) -> int {
+    if (k == 0) return GI_OK;
+    d->P = c->P;
+    for (int m = 0; m < 2; m++) {
+      d->hmap[m] = c->hmap[m];
+      int rc = upload_map(d, m);
+      if (rc) return rc;
+    }
+    return (int)GI_OK;
+  });
 }
 
 int check_ready(gi_ctx *c) {
@@ -1135,14 +1280,58 @@ int gi_create(gi_ctx **out, int dev) {
   return GI_OK;
 }
 
+int gi_create_devices(gi_ctx **out, const gi_device_set *set) {
+  if (!out || !set || set->count < 1 || set->count > GI_MAX_DEVICES) return GI_ERR_ARG;
+  *out = nullptr;
+  gi_ctx *c = nullptr;
+  int rc = gi_create(&c, set->devices[0]);
+  if (rc) return rc;
+  bool distinct = true;
+  for (int k = 1; k < set->count; k++) {
+    gi_ctx *d = nullptr;
+    rc = gi_create(&d, set->devices[k]);
+    if (rc) {
+      gi_destroy(c);
+      return rc;
+    }
+    c->peers.push_back(d);
+    for (int j = 0; j < k; j++) distinct = distinct && set->devices[j] != set->devices[k];
+  }
+  const char *g = getenv("GI_GATHER");  // "peer": hipMemcpyPeer instead of RCCL (diagnostics)
+  if (set->count > 1 && distinct && !(g && !strcmp(g, "peer"))) {
+    if (!g_rccl.load()) {
+      gi_destroy(c);
+      return GI_ERR_UNSUPPORTED;
+    }
+    c->comms.assign(set->count, nullptr);
+    ncclResult_t r = g_rccl.commInitAll(c->comms.data(), set->count, set->devices);
+    if (r != ncclSuccess) {
+      c->comms.clear();
+      gi_destroy(c);
+      return GI_ERR_HIP;
+    }
+  }
+  hipSetDevice(c->device);
+  *out = c;
+  return GI_OK;
+}
+
 void gi_destroy(gi_ctx *c) {
   if (!c) return;
+  for (ncclComm_t m : c->comms)
+    if (m) g_rccl.commDestroy(m);
+  c->comms.clear();
+  for (gi_ctx *d : c->peers) gi_destroy(d);
+  c->peers.clear();
   hipSetDevice(c->device);
   DBuf *bufs[] = {&c->d_nodes, &c->d_elems, &c->d_shapes, &c->d_tris, &c->d_bvh, &c->d_mats, &c->d_lights,
                   &c->d_lut, &c->d_stats, &c->spawn, &c->npaths, &c->path_off, &c->base,
                   &c->pixels, &c->rgbf, &c->rgb8, &c->qcount,
                   &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont, &c->mc_cont, &c->mc_ncont, &c->prim_rgb, &c->ind_tab, &c->mc_tab};
   for (DBuf *b : bufs) b->release();
+  c->pack.release();
+  for (auto &b : c->recv) b.release();
+  for (auto &b : c->peer_pix) b.release();
   for (int m = 0; m < 2; m++) {
     MapExec &X = c->mx[m];
     DBuf *xb[] = {&X.list_idx, &X.list_d2, &X.list_n, &X.gheap_d2, &X.gheap_idx, &X.fb_list, &X.fb_count,
@@ -1179,31 +1368,25 @@ int gi_set_params(gi_ctx *c, const gi_params *p) {
   if (!c || !p) return GI_ERR_ARG;
   c->P = *p;
   c->have_params = true;
+  for (gi_ctx *d : c->peers) {
+    d->P = *p;
+    d->have_params = true;
+  }
   return GI_OK;
 }
 
 int gi_read_scene(gi_ctx *c, const char *path, int real) {
   if (!c || !path) return GI_ERR_ARG;
+  hipSetDevice(c->device);
   std::string err;
   HostScene S;
   if (!load_scene(path, real != 0, S, err)) return fail(c, GI_ERR_IO, err);
   c->scene = std::move(S);
-  HostScene &H = c->scene;
-  HIPCHK(c, upload(c->d_nodes, H.nodes.data(), H.nodes.size() * sizeof(DNode), c->stream));
-  HIPCHK(c, upload(c->d_elems, H.elems.data(), H.elems.size() * sizeof(DElement), c->stream));
-  HIPCHK(c, upload(c->d_shapes, H.shapes.data(), H.shapes.size() * sizeof(DShape), c->stream));
-  HIPCHK(c, upload(c->d_tris, H.tris.data(), H.tris.size() * sizeof(DTri), c->stream));
-  HIPCHK(c, upload(c->d_bvh, H.bvh.data(), H.bvh.size() * sizeof(DBvhNode), c->stream));
-  HIPCHK(c, upload(c->d_mats, H.mats.data(), H.mats.size() * sizeof(DMaterial), c->stream));
-  HIPCHK(c, upload(c->d_lights, H.lights.data(), H.lights.size() * sizeof(DLight), c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  c->have_scene = true;
-  c->map_valid[0] = c->map_valid[1] = false;
-  for (int i = 0; i < 3; i++) {
-    c->sbmin[i] = (float)H.bmin[i];
-    c->sbmax[i] = (float)H.bmax[i];
-  }
-  return GI_OK;
+  // the device set shares the host scene; every device gets its own copy of the arrays
+  return on_devices(c, [&](int k, gi_ctx *d) -> int {
+    if (k) d->scene = c->scene;
+    return upload_scene(d);
+  });
 }
 
 int gi_scene_info(gi_ctx *c, int *nnodes, int *nlights, int *nprims, double *radius) {
@@ -1218,6 +1401,7 @@ int gi_scene_info(gi_ctx *c, int *nnodes, int *nlights, int *nprims, double *rad
 // MapPhotons, photonmap.cpp:260-436
 int gi_map_photons(gi_ctx *c, gi_photon_stats *st) {
   if (!c) return GI_ERR_ARG;
+  hipSetDevice(c->device);
   int rc = check_ready(c);
   if (rc) return rc;
   auto t0 = std::chrono::steady_clock::now();
@@ -1309,6 +1493,8 @@ int gi_map_photons(gi_ctx *c, gi_photon_stats *st) {
     rc = set_map(c, GI_MAP_GLOBAL, cached.data(), n);
     if (rc) return rc;
   }
+  rc = replicate_maps(c);
+  if (rc) return rc;
   auto t3 = std::chrono::steady_clock::now();
   if (st) {
     st->global_stored = (int64_t)c->hmap[0].storage.size();
@@ -1325,7 +1511,10 @@ int gi_map_photons(gi_ctx *c, gi_photon_stats *st) {
 
 int gi_set_photon_map(gi_ctx *c, int map, const gi_photon *ph, int64_t n) {
   if (!c || map < 0 || map > 1 || (n > 0 && !ph)) return GI_ERR_ARG;
-  return set_map(c, map, ph, n);
+  hipSetDevice(c->device);
+  int rc = set_map(c, map, ph, n);
+  if (rc) return rc;
+  return replicate_maps(c);
 }
 
 int gi_get_photon_map(gi_ctx *c, int map, gi_photon *out, int64_t cap, int64_t *n) {
@@ -1397,10 +1586,120 @@ static int render_common(gi_ctx *c, int aa, int w, int h, const std::vector<int3
   return GI_OK;
 }
 
+// output pixels of tiles t (tile x tile, row-major tile id) with t % nshards == shard
+static std::vector<int32_t> shard_pixels(int w, int h, int tile, int shard, int nshards) {
+  int tx = (w + tile - 1) / tile, ty = (h + tile - 1) / tile;
+  std::vector<int32_t> pix;
+  for (int t = 0; t < tx * ty; t++) {
+    if (t % nshards != shard) continue;
+    int x0 = (t % tx) * tile, y0 = (t / tx) * tile;
+    for (int y = y0; y < std::min(h, y0 + tile); y++)
+      for (int x = x0; x < std::min(w, x0 + tile); x++) {
+        pix.push_back(x);
+        pix.push_back(y);
+      }
+  }
+  return pix;
+}
+
+// RenderImage on a device set: device k renders the 16x16 output tiles
+// t % ndev == k (the reference's column interleave, render.cpp:90, re-cut as tiles), packs its
+// pixels (16 B each) and sends them to the first device: ncclSend / ncclRecv in one group over
+// xGMI when the devices are distinct (each peer's stream feeds its own link into device 0), a
+// peer copy otherwise. Device 0 scatters them into the image; nothing else is exchanged.
+static int render_multi(gi_ctx *c, int aa, int w, int h, uint8_t *rgb8, float *rgbf,
+                        gi_render_stats *st) {
+  const int nd = 1 + (int)c->peers.size();
+  const int tile = 16;
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<std::vector<int32_t>> pix(nd);
+  std::vector<gi_render_stats> ls(nd);
+  for (int k = 0; k < nd; k++) {
+    pix[k] = shard_pixels(w, h, tile, k, nd);
+    memset(&ls[k], 0, sizeof ls[k]);
+  }
+  int rc = on_devices(c, [&](int k, gi_ctx *d) -> int {
+    int r = render_common(d, aa, w, h, pix[k], nullptr, nullptr, &ls[k], false);
+    if (r || k == 0) return r;
+    const int64_t n = (int64_t)pix[k].size() / 2;
+    HIPCHK(d, d->pack.ensure((size_t)n * 16));
+    launch_pack_pixels(d->pixels.as<int32_t>(), n, w, d->rgbf.as<float>(), d->rgb8.as<uint8_t>(),
+                       d->pack.p, d->stream);
+    HIPCHK(d, hipGetLastError());
+    HIPCHK(d, hipStreamSynchronize(d->stream));
+    return (int)GI_OK;
+  });
+  if (rc) return rc;
+  c->recv.resize(nd);
+  c->peer_pix.resize(nd);
+  for (int k = 1; k < nd; k++) {
+    const int64_t n = (int64_t)pix[k].size() / 2;
+    HIPCHK(c, c->recv[k].ensure((size_t)n * 16));
+    HIPCHK(c, upload(c->peer_pix[k], pix[k].data(), pix[k].size() * 4, c->stream));
+  }
+  if (!c->comms.empty()) {
+    ncclResult_t r = g_rccl.groupStart();
+    for (int k = 1; k < nd && r == ncclSuccess; k++) {
+      const size_t bytes = pix[k].size() / 2 * 16;
+      gi_ctx *d = c->peers[k - 1];
+      r = g_rccl.send(d->pack.p, bytes, ncclUint8, 0, c->comms[k], d->stream);
+      if (r == ncclSuccess) r = g_rccl.recv(c->recv[k].p, bytes, ncclUint8, k, c->comms[0], c->stream);
+    }
+    ncclResult_t r2 = g_rccl.groupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+      return fail(c, GI_ERR_HIP, std::string("RCCL tile gather: ") +
+                                     g_rccl.errString(r != ncclSuccess ? r : r2));
+  } else {
+    for (int k = 1; k < nd; k++) {
+      gi_ctx *d = c->peers[k - 1];
+      HIPCHK(c, hipMemcpyPeerAsync(c->recv[k].p, c->device, d->pack.p, d->device,
+                                   pix[k].size() / 2 * 16, c->stream));
+    }
+  }
+  for (int k = 1; k < nd; k++)
+    launch_unpack_pixels(c->peer_pix[k].as<int32_t>(), (int64_t)pix[k].size() / 2, w,
+                         c->recv[k].p, c->rgbf.as<float>(), c->rgb8.as<uint8_t>(), c->stream);
+  HIPCHK(c, hipGetLastError());
+  const size_t npx = (size_t)w * h * 3;
+  if (rgbf) HIPCHK(c, hipMemcpyAsync(rgbf, c->rgbf.p, npx * 4, hipMemcpyDeviceToHost, c->stream));
+  if (rgb8) HIPCHK(c, hipMemcpyAsync(rgb8, c->rgb8.p, npx, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (st) {
+    memset(st, 0, sizeof *st);
+    for (int k = 0; k < nd; k++) {
+      const gi_render_stats &a = ls[k];
+      st->screen_rays += a.screen_rays; st->shadow_rays += a.shadow_rays;
+      st->monte_carlo_rays += a.monte_carlo_rays; st->transmissive_samples += a.transmissive_samples;
+      st->specular_samples += a.specular_samples; st->indirect_samples += a.indirect_samples;
+      st->caustic_samples += a.caustic_samples; st->knn_queries += a.knn_queries;
+      st->knn_photons += a.knn_photons; st->knn_visited += a.knn_visited;
+      st->knn_kernel_ms += a.knn_kernel_ms; st->knn_kernel_launches += a.knn_kernel_launches;
+      for (int m = 0; m < 2; m++) {
+        st->knn_map_queries[m] += a.knn_map_queries[m];
+        st->knn_map_photons[m] += a.knn_map_photons[m];
+        st->knn_map_visited[m] += a.knn_map_visited[m];
+        st->knn_map_kernel_ms[m] += a.knn_map_kernel_ms[m];
+        st->knn_map_launches[m] += a.knn_map_launches[m];
+        st->knn_map_fallback_ms[m] += a.knn_map_fallback_ms[m];
+        st->knn_map_fallback_queries[m] += a.knn_map_fallback_queries[m];
+      }
+    }
+    st->render_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return GI_OK;
+}
+
 // RenderImage, render.cpp:155-259
 int gi_render_image(gi_ctx *c, int aa, int w, int h, uint8_t *rgb8, float *rgbf,
                     gi_render_stats *st) {
   if (!c) return GI_ERR_ARG;
+  hipSetDevice(c->device);
+  if (!c->peers.empty()) {
+    int rc = check_ready(c);
+    if (rc) return rc;
+    if (aa < 0 || w <= 0 || h <= 0) return fail(c, GI_ERR_ARG, "bad image size");
+    return render_multi(c, aa, w, h, rgb8, rgbf, st);
+  }
   std::vector<int32_t> pix((size_t)w * h * 2);
   for (int y = 0; y < h; y++)
     for (int x = 0; x < w; x++) {
@@ -1413,17 +1712,8 @@ int gi_render_image(gi_ctx *c, int aa, int w, int h, uint8_t *rgb8, float *rgbf,
 int gi_render_tiles(gi_ctx *c, int aa, int w, int h, int tile, int shard, int nshards,
                     float *rgbf, gi_render_stats *st) {
   if (!c || tile <= 0 || nshards <= 0 || shard < 0 || shard >= nshards || !rgbf) return GI_ERR_ARG;
-  int tx = (w + tile - 1) / tile, ty = (h + tile - 1) / tile;
-  std::vector<int32_t> pix;
-  for (int t = 0; t < tx * ty; t++) {
-    if (t % nshards != shard) continue;
-    int x0 = (t % tx) * tile, y0 = (t / tx) * tile;
-    for (int y = y0; y < std::min(h, y0 + tile); y++)
-      for (int x = x0; x < std::min(w, x0 + tile); x++) {
-        pix.push_back(x);
-        pix.push_back(y);
-      }
-  }
+  hipSetDevice(c->device);
+  std::vector<int32_t> pix = shard_pixels(w, h, tile, shard, nshards);
   return render_common(c, aa, w, h, pix, nullptr, rgbf, st, true);
 }
 

@@ -318,6 +318,11 @@ void launch_fb_compact(const uint32_t *list, const uint32_t *count, uint32_t cap
                        uint32_t *total, hipStream_t st);  // slot0 + indirect + Monte Carlo
 void launch_reduce(const RenderArgs &a, hipStream_t st);
 void launch_owner_table(const uint32_t *off, int64_t n, uint32_t *tab, hipStream_t st);
+// device-set gather: pixels (x, y int32 pairs) packed 16 B each / scattered back
+void launch_pack_pixels(const int32_t *pix_xy, int64_t n, int w, const float *rgbf,
+                        const uint8_t *rgb8, void *out, hipStream_t st);
+void launch_unpack_pixels(const int32_t *pix_xy, int64_t n, int w, const void *in, float *rgbf,
+                          uint8_t *rgb8, hipStream_t st);
 void launch_segments(const uint64_t *skeys, uint32_t n, uint32_t nprim, uint32_t *seg,
                      hipStream_t st);
 // generic per-lane kernel with its heaps in global scratch (any K; used beyond the LDS kernels)

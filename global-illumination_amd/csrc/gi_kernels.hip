@@ -1476,6 +1476,45 @@ void launch_path(const RenderArgs &a, hipStream_t st, hipStream_t st2, hipEvent_
     (void)hipStreamWaitEvent(st, join, 0);
   }
 }
+// Shard gather of a device set (gi_host.cpp render_multi): a device's output pixels packed in
+// its pixel-list order as {r, g, b, rgb8 bytes} (16 B), and their scatter on the first device.
+__global__ void pack_pixels_kernel(const int2 *pix, int64_t n, int w, const float *rgbf,
+                                   const uint8_t *rgb8, uint4 *out) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int2 p = pix[i];
+  size_t o = 3 * ((size_t)p.y * w + p.x);
+  uint32_t b = (uint32_t)rgb8[o] | ((uint32_t)rgb8[o + 1] << 8) | ((uint32_t)rgb8[o + 2] << 16);
+  out[i] = make_uint4(__float_as_uint(rgbf[o]), __float_as_uint(rgbf[o + 1]),
+                      __float_as_uint(rgbf[o + 2]), b);
+}
+__global__ void unpack_pixels_kernel(const int2 *pix, int64_t n, int w, const uint4 *in,
+                                     float *rgbf, uint8_t *rgb8) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int2 p = pix[i];
+  size_t o = 3 * ((size_t)p.y * w + p.x);
+  uint4 v = in[i];
+  rgbf[o] = __uint_as_float(v.x);
+  rgbf[o + 1] = __uint_as_float(v.y);
+  rgbf[o + 2] = __uint_as_float(v.z);
+  rgb8[o] = (uint8_t)(v.w & 255u);
+  rgb8[o + 1] = (uint8_t)((v.w >> 8) & 255u);
+  rgb8[o + 2] = (uint8_t)((v.w >> 16) & 255u);
+}
+void launch_pack_pixels(const int32_t *pix_xy, int64_t n, int w, const float *rgbf,
+                        const uint8_t *rgb8, void *out, hipStream_t st) {
+  if (n == 0) return;
+  pack_pixels_kernel<<<nblk(n, 256), 256, 0, st>>>(reinterpret_cast<const int2 *>(pix_xy), n, w,
+                                                   rgbf, rgb8, reinterpret_cast<uint4 *>(out));
+}
+void launch_unpack_pixels(const int32_t *pix_xy, int64_t n, int w, const void *in, float *rgbf,
+                          uint8_t *rgb8, hipStream_t st) {
+  if (n == 0) return;
+  unpack_pixels_kernel<<<nblk(n, 256), 256, 0, st>>>(reinterpret_cast<const int2 *>(pix_xy), n, w,
+                                                     reinterpret_cast<const uint4 *>(in), rgbf,
+                                                     rgb8);
+}
 void launch_owner_table(const uint32_t *off, int64_t n, uint32_t *tab, hipStream_t st) {
   if (n > 0) owner_table_kernel<<<nblk(n, 256), 256, 0, st>>>(off, n, tab);
 }

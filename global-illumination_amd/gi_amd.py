@@ -25,7 +25,8 @@ DISK, CONE, GAUSS = 0, 1, 2
 GLOBAL, CAUSTIC = 0, 1
 
 EXPORTED = [
-    "gi_params_default", "gi_parse_args", "gi_create", "gi_destroy", "gi_last_error",
+    "gi_params_default", "gi_parse_args", "gi_create", "gi_create_devices", "gi_destroy",
+    "gi_last_error",
     "gi_set_params", "gi_read_scene", "gi_scene_info", "gi_map_photons", "gi_set_photon_map",
     "gi_get_photon_map", "gi_render_image", "gi_render_tiles", "gi_quantize",
     "gi_estimate_radiance_batch", "gi_knn_batch", "gi_knn_bench", "gi_intersect_batch",
@@ -41,7 +42,7 @@ class GiParams(C.Structure):
         "max_monte_depth", "recursive_shadows", "distrib_transmissive", "transmissive_test",
         "distrib_specular", "specular_test", "depth_of_field", "dof_test", "global_photon_count",
         "caustic_photon_count", "max_photon_depth", "indirect_test", "global_estimate_size",
-        "global_filter", "caustic_estimate_size", "caustic_filter", "pad0")] + [
+        "global_filter", "caustic_estimate_size", "caustic_filter", "gpus")] + [
         (n, C.c_double) for n in (
             "ir_air", "prob_absorb", "focus_depth", "aperture_radius", "global_estimate_dist",
             "caustic_estimate_dist", "filter_const_a", "filter_const_b", "filter_const_k")] + [
@@ -55,6 +56,13 @@ QUERY_DTYPE = np.dtype([
     ("point", "<f8", 3), ("normal", "<f8", 3), ("exact_bounce", "<f8", 3), ("cos_theta", "<f8"),
     ("kd", "<f8", 3), ("ks", "<f8", 3), ("shininess", "<f8"), ("max_dist", "<f8"),
     ("k", "<i4"), ("filter", "<i4")])
+
+
+GI_MAX_DEVICES = 64
+
+
+class DeviceSet(C.Structure):
+    _fields_ = [("count", C.c_int32), ("devices", C.c_int32 * GI_MAX_DEVICES)]
 
 
 class PhotonStats(C.Structure):
@@ -100,6 +108,7 @@ def lib():
                                     P(C.c_char_p), P(C.c_int), P(C.c_int), P(C.c_int),
                                     P(C.c_int), P(C.c_char_p)]
         L.gi_create.argtypes = [P(C.c_void_p), C.c_int]
+        L.gi_create_devices.argtypes = [P(C.c_void_p), P(DeviceSet)]
         L.gi_destroy.argtypes = [C.c_void_p]
         L.gi_destroy.restype = None
         L.gi_last_error.argtypes = [C.c_void_p]
@@ -158,13 +167,24 @@ class GiError(RuntimeError):
 
 
 class Renderer:
-    """One device context (one HIP device): scene, photon maps and render scratch."""
+    """One context: scene, photon maps and render scratch on one HIP device, or on a device
+    set (`devices=[...]`, gi_create_devices: tiles dealt across the devices, gathered onto the
+    first)."""
 
-    def __init__(self, device=0, params=None):
+    def __init__(self, device=0, params=None, devices=None):
         self._ctx = C.c_void_p()
-        rc = lib().gi_create(C.byref(self._ctx), device)
-        if rc != GI_OK:
-            raise GiError(f"gi_create failed (rc={rc}): no usable HIP device {device}")
+        if devices is not None:
+            ds = DeviceSet()
+            ds.count = len(devices)
+            for i, d in enumerate(devices):
+                ds.devices[i] = d
+            rc = lib().gi_create_devices(C.byref(self._ctx), C.byref(ds))
+            if rc != GI_OK:
+                raise GiError(f"gi_create_devices failed (rc={rc}) for devices {list(devices)}")
+        else:
+            rc = lib().gi_create(C.byref(self._ctx), device)
+            if rc != GI_OK:
+                raise GiError(f"gi_create failed (rc={rc}): no usable HIP device {device}")
         self.params = params if params is not None else default_params()
         self._check(lib().gi_set_params(self._ctx, C.byref(self.params)))
 

@@ -7,6 +7,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 #include "../../include/gi.h"
 
@@ -24,11 +25,28 @@ int main(int argc, char **argv) {
     fprintf(stderr, "%s\n", err);
     return -1;
   }
-  int dev = 0;
-  if (const char *d = getenv("GI_DEVICE")) dev = atoi(d);
+  // devices: -gpus N takes devices 0..N-1 (the reference's -threads N re-cut as a device
+  // shard); GI_DEVICES="a,b,..." names them explicitly, GI_DEVICE the single device
+  gi_device_set ds;
+  memset(&ds, 0, sizeof ds);
+  ds.count = 1;
+  if (const char *d = getenv("GI_DEVICE")) ds.devices[0] = atoi(d);
+  if (P.gpus > 1) {
+    ds.count = P.gpus < GI_MAX_DEVICES ? P.gpus : GI_MAX_DEVICES;
+    for (int k = 0; k < ds.count; k++) ds.devices[k] = k;
+  }
+  if (const char *l = getenv("GI_DEVICES")) {
+    ds.count = 0;
+    for (const char *q = l; *q && ds.count < GI_MAX_DEVICES;) {
+      ds.devices[ds.count++] = atoi(q);
+      while (*q && *q != ',') q++;
+      if (*q == ',') q++;
+    }
+    if (ds.count == 0) ds.count = 1;
+  }
   gi_ctx *ctx = nullptr;
-  if (gi_create(&ctx, dev) != GI_OK) {
-    fprintf(stderr, "Unable to initialise HIP device %d\n", dev);
+  if (gi_create_devices(&ctx, &ds) != GI_OK) {
+    fprintf(stderr, "Unable to initialise %d HIP device(s) starting at %d\n", ds.count, ds.devices[0]);
     return -1;
   }
   gi_set_params(ctx, &P);

@@ -86,7 +86,7 @@ typedef struct gi_params {
   int32_t global_filter;        /* GLOBAL_FILTER                  -gf cone K | gauss */
   int32_t caustic_estimate_size;/* CAUSTIC_ESTIMATE_SIZE          -cs N         */
   int32_t caustic_filter;       /* CAUSTIC_FILTER                 -cf cone K | gauss */
-  int32_t pad0;
+  int32_t gpus;                 /* extension: devices of the drop-in CLI (-gpus N); 0/1 = one */
   double ir_air;                /* IR_AIR                         -ir F         */
   double prob_absorb;           /* PROB_ABSORB                    -absorb F     */
   double focus_depth;           /* FOCUS_DEPTH                                  */
@@ -155,6 +155,18 @@ int gi_parse_args(int argc, char **argv, gi_params *p, const char **scene_path,
 
 /* ---- context ----------------------------------------------------------------------- */
 int gi_create(gi_ctx **out, int hip_device);
+/* One context over several HIP devices (SURVEY.md 8(b) gi_create(gi_ctx**, const
+ * gi_device_set*); render.cpp:90's thread interleave re-cut as a device shard). Every call on
+ * it drives all of them: the scene and photon maps are replicated (photon emission ranges are
+ * split across the devices, the maps built once), gi_render_image deals 16x16 output tiles
+ * t % count to device t and gathers the tiles onto devices[0] (RCCL send/recv over xGMI when the
+ * devices are distinct, else a peer copy). Test seams (gi_*_batch) run on devices[0]. */
+#define GI_MAX_DEVICES 64
+typedef struct gi_device_set {
+  int32_t count;
+  int32_t devices[GI_MAX_DEVICES];
+} gi_device_set;
+int gi_create_devices(gi_ctx **out, const gi_device_set *set);
 void gi_destroy(gi_ctx *ctx);
 const char *gi_last_error(const gi_ctx *ctx);
 int gi_set_params(gi_ctx *ctx, const gi_params *p);

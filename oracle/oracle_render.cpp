@@ -1346,7 +1346,7 @@ static void render_image(const Ctx &c, int aa, int width, int height, Image &img
 }
 
 // ---------------------------------------------------------------------------------------
-// ParseArgs, io_utils.cpp:16-212 (+ extension: -seed S)
+// ParseArgs, io_utils.cpp:16-212 (+ extensions: -seed S, -gpus N)
 // ---------------------------------------------------------------------------------------
 static void params_default(gi_params &P) {
   memset(&P, 0, sizeof P);
@@ -1436,6 +1436,7 @@ static int parse_args(int argc, char **argv, gi_params &P, std::string &scene, s
         if (h < 0) h *= -1;
       }
       else if (!strcmp(a, "-seed") && need(1)) { argc--; argv++; P.seed = strtoull(*argv, nullptr, 10); }
+      else if (!strcmp(a, "-gpus") && need(1)) { argc--; argv++; P.gpus = atoi(*argv); }
       else { err = std::string("Invalid program argument: ") + a; return 1; }
       argv++; argc--;
     } else {

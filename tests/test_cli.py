@@ -103,3 +103,20 @@ def test_cli_render_matches_oracle_cli(tmp_path):
     assert got["# Indirect Samples"] == st["indirect_samples"]
     assert got["# Caustic Samples"] == st["caustic_samples"]
     assert "Width = 32" in r.stdout and "Height = 24" in r.stdout
+
+
+@pytest.mark.gpu
+def test_cli_device_set_matches_one_device(tmp_path):
+    """`-gpus N` (extension flag) runs the drop-in over a device set; GI_DEVICES=0,0 lets one GPU
+    stand in for two (tiles t % 2, gathered by peer copy). The PNG equals the one-device PNG."""
+    flags = ["-resolution", "40", "24", "-aa", "1", "-global", "20000", "-caustic", "20000",
+             "-it", "8", "-tt", "8", "-st", "8"]
+    scn = os.path.join(SCENES, "cornell.scn")
+    one, two = str(tmp_path / "one.png"), str(tmp_path / "two.png")
+    r1 = run(CLI, [scn, one] + flags, timeout=300)
+    assert r1.returncode == 0, r1.stderr
+    env = dict(os.environ, GI_DEVICES="0,0")
+    r2 = subprocess.run([CLI, scn, two] + flags + ["-gpus", "2"], capture_output=True, text=True,
+                        timeout=300, env=env)
+    assert r2.returncode == 0, r2.stderr
+    np.testing.assert_array_equal(pngio.read_png(one), pngio.read_png(two))

@@ -1,7 +1,9 @@
 """Multi-rank tile sharding and gather (gi_dist.py) on CPU with the gloo backend, world size
 2 and 3. The renderer is replaced by a stand-in with gi_render_tiles' contract: a full-size f32
-image that holds this rank's tiles and zeros elsewhere (gi_host.cpp gi_render_tiles). The
-device-side composition of real tiles is covered by test_gpu_render.py."""
+image that holds this rank's tiles and zeros elsewhere (gi_host.cpp gi_render_tiles). Each rank
+sends only its own pixels (checked: the gathered buffers hold 1/world of the frame). The
+device-side composition of real tiles is covered by test_gpu_render.py, and the single-process
+device-set gather by test_gpu_features.py."""
 import os
 import socket
 
@@ -36,8 +38,15 @@ def _worker(rank, world, port, w, h, tile, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        sent = []
+        real_gather = dist.gather
+
+        def spy(t, parts=None, dst=0):
+            sent.append(t.numel())
+            return real_gather(t, parts, dst=dst)
+        dist.gather = spy
         img, st = gi_dist.render_sharded(FakeTiles(), 0, w, h, tile, rank, world, dist)
-        q.put((rank, st["pixels"], None if img is None else img))
+        q.put((rank, st["pixels"], None if img is None else img, sent))
     finally:
         dist.destroy_process_group()
 
@@ -58,6 +67,11 @@ def test_sharded_gather_equals_full_frame(world, w, h, tile):
     assert sum(o[1] for o in out) == w * h             # every pixel rendered exactly once
     np.testing.assert_array_equal(out[0][2], reference_image(w, h))
     assert all(o[2] is None for o in out[1:])
+    # one gather per rank of at most the largest shard (not the whole frame)
+    biggest = int(np.bincount(gi_dist.tile_owner_map(w, h, tile, world).ravel()).max())
+    for o in out:
+        assert o[3] == [biggest * 3]
+        assert biggest * world < w * h + tile * tile * world
 
 
 def test_tile_owner_map_round_robin():

@@ -274,3 +274,40 @@ def test_mesh_bvh_matches_linear_loop(renderer, kind):
     np.testing.assert_array_equal(gt[both], ot[both])
     np.testing.assert_array_equal(gn[both], on[both])
     np.testing.assert_array_equal(gp[both], op[both])
+
+
+@pytest.mark.parametrize("devices,name,extra", [
+    ([0, 0], "cornell.scn", ["-global", "40000", "-caustic", "40000", "-it", "16"]),
+    ([0, 0, 0], "jensen.scn", ["-global", "4000", "-caustic", "40000", "-lt", "4", "-ss", "4",
+                               "-it", "8"]),
+])
+def test_device_set_matches_one_device(devices, name, extra):
+    """gi_create_devices: photon emission split across the set, maps replicated, 16x16 tiles
+    dealt t % ndev and gathered onto the first device. On one GPU the set repeats device 0 (the
+    gather is then a peer copy; distinct devices use RCCL send/recv): the image, the f32 frame,
+    the photon maps and every -v counter equal the single-device render's."""
+    args = [scene(name), "/tmp/x.png", "-resolution", "40", "24", "-aa", "1", "-tt", "8",
+            "-st", "8", "-seed", "8"] + extra
+    p, sc, _o, w, h, aa, real = gi_amd.ParseArgs(args)
+    out = []
+    for devs in (None, devices):
+        r = gi_amd.Renderer(0, p, devices=devs)
+        try:
+            r.ReadScene(sc, real)
+            ps = r.MapPhotons()
+            rgb, f, st = r.RenderImage(aa, w, h, want_float=True)
+            maps = [r.photon_map(m) for m in (gi_amd.GLOBAL, gi_amd.CAUSTIC)]
+            out.append((rgb, f, st, ps, maps))
+        finally:
+            r.close()
+    (r1, f1, s1, p1, m1), (r2, f2, s2, p2, m2) = out
+    for m in (0, 1):
+        assert len(m1[m]) == len(m2[m])
+        assert (m1[m].tobytes() == m2[m].tobytes())
+    assert p1["global_stored"] == p2["global_stored"]
+    np.testing.assert_array_equal(f1, f2)
+    np.testing.assert_array_equal(r1, r2)
+    for k in ("screen_rays", "shadow_rays", "monte_carlo_rays", "transmissive_samples",
+              "specular_samples", "indirect_samples", "caustic_samples", "knn_queries",
+              "knn_photons"):
+        assert s1[k] == s2[k], k

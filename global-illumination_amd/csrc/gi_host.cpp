@@ -305,7 +305,13 @@ struct gi_ctx {
   DBuf scan_lvl[8], scan_out[8];
   // photon tracing scratch
   DBuf pcounts, poffs, pbuf;
-  int64_t prim_per_batch = 1 << 19;  // denser query batches: fewer chunk k-NN overflows (measured best)
+  // Primary samples per batch. Denser query batches make the chunk k-NN's 64 Morton-adjacent
+  // queries span less of a K-neighbourhood (fewer LDS candidates per query): C2 at 2^19 / 2^20 /
+  // 2^21 / 2^22 ran 6.85 / 7.44 / 7.89 / 7.69 Mpixel-samples/s. A batch is also capped by the
+  // query budget below (queries per primary sample vary ~10x between scenes).
+  int64_t prim_per_batch = 1 << 21;
+  int64_t query_budget = 400000000;  // photon-map queries per batch (~120 B each: ~48 GB)
+  double q_per_prim = 0.0;           // largest queries per primary sample seen so far
   bool sort_queries = true;
   float sbmin[3] = {0, 0, 0}, sbmax[3] = {1, 1, 1};
 };
@@ -943,13 +949,20 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
   int dof = std::max(1, P.dof_test);
   int64_t per_pix = (int64_t)af * af * dof;
   int64_t npix_total = (int64_t)pix_xy.size() / 2;
-  int64_t pix_batch = std::max<int64_t>(1, c->prim_per_batch / per_pix);
   double knn_ms[2] = {0, 0}, launches[2] = {0, 0};
   HIPCHK(c, upload(c->pixels, pix_xy.data(), pix_xy.size() * 4, c->stream));
   HIPCHK(c, c->qcount.ensure(16));
   HIPCHK(c, c->stats_bak.ensure(ST_BYTES));
-  for (int64_t p0 = 0; p0 < npix_total; p0 += pix_batch) {
-    int64_t npix = std::min(pix_batch, npix_total - p0);
+  for (int64_t p0 = 0, npix = 0; p0 < npix_total; p0 += npix) {
+    // batch size: prim_per_batch primary samples, fewer when the query rate seen so far would
+    // exceed the query budget (the first batch of a scene starts at 1/8 to measure that rate)
+    int64_t prim_cap = c->prim_per_batch;
+    if (c->q_per_prim > 0.0)
+      prim_cap = std::min<int64_t>(prim_cap, (int64_t)(c->query_budget / c->q_per_prim));
+    else
+      prim_cap = std::max<int64_t>(1, prim_cap / 8);
+    const int64_t pix_batch = std::max<int64_t>(1, prim_cap / per_pix);
+    npix = std::min(pix_batch, npix_total - p0);
     int64_t nprim = npix * per_pix;
     RenderArgs a;
     memset(&a, 0, sizeof a);
@@ -1070,6 +1083,7 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
       }
       for (int l = 0; l < 2; l++)
         c->qcap_hint[l] = std::max<size_t>(c->qcap_hint[l], (size_t)(nq[l] * 1.25) + 1024);
+      c->q_per_prim = std::max(c->q_per_prim, (double)((uint64_t)nq[0] + nq[1]) / (double)nprim);
       if (ok) break;
       if (attempt == 2) return fail(c, GI_ERR_ALLOC, "query list overflow");
       HIPCHK(c, hipMemcpyAsync(c->d_stats.p, c->stats_bak.p, ST_BYTES,
@@ -1190,6 +1204,7 @@ int upload_scene(gi_ctx *c) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->have_scene = true;
   c->map_valid[0] = c->map_valid[1] = false;
+  c->q_per_prim = 0.0;  // the batch size is re-measured on the new scene
   for (int i = 0; i < 3; i++) {
     c->sbmin[i] = (float)H.bmin[i];
     c->sbmax[i] = (float)H.bmax[i];
@@ -1256,6 +1271,7 @@ int gi_create(gi_ctx **out, int dev) {
   }
   hipStreamSynchronize(c->stream);
   if (const char *s = getenv("GI_PRIM_PER_BATCH")) c->prim_per_batch = std::max(1LL, atoll(s));
+  if (const char *s = getenv("GI_QUERY_BUDGET")) c->query_budget = std::max(1LL, atoll(s));
   // tuning knobs (measurement only; defaults are the measured best)
   if (const char *s = getenv("GI_LEAF_SIZE")) c->leaf_size[0] = c->leaf_size[1] = std::max(1, atoi(s));
   if (const char *s = getenv("GI_LEAF_SIZE_C")) c->leaf_size[1] = std::max(1, atoi(s));

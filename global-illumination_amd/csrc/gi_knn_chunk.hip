@@ -69,6 +69,46 @@ __device__ __forceinline__ float metric(float qx, float qy, float qz, const floa
   return __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
 }
 
+// The chunk's LDS candidates, structure of arrays: x[CAPC], y[CAPC], z[CAPC], w[CAPC] (w = the
+// photon's dir | flags bits). The select loops read four consecutive candidates' x (y, z) with
+// one broadcast ds_read_b128 (4 LDS cycles; a float4 per candidate would be a ds_read_b96 at 8
+// cycles each, MI355X_MICROARCH.md LDS table).
+template <int CAPC>
+struct Cands {
+  float *b;
+  __device__ __forceinline__ float4 get(uint32_t s) const {
+    return make_float4(b[s], b[CAPC + s], b[2 * CAPC + s], b[3 * CAPC + s]);
+  }
+  __device__ __forceinline__ void put(uint32_t s, const float4 &p) const {
+    b[s] = p.x; b[CAPC + s] = p.y; b[2 * CAPC + s] = p.z; b[3 * CAPC + s] = p.w;
+  }
+  __device__ __forceinline__ float wbits(uint32_t s) const { return b[3 * CAPC + s]; }
+  // candidates s0 .. s0 + 3 (s0 % 4 == 0) of coordinate c
+  __device__ __forceinline__ float4 quad(int c, uint32_t s0) const {
+    return *reinterpret_cast<const float4 *>(b + c * CAPC + s0);
+  }
+  __device__ __forceinline__ float d2(float qx, float qy, float qz, uint32_t s) const {
+    return metric(qx, qy, qz, make_float4(b[s], b[CAPC + s], b[2 * CAPC + s], 0.0f));
+  }
+};
+
+// d2 of the 8 candidates s0 .. s0 + 7 (s0 % 8 == 0, s0 + 8 <= CAPC): six broadcast reads
+template <int CAPC>
+__device__ __forceinline__ void cand_d2x8(const Cands<CAPC> &C, uint32_t s0, float qx, float qy,
+                                          float qz, float (&d)[8]) {
+  const float4 x0 = C.quad(0, s0), x1 = C.quad(0, s0 + 4);
+  const float4 y0 = C.quad(1, s0), y1 = C.quad(1, s0 + 4);
+  const float4 z0 = C.quad(2, s0), z1 = C.quad(2, s0 + 4);
+  d[0] = metric(qx, qy, qz, make_float4(x0.x, y0.x, z0.x, 0.f));
+  d[1] = metric(qx, qy, qz, make_float4(x0.y, y0.y, z0.y, 0.f));
+  d[2] = metric(qx, qy, qz, make_float4(x0.z, y0.z, z0.z, 0.f));
+  d[3] = metric(qx, qy, qz, make_float4(x0.w, y0.w, z0.w, 0.f));
+  d[4] = metric(qx, qy, qz, make_float4(x1.x, y1.x, z1.x, 0.f));
+  d[5] = metric(qx, qy, qz, make_float4(x1.y, y1.y, z1.y, 0.f));
+  d[6] = metric(qx, qy, qz, make_float4(x1.z, y1.z, z1.z, 0.f));
+  d[7] = metric(qx, qy, qz, make_float4(x1.w, y1.w, z1.w, 0.f));
+}
+
 // squared gap between a point/box and box B, same fp32 operation order as the photon metric
 __device__ __forceinline__ float gap2(float lx, float ly, float lz, float hx, float hy, float hz,
                                       const float *bl, const float *bh) {
@@ -226,7 +266,7 @@ __device__ __forceinline__ uint32_t walk_within(const float *nodes, int L, float
 
 template <int CAPC>
 __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, bool valid, float4 qp,
-                                                   uint32_t cap, float4 *cpos, uint32_t *cidx,
+                                                   uint32_t cap, const Cands<CAPC> &cpos, uint32_t *cidx,
                                                    uint32_t *crgbe, uint32_t *hist, uint32_t *stk,
                                                    ChunkGeom &G, ChunkProf &P) {
   constexpr int PER = CAPC / 64;
@@ -302,7 +342,7 @@ __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, b
               if (na + nn > (uint32_t)CAPC) { ovf = true; return true; }
               if (take) {
                 uint32_t off = na + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                cpos[off] = p;
+                cpos.put(off, p);
                 cidx[off] = (uint32_t)ii;
               }
               na += nn;
@@ -319,7 +359,7 @@ __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, b
           uint32_t s = (uint32_t)(u * 64 + lane);
           kc[u] = ~0ull;
           if (s < na) {
-            float dd = metric(cx, cy, cz, cpos[s]);
+            float dd = cpos.d2(cx, cy, cz, s);
             kc[u] = ((uint64_t)__float_as_uint(dd) << 32) | (uint64_t)s;
             mn = fminf(mn, dd);
             mx = fmaxf(mx, dd);
@@ -369,7 +409,7 @@ __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, b
             }
             if (take) {
               uint32_t off = count + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-              cpos[off] = p;
+              cpos.put(off, p);
               cidx[off] = (uint32_t)ii;
               crgbe[off] = e;
             }
@@ -419,9 +459,9 @@ __device__ __forceinline__ void to_fallback(const KnnArgs &a, uint64_t vmask, bo
 
 // ---- 4. the estimate of one query from LDS-staged photons (slot_at(s) = s-th kept slot).
 //         EstimateRadiance photon_utils.cpp:72-162 / irradiance :209-246
-template <typename SlotAt>
+template <int CAPC, typename SlotAt>
 __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, float4 qp, int num,
-                                               float km, const float4 *cpos, const uint32_t *crgbe,
+                                               float km, const Cands<CAPC> &cpos, const uint32_t *crgbe,
                                                SlotAt slot_at) {
   const int K = a.K;
   double maxd2 = kEps;
@@ -464,8 +504,7 @@ __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, flo
       constexpr int EB = CHUNK_EST_EB;
       if (a.filter == 0 && diff_only) {
         // the common case (disk filter, no specular term): neither d2 nor the exact bounce is
-        // needed, so only the direction code (cpos[slot].w) and the rgbe word are read
-        const float *cw = reinterpret_cast<const float *>(cpos) + 3;
+        // needed, so only the direction code (w bits) and the rgbe word are read
         const double kd0 = mt.kd[0], kd1 = mt.kd[1], kd2 = mt.kd[2];
         for (int s0 = 0; s0 < num; s0 += EB) {
           uint32_t eg[EB];
@@ -474,7 +513,7 @@ __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, flo
           for (int u = 0; u < EB; u++) {
             uint32_t slot = slot_at(s0 + u < num ? s0 + u : s0);
             eg[u] = crgbe[slot];
-            uint32_t dc = __float_as_uint(cw[4 * slot]) & 0xffffu;
+            uint32_t dc = __float_as_uint(cpos.wbits(slot)) & 0xffffu;
             lg[u][0] = a.lut[3 * dc];
             lg[u][1] = a.lut[3 * dc + 1];
             lg[u][2] = a.lut[3 * dc + 2];
@@ -507,7 +546,7 @@ __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, flo
 #pragma unroll
       for (int u = 0; u < EB; u++) {
         uint32_t slot = slot_at(s0 + u < num ? s0 + u : s0);
-        pg[u] = cpos[slot];
+        pg[u] = cpos.get(slot);
         eg[u] = crgbe[slot];
         uint32_t dc = __float_as_uint(pg[u].w) & 0xffffu;
         lg[u][0] = a.lut[3 * dc];
@@ -613,7 +652,7 @@ constexpr int LS_BR = 4;       // bracket photons resolved by the collect pass (
 #endif
 constexpr int LS_PASSES = 10;  // counting passes before a query goes to the fallback
 #ifndef LS_UNROLL
-#define LS_UNROLL 8            // candidates per LDS round trip in the counting / collect loops (8: -1 % vs 4)
+#define LS_UNROLL 8            // candidates per loop trip in the counting / collect loops (fixed by cand_d2x8)
 #endif
 
 // value-range bin of d2 in the bracket binning (lo, sc): monotone non-decreasing in d2, 0 at lo
@@ -650,14 +689,16 @@ template <int WPE, bool PROF>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE)))
 void knn_chunk_lane_kernel(KnnArgs a) {
   constexpr int CAPC = 256;
-  __shared__ float4 cpos[CAPC];
+  __shared__ float4 cpos_lds[CAPC];
+  const Cands<CAPC> cpos{reinterpret_cast<float *>(cpos_lds)};
   __shared__ uint32_t cidx[CAPC];
   __shared__ uint32_t crgbe[CAPC];
   __shared__ uint32_t stk[64];  // kd walk stack (walk_within)
   // kept LDS slots [s][lane] (K <= 64, u8) during the collect and the estimate; during the
-  // counting passes the same 4 KiB hold the lanes' bin counters [bin][lane] (u32), and during
-  // the bound phase the centre select's 256-bin histogram
-  __shared__ uint32_t selh[16 * 64];
+  // counting passes the lanes' bin counters [bin][lane] (u32), and during the bound phase the
+  // centre select's 256-bin histogram. Row 16 (u32) / 64 (u8) takes the branch-free loops'
+  // writes of non-members.
+  __shared__ uint32_t selh[17 * 64];
   uint8_t *sel = reinterpret_cast<uint8_t *>(selh);
   uint32_t *hist = selh;
   const int lane = threadIdx.x;
@@ -718,12 +759,18 @@ void knn_chunk_lane_kernel(KnnArgs a) {
         // 16 bins per lane as LDS counters [bin][lane] (conflict-free, one ds_add per member)
 #pragma unroll
         for (int b = 0; b < 16; b++) selh[b * 64 + lane] = 0u;
-#pragma unroll LS_UNROLL
-        for (uint32_t s = 0; s < count; s++) {
-          float d2 = metric(qx, qy, qz, cpos[s]);
-          bool mem = on && d2 >= A && d2 <= B;
-          uint32_t b = bin16(d2, O, sc);
-          if (mem) atomicAdd(&selh[b * 64 + lane], 1u);
+        // groups of LS_UNROLL candidates: the group's (broadcast) LDS reads are issued together
+        // and the loop body has no branches (non-members count into the trash row 16)
+        for (uint32_t s0 = 0; s0 < count; s0 += 8) {
+          float dg[8];
+          cand_d2x8(cpos, s0, qx, qy, qz, dg);
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            float d2 = dg[u];
+            bool mem = on && (s0 + u < count) && d2 >= A && d2 <= B;
+            uint32_t b = mem ? bin16(d2, O, sc) : 16u;
+            atomicAdd(&selh[b * 64 + lane], 1u);
+          }
         }
         if (on) {
           uint32_t before = 0, bs = 16, cb = 0;
@@ -774,17 +821,22 @@ void knn_chunk_lane_kernel(KnnArgs a) {
     int n = 0, m = 0;
     float km = 0.0f;
     const bool inb_on = col && need > 0;
-#pragma unroll LS_UNROLL
-    for (uint32_t s = 0; s < count; s++) {
-      float d2 = metric(qx, qy, qz, cpos[s]);
-      if (col && d2 < A) {
-        sel[n * 64 + lane] = (uint8_t)s;
-        n++;
-        km = fmaxf(km, d2);
-      }
-      if (inb_on && d2 >= A && d2 <= B) {
-        sel[(63 - m) * 64 + lane] = (uint8_t)s;
-        m++;
+    // branch-free like the counting passes: a candidate that is not kept is written to row 64
+    for (uint32_t s0 = 0; s0 < count; s0 += 8) {
+      float dg[8];
+      cand_d2x8(cpos, s0, qx, qy, qz, dg);
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const uint32_t s = s0 + u;
+        float d2 = dg[u];
+        const bool ok = s < count;
+        const bool kf = col && ok && d2 < A;
+        const bool kb = inb_on && ok && d2 >= A && d2 <= B;
+        sel[(kf ? n : 64) * 64 + lane] = (uint8_t)s;
+        sel[(kb ? 63 - m : 64) * 64 + lane] = (uint8_t)s;
+        n += kf ? 1 : 0;
+        m += kb ? 1 : 0;
+        km = kf ? fmaxf(km, d2) : km;
       }
     }
     if (inb_on) {
@@ -797,7 +849,7 @@ void knn_chunk_lane_kernel(KnnArgs a) {
         fk[i] = ~0ull;
         if (i < m) {
           sl[i] = sel[(63 - i) * 64 + lane];
-          float d2 = metric(qx, qy, qz, cpos[sl[i]]);
+          float d2 = cpos.d2(qx, qy, qz, sl[i]);
           fk[i] = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)cidx[sl[i]];
         }
       }
@@ -849,14 +901,15 @@ template <int CAPC, bool PROF>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
 void knn_chunk_big_kernel(KnnArgs a) {
   constexpr int NW = CAPC / 32;
-  __shared__ float4 cpos[CAPC];
+  __shared__ float4 cpos_lds[CAPC];
+  const Cands<CAPC> cpos{reinterpret_cast<float *>(cpos_lds)};
   __shared__ uint32_t cidx[CAPC];
   __shared__ uint32_t crgbe[CAPC];
   __shared__ uint32_t hist[4];       // unused by the dk bound (chunk_bound_gather signature)
   __shared__ uint32_t stk[64];
   // kept-candidate bitmask [word][lane] during the collect and the estimate; during the counting
   // passes the lanes' 16 bin counters [bin][lane]
-  __shared__ uint32_t selw[(NW > 16 ? NW : 16) * 64];
+  __shared__ uint32_t selw[(NW > 17 ? NW : 17) * 64];  // row 16: trash counters
   const int lane = threadIdx.x;
   const int K = a.K;
   const int minsub = a.chunk_minsub > 0 ? a.chunk_minsub : 64;
@@ -907,12 +960,17 @@ void knn_chunk_big_kernel(KnnArgs a) {
       const float sc = 16.0f / (B - O);
 #pragma unroll
       for (int b = 0; b < 16; b++) selw[b * 64 + lane] = 0u;
-#pragma unroll 4
-      for (uint32_t s = 0; s < count; s++) {
-        float d2 = metric(qx, qy, qz, cpos[s]);
-        bool mem = on && d2 >= A && d2 <= B;
-        uint32_t b = bin16(d2, O, sc);
-        if (mem) atomicAdd(&selw[b * 64 + lane], 1u);
+      // branch-free groups, as in the lane kernel (non-members count into row 16)
+      for (uint32_t s0 = 0; s0 < count; s0 += 8) {
+        float dg[8];
+        cand_d2x8(cpos, s0, qx, qy, qz, dg);
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          float d2 = dg[u];
+          bool mem = on && (s0 + u < count) && d2 >= A && d2 <= B;
+          uint32_t b = mem ? bin16(d2, O, sc) : 16u;
+          atomicAdd(&selw[b * 64 + lane], 1u);
+        }
       }
       if (on) {
         uint32_t before = 0, bs = 16, cb = 0;
@@ -966,7 +1024,7 @@ void knn_chunk_big_kernel(KnnArgs a) {
       for (uint32_t j = 0; j < 32; j++) {
         uint32_t s = w0 * 32 + j;
         if (s >= count) break;
-        float d2 = metric(qx, qy, qz, cpos[s]);
+        float d2 = cpos.d2(qx, qy, qz, s);
         if (col && d2 < A) {
           bits |= 1u << j;
           km = fmaxf(km, d2);

@@ -207,7 +207,8 @@ __device__ __forceinline__ void wave_select_k(uint64_t (&key)[PER], int K, float
 struct ChunkGeom {
   float bl[3], bh[3];  // the chunk's query box B
   float cx, cy, cz;    // its centre c
-  double dkc;          // exact d_K(c) as a true-distance upper bound; -1 when not found
+  double dkc;          // d_K(c) as a true-distance upper bound; -1 when not found
+  bool dkc_exact;      // dkc is d_K(c) itself (within rounding), not a looser upper bound
   uint32_t count;      // candidates gathered into LDS
   bool overflow;       // more than `cap` candidates: the chunk goes to the fallback
 };
@@ -289,6 +290,7 @@ __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, b
   // ---- 1. U: r_max, tightened by the exact d_K(c)
   double U = a.rmax;
   G.dkc = -1.0;
+  G.dkc_exact = false;
   if (N > 0 && K > 0) {
     int node = 1;
     while (node < L) {
@@ -375,6 +377,7 @@ __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, b
       __syncthreads();
       // metric -> true distance: 1e-5 relative margin covers the fp32 rounding
       G.dkc = sqrt((double)dk2 * (1.0 + 1e-5));
+      G.dkc_exact = !ovf && na >= (uint32_t)K;
       double ub = G.dkc + rho * (1.0 + 1e-6) + 1e-12;
       if (ub < U) U = ub;
     }
@@ -419,6 +422,10 @@ __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, b
         });
     if (P.on) P.c[6] += rd;
   }
+  // +inf positions after the last candidate, up to the next multiple of 8: the select loops
+  // read whole groups of 8, and d2 = +inf is never below a bound or inside a bracket
+  if (!overflow && lane < 8 && (count & 7u) != 0u && count + lane < ((count + 7u) & ~7u))
+    cpos.put(count + lane, make_float4(INFINITY, INFINITY, INFINITY, 0.0f));
   G.count = count;
   G.overflow = overflow;
   if (P.on) {
@@ -651,35 +658,52 @@ constexpr int LS_BR = 4;       // bracket photons resolved by the collect pass (
 #define LS_BR_L 12             // the same for the lane-select kernel (bracket kept in its LDS slot list; measured best)
 #endif
 constexpr int LS_PASSES = 10;  // counting passes before a query goes to the fallback
+#ifndef LS_NB
+#define LS_NB 64               // value-range bins per counting pass of the lane-select kernel
+#endif
 #ifndef LS_UNROLL
 #define LS_UNROLL 8            // candidates per loop trip in the counting / collect loops (fixed by cand_d2x8)
 #endif
 
-// value-range bin of d2 in the bracket binning (lo, sc): monotone non-decreasing in d2, 0 at lo
-// (also for sc = inf), 15 at the bracket's top
-__device__ __forceinline__ uint32_t bin16(float d2, float lo, float sc) {
-  float t = (d2 - lo) * sc;
-  t = (t > 0.0f) ? t : 0.0f;
-  return (t >= 15.0f) ? 15u : (uint32_t)t;
+// value-range bin (of NB) of d2 in the bracket binning of [lo, hi]: sc = NB / (hi - lo), off =
+// -lo * sc. fma + clamp + truncate: monotone non-decreasing in d2 (any monotone map works:
+// bin_floor inverts this same function), 0 at lo and NB - 1 at hi. sc = 0 (an empty bracket)
+// puts all in bin 0.
+template <int NB>
+__device__ __forceinline__ uint32_t binN(float d2, float sc, float off) {
+  return (uint32_t)__builtin_amdgcn_fmed3f(__builtin_fmaf(d2, sc, off), 0.0f, (float)(NB - 1));
+}
+template <int NB>
+__device__ __forceinline__ void bin_setup(float lo, float hi, float &sc, float &off) {
+  sc = (hi > lo) ? (float)NB / (hi - lo) : 0.0f;
+  off = -lo * sc;
 }
 
-// smallest float x in (lo, hi] with bin16(x) >= b, for 1 <= b <= 15, lo < hi, bin16(hi) == 15
-__device__ __forceinline__ float bin_floor(uint32_t b, float lo, float hi, float sc) {
+// smallest float x in (lo, hi] with binN(x) >= b, for 1 <= b <= NB - 1, lo < hi,
+// binN(hi) == NB - 1
+template <int NB>
+__device__ __forceinline__ float bin_floor(uint32_t b, float lo, float hi, float sc, float off) {
   uint32_t l = __float_as_uint(lo), h = __float_as_uint(hi);  // bin(l) < b <= bin(h)
   float g = lo + (float)b / sc;
   if (g > lo && g < hi) {
     uint32_t gb = __float_as_uint(g);
     uint32_t gl = (gb - l > 64u) ? gb - 64u : l;
     uint32_t gh = (h - gb > 64u) ? gb + 64u : h;
-    if (bin16(__uint_as_float(gl), lo, sc) < b) l = gl;
-    if (bin16(__uint_as_float(gh), lo, sc) >= b) h = gh;
+    if (binN<NB>(__uint_as_float(gl), sc, off) < b) l = gl;
+    if (binN<NB>(__uint_as_float(gh), sc, off) >= b) h = gh;
   }
   while (h - l > 1u) {
     uint32_t m = l + ((h - l) >> 1);
-    if (bin16(__uint_as_float(m), lo, sc) >= b) h = m;
+    if (binN<NB>(__uint_as_float(m), sc, off) >= b) h = m;
     else l = m;
   }
   return __uint_as_float(h);
+}
+
+// d2 in [A, B] as one unsigned compare on the float bits (d2 >= 0): ab = bits(A), span =
+// bits(B) - bits(A); a lane that counts nothing passes ab = ~0, span = 0 (only a NaN matches)
+__device__ __forceinline__ bool in_bracket(float d2, uint32_t ab, uint32_t span) {
+  return __float_as_uint(d2) - ab <= span;
 }
 
 __device__ __forceinline__ float next_up(float x) { return __uint_as_float(__float_as_uint(x) + 1u); }
@@ -737,11 +761,14 @@ void knn_chunk_lane_kernel(KnnArgs a) {
     // ---- 3. lane select. State: every valid candidate with d2 < A is kept; `need` more come
     //         from the bracket [A, B] (smallest (d2, kd index) first); above B nothing is kept.
     float A = 0.0f, B = query_lim2(a, G, qx, qy, qz);
-    // Bin origin of the first pass: d_K(q) >= d_K(c) - |q - c|, so the K-th key most likely
-    // lies in [O, B] with O = (d_K(c) - |q - c|)^2; bin 0 takes everything below O. The
-    // origin only shapes the bins (any O < B gives the same result), so no rounding margin.
+    // Bin origin of the first pass: with the exact d_K(c), d_K(q) >= d_K(c) - |q - c|, so the
+    // K-th key lies in [O, B] with O = (d_K(c) - |q - c|)^2; bin 0 takes everything below O.
+    // The origin only shapes the bins (any O < B gives the same result), so no rounding
+    // margin. From a looser upper bound on d_K(c) (the dk bounds) the same O can lie above the
+    // K-th key (all of it in bin 0, a second pass): those bins start at 0 (GI_KNN_DBG & 32
+    // restores the old origin for measurements).
     float O = A;
-    if (G.dkc >= 0.0) {
+    if (G.dkc >= 0.0 && (G.dkc_exact || (a.dbg & 32))) {
       double ex = (double)qx - G.cx, ey = (double)qy - G.cy, ez = (double)qz - G.cz;
       double lo = G.dkc - sqrt(ex * ex + ey * ey + ez * ez);
       if (lo > 0.0) {
@@ -755,42 +782,58 @@ void knn_chunk_lane_kernel(KnnArgs a) {
       for (int pass = 0; pass < LS_PASSES && __ballot(mode == 1); pass++) {
         if (P.on) P.c[8]++;
         const bool on = mode == 1;
-        const float sc = 16.0f / (B - O);
-        // 16 bins per lane as LDS counters [bin][lane] (conflict-free, one ds_add per member)
+        float sc, off;
+        bin_setup<LS_NB>(O, B, sc, off);
+        const uint32_t ab = on ? __float_as_uint(A) : ~0u;
+        const uint32_t span = on ? __float_as_uint(B) - __float_as_uint(A) : 0u;
+        // LS_NB = 64 bins per lane: u8 counters packed four per LDS word [w][lane] (w = bin / 4;
+        // conflict-free, one ds_add per candidate; at most 255 members, so no byte carries)
 #pragma unroll
-        for (int b = 0; b < 16; b++) selh[b * 64 + lane] = 0u;
-        // groups of LS_UNROLL candidates: the group's (broadcast) LDS reads are issued together
-        // and the loop body has no branches (non-members count into the trash row 16)
+        for (int w = 0; w < 16; w++) selh[w * 64 + lane] = 0u;
+        // groups of 8 candidates: the group's (broadcast) LDS reads are issued together and the
+        // loop body has no branches (non-members, and the +inf padding past `count`, count into
+        // the trash row 16)
         for (uint32_t s0 = 0; s0 < count; s0 += 8) {
           float dg[8];
           cand_d2x8(cpos, s0, qx, qy, qz, dg);
 #pragma unroll
           for (int u = 0; u < 8; u++) {
-            float d2 = dg[u];
-            bool mem = on && (s0 + u < count) && d2 >= A && d2 <= B;
-            uint32_t b = mem ? bin16(d2, O, sc) : 16u;
-            atomicAdd(&selh[b * 64 + lane], 1u);
+            const uint32_t b = binN<LS_NB>(dg[u], sc, off);
+            const uint32_t w = in_bracket(dg[u], ab, span) ? (b >> 2) : 16u;
+            atomicAdd(&selh[w * 64 + lane], 1u << ((b & 3u) << 3));
           }
         }
         if (on) {
-          uint32_t before = 0, bs = 16, cb = 0;
+          // the K-th key's bin: word sums first (sum of four bytes), bytes inside the word
+          uint32_t before = 0, bs = LS_NB, cb = 0;
 #pragma unroll
-          for (int b = 0; b < 16; b++) {
-            uint32_t c = selh[b * 64 + lane];
-            if (bs == 16) {
-              if (before + c >= (uint32_t)need) { bs = (uint32_t)b; cb = c; }
-              else before += c;
+          for (int w = 0; w < 16; w++) {
+            const uint32_t c4 = selh[w * 64 + lane];
+            const uint32_t ws = __builtin_amdgcn_sad_u8(c4, 0u, 0u);
+            if (bs == LS_NB) {
+              if (before + ws >= (uint32_t)need) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                  const uint32_t c = (c4 >> (8 * j)) & 255u;
+                  if (bs == LS_NB) {
+                    if (before + c >= (uint32_t)need) { bs = (uint32_t)(4 * w + j); cb = c; }
+                    else before += c;
+                  }
+                }
+              } else {
+                before += ws;
+              }
             }
           }
-          if (bs == 16) {
+          if (bs == LS_NB) {
             // fewer members than needed (first pass: fewer than K within the bound): keep all
             A = next_up(B);
             need = 0;
             mode = 0;
           } else {
             need -= (int)before;
-            float nA = (bs == 0) ? A : bin_floor(bs, O, B, sc);
-            float nB = (bs == 15) ? B : next_down(bin_floor(bs + 1, O, B, sc));
+            float nA = (bs == 0) ? A : bin_floor<LS_NB>(bs, O, B, sc, off);
+            float nB = (bs == LS_NB - 1) ? B : next_down(bin_floor<LS_NB>(bs + 1, O, B, sc, off));
             if (cb == (uint32_t)need) {
               A = next_up(nB);
               need = 0;
@@ -822,23 +865,27 @@ void knn_chunk_lane_kernel(KnnArgs a) {
     float km = 0.0f;
     const bool inb_on = col && need > 0;
     // branch-free like the counting passes: a candidate that is not kept is written to row 64
+    const float acol = col ? A : 0.0f;  // kept: d2 < acol
+    const uint32_t ab = inb_on ? __float_as_uint(A) : ~0u;
+    const uint32_t span = inb_on ? __float_as_uint(B) - __float_as_uint(A) : 0u;
+    int bm = 63;  // next bracket entry, from the back
     for (uint32_t s0 = 0; s0 < count; s0 += 8) {
       float dg[8];
       cand_d2x8(cpos, s0, qx, qy, qz, dg);
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const uint32_t s = s0 + u;
-        float d2 = dg[u];
-        const bool ok = s < count;
-        const bool kf = col && ok && d2 < A;
-        const bool kb = inb_on && ok && d2 >= A && d2 <= B;
+        const float d2 = dg[u];
+        const bool kf = d2 < acol;
+        const bool kb = in_bracket(d2, ab, span);
         sel[(kf ? n : 64) * 64 + lane] = (uint8_t)s;
-        sel[(kb ? 63 - m : 64) * 64 + lane] = (uint8_t)s;
+        sel[(kb ? bm : 64) * 64 + lane] = (uint8_t)s;
         n += kf ? 1 : 0;
-        m += kb ? 1 : 0;
-        km = kf ? fmaxf(km, d2) : km;
+        bm -= kb ? 1 : 0;
+        km = fmaxf(km, kf ? d2 : 0.0f);
       }
     }
+    m = 63 - bm;
     if (inb_on) {
       // sort the bracket by (d2, kd index) and keep `need` of it
       uint64_t fk[LS_BR_L];
@@ -943,8 +990,10 @@ void knn_chunk_big_kernel(KnnArgs a) {
     const float qx = qp.x, qy = qp.y, qz = qp.z;
     // ---- lane select (see knn_chunk_lane_kernel), 16 bins x 16-bit counters
     float A = 0.0f, B = query_lim2(a, G, qx, qy, qz);
+    // bins from 0 unless GI_KNN_DBG & 64: dkc here is the dk upper bound, and the origin
+    // (dkc - |q - c|)^2 from it can lie above the K-th key (measured 33.3 -> 32.1 ms/launch)
     float O = A;
-    {
+    if (a.dbg & 64) {
       double ex = (double)qx - G.cx, ey = (double)qy - G.cy, ez = (double)qz - G.cz;
       double lo = G.dkc - sqrt(ex * ex + ey * ey + ez * ez);
       if (lo > 0.0) {
@@ -957,7 +1006,10 @@ void knn_chunk_big_kernel(KnnArgs a) {
     for (int pass = 0; pass < LS_PASSES && __ballot(mode == 1); pass++) {
       if (P.on) P.c[8]++;
       const bool on = mode == 1;
-      const float sc = 16.0f / (B - O);
+      float sc, off;
+      bin_setup<16>(O, B, sc, off);
+      const uint32_t ab = on ? __float_as_uint(A) : ~0u;
+      const uint32_t span = on ? __float_as_uint(B) - __float_as_uint(A) : 0u;
 #pragma unroll
       for (int b = 0; b < 16; b++) selw[b * 64 + lane] = 0u;
       // branch-free groups, as in the lane kernel (non-members count into row 16)
@@ -966,9 +1018,7 @@ void knn_chunk_big_kernel(KnnArgs a) {
         cand_d2x8(cpos, s0, qx, qy, qz, dg);
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-          float d2 = dg[u];
-          bool mem = on && (s0 + u < count) && d2 >= A && d2 <= B;
-          uint32_t b = mem ? bin16(d2, O, sc) : 16u;
+          const uint32_t b = in_bracket(dg[u], ab, span) ? binN<16>(dg[u], sc, off) : 16u;
           atomicAdd(&selw[b * 64 + lane], 1u);
         }
       }
@@ -988,8 +1038,8 @@ void knn_chunk_big_kernel(KnnArgs a) {
           mode = 0;
         } else {
           need -= (int)before;
-          float nA = (bs == 0) ? A : bin_floor(bs, O, B, sc);
-          float nB = (bs == 15) ? B : next_down(bin_floor(bs + 1, O, B, sc));
+          float nA = (bs == 0) ? A : bin_floor<16>(bs, O, B, sc, off);
+          float nB = (bs == 15) ? B : next_down(bin_floor<16>(bs + 1, O, B, sc, off));
           if (cb == (uint32_t)need) {
             A = next_up(nB);
             need = 0;

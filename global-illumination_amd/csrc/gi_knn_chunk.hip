@@ -270,7 +270,7 @@ __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, b
                                                    uint32_t cap, const Cands<CAPC> &cpos, uint32_t *cidx,
                                                    uint32_t *crgbe, uint32_t *hist, uint32_t *stk,
                                                    ChunkGeom &G, ChunkProf &P) {
-  constexpr int PER = CAPC / 64;
+  constexpr int PER = (CAPC + 63) / 64;
   const float4 *pos = reinterpret_cast<const float4 *>(a.map.pos4);
   const int L = a.map.nleaves;
   const int64_t N = a.map.n;
@@ -712,17 +712,18 @@ __device__ __forceinline__ float next_down(float x) { return __uint_as_float(__f
 template <int WPE, bool PROF>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE)))
 void knn_chunk_lane_kernel(KnnArgs a) {
-  constexpr int CAPC = 256;
+  // 240 candidates: 10,112 B of LDS per wave, so 16 waves (4 per SIMD, the VGPR limit) fit
+  // in a CU's 160 KiB (256 candidates took 10,752 B: 14 waves)
+  constexpr int CAPC = 240;
   __shared__ float4 cpos_lds[CAPC];
   const Cands<CAPC> cpos{reinterpret_cast<float *>(cpos_lds)};
   __shared__ uint32_t cidx[CAPC];
   __shared__ uint32_t crgbe[CAPC];
   __shared__ uint32_t stk[64];  // kd walk stack (walk_within)
   // kept LDS slots [s][lane] (K <= 64, u8) during the collect and the estimate; during the
-  // counting passes the lanes' bin counters [bin][lane] (u32), and during the bound phase the
-  // centre select's 256-bin histogram. Row 16 (u32) / 64 (u8) takes the branch-free loops'
-  // writes of non-members.
-  __shared__ uint32_t selh[17 * 64];
+  // counting passes the lanes' bin counters [w][lane] (u32, four u8 bins each), and during the
+  // bound phase the centre select's 256-bin histogram
+  __shared__ uint32_t selh[16 * 64];
   uint8_t *sel = reinterpret_cast<uint8_t *>(selh);
   uint32_t *hist = selh;
   const int lane = threadIdx.x;
@@ -791,16 +792,15 @@ void knn_chunk_lane_kernel(KnnArgs a) {
 #pragma unroll
         for (int w = 0; w < 16; w++) selh[w * 64 + lane] = 0u;
         // groups of 8 candidates: the group's (broadcast) LDS reads are issued together and the
-        // loop body has no branches (non-members, and the +inf padding past `count`, count into
-        // the trash row 16)
+        // loop body has no branches (non-members, and the +inf padding past `count`, add 0)
         for (uint32_t s0 = 0; s0 < count; s0 += 8) {
           float dg[8];
           cand_d2x8(cpos, s0, qx, qy, qz, dg);
 #pragma unroll
           for (int u = 0; u < 8; u++) {
             const uint32_t b = binN<LS_NB>(dg[u], sc, off);
-            const uint32_t w = in_bracket(dg[u], ab, span) ? (b >> 2) : 16u;
-            atomicAdd(&selh[w * 64 + lane], 1u << ((b & 3u) << 3));
+            const uint32_t inc = in_bracket(dg[u], ab, span) ? (1u << ((b & 3u) << 3)) : 0u;
+            atomicAdd(&selh[(b >> 2) * 64 + lane], inc);
           }
         }
         if (on) {
@@ -842,8 +842,10 @@ void knn_chunk_lane_kernel(KnnArgs a) {
               A = nA;
               B = nB;
               // the collect keeps the K - need photons below A at the front of the lane's
-              // slot list and the bracket's cb at its back: both must fit its 64 entries
-              if (cb <= (uint32_t)LS_BR_L && (uint32_t)(K - need) + cb <= 64u) mode = 2;
+              // slot list and the bracket's cb at its back: both must fit its 64 entries with
+              // a gap of two (the collect's stores of unkept candidates land on the next free
+              // entry of each end)
+              if (cb <= (uint32_t)LS_BR_L && (uint32_t)(K - need) + cb <= 62u) mode = 2;
               else if (!(B > A)) mode = 3;  // more than LS_BR_L photons tied at one d2
             }
           }
@@ -864,7 +866,8 @@ void knn_chunk_lane_kernel(KnnArgs a) {
     int n = 0, m = 0;
     float km = 0.0f;
     const bool inb_on = col && need > 0;
-    // branch-free like the counting passes: a candidate that is not kept is written to row 64
+    // branch-free like the counting passes: a candidate that is not kept is written to the next
+    // free entry of its end of the list (overwritten by the next kept one, or never read)
     const float acol = col ? A : 0.0f;  // kept: d2 < acol
     const uint32_t ab = inb_on ? __float_as_uint(A) : ~0u;
     const uint32_t span = inb_on ? __float_as_uint(B) - __float_as_uint(A) : 0u;
@@ -878,8 +881,10 @@ void knn_chunk_lane_kernel(KnnArgs a) {
         const float d2 = dg[u];
         const bool kf = d2 < acol;
         const bool kb = in_bracket(d2, ab, span);
-        sel[(kf ? n : 64) * 64 + lane] = (uint8_t)s;
-        sel[(kb ? bm : 64) * 64 + lane] = (uint8_t)s;
+        // (a lane without a bracket may fill all 64 entries: its bracket store goes to n too,
+        // before the front store of the same value)
+        sel[(inb_on ? bm : n) * 64 + lane] = (uint8_t)s;
+        sel[n * 64 + lane] = (uint8_t)s;
         n += kf ? 1 : 0;
         bm -= kb ? 1 : 0;
         km = fmaxf(km, kf ? d2 : 0.0f);

@@ -262,6 +262,8 @@ struct gi_ctx {
   hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;  // caustic k-NN on the side stream
   bool overlap_mc = true;
   bool overlap_maps = true;         // caustic k-NN on the side stream beside the global k-NN
+  bool fork_after_sort = true;      // ... forked after the global queries' Morton sort (a radix
+                                    // sort pass co-running with the caustic kernels stalled)
   MapExec mx[2];
   std::string err;
   gi_params P;
@@ -281,6 +283,8 @@ struct gi_ctx {
   int chunk_minsub = 32;          // chunk kernel: overflowing chunks retried as halves (measured best with the dk bound)
   double fb_ms[2] = {0, 0};       // fallback time and queries per map (since the last reset)
   uint64_t fb_q[2] = {0, 0};
+  int last_kind[2] = {-1, -1};
+  bool knn_log = false;            // GI_KNN_LOG: one stderr line per chunk k-NN launch     // k-NN kind run_knn chose last, per map (gi_render_stats)
   int sel_slack = 64;
   int knn_qpl = 1;
   int ind_waves = 3;              // indirect-path kernel occupancy target (waves per SIMD)
@@ -701,6 +705,7 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
   if (kind == 8 && (list || dkm || k.K + 64 > 1024 || !c->use_dk)) kind = auto_kind == 8 ? 1 : auto_kind;
   if (kind == 3 && (size_t)k.K * 512 > 64 * 1024) kind = auto_kind;
   if (kind == 1 && k.K + 64 > 1024) kind = 0;
+  if (!dkm) c->last_kind[k.stat_off ? 1 : 0] = kind;
   if (kind == 8) {
     // large-K chunk kernel, then the query-per-wave kernel on what it hands over
     int rc = ensure_dk(c, k);
@@ -779,6 +784,9 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
       int mi = k.stat_off ? 1 : 0;
       c->fb_ms[mi] += tf;
       c->fb_q[mi] += nfb;
+      if (c->knn_log)
+        fprintf(stderr, "[gi] knn map %d kind 8: nq %lld chunk pass %.2f ms, second pass %u, wave %u, fallback %.2f ms\n",
+                mi, (long long)nq, t - tf, nfb, nfb2, tf);
     }
     return GI_OK;
   }
@@ -840,6 +848,9 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
       int mi = k.stat_off ? 1 : 0;
       c->fb_ms[mi] += tf;
       c->fb_q[mi] += nfb;
+      if (c->knn_log)
+        fprintf(stderr, "[gi] knn map %d kind 7: nq %lld chunk %.2f ms, fallback %u in %.2f ms\n", mi,
+                (long long)nq, t - tf, nfb, tf);
     }
     return GI_OK;
   }
@@ -920,20 +931,24 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
 }
 
 // run the k-NN estimate of one query list into out[slot] (Morton-ordered launch)
+// (perm: the Morton order when the caller already sorted this list, else null)
 int knn_list(gi_ctx *c, int mi, const float4 *qpos, const QShade *qshade, int64_t nq,
-             double *out, double *ms) {
+             double *out, double *ms, uint32_t *perm_in = nullptr) {
   MapExec &X = c->mx[mi];
   KnnArgs k = knn_args(c, mi);
   k.qpos = qpos;
   k.qshade = qshade;
   k.out = out;
   k.nq = nq;
-  if (c->sort_queries) {
+  if (perm_in) {
+    k.perm = perm_in;
+  } else if (c->sort_queries) {
     uint32_t *perm = nullptr;
     HIPCHK(c, morton_order(qpos, nq, c->sbmin, c->sbmax, X.sorter, &perm, X.st));
     k.perm = perm;
   }
   if (c->P.irradiance_cache && mi == GI_MAP_GLOBAL) {
+    c->last_kind[mi] = 9;
     launch_cached(k, X.st);
     HIPCHK(c, hipGetLastError());
     return GI_OK;
@@ -1114,6 +1129,17 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     const bool side = c->overlap_maps && c->stream2 && run[0] && run[1];
     int rcm[2] = {GI_OK, GI_OK};
     std::thread worker;
+    // The global list's Morton sort runs before the fork: onesweep radix passes wait on their
+    // predecessor blocks (decoupled look-back), and beside the caustic k-NN kernels one pass
+    // took ~150 ms instead of ~4 ms (profiles/r02 kernel trace).
+    // The caustic list is sorted there too (its kernels then start beside the global chunk
+    // kernel, not beside a sort).
+    uint32_t *mperm[2] = {nullptr, nullptr};
+    if (side && c->fork_after_sort && c->sort_queries) {
+      if (!c->P.irradiance_cache)
+        HIPCHK(c, morton_order(a.qpos[0], nq[0], c->sbmin, c->sbmax, c->mx[0].sorter, &mperm[0], c->stream));
+      HIPCHK(c, morton_order(a.qpos[1], nq[1], c->sbmin, c->sbmax, c->mx[1].sorter, &mperm[1], c->stream));
+    }
     if (side) {
       HIPCHK(c, hipEventRecord(c->ev_fork2, c->stream));
       HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork2, 0));
@@ -1125,7 +1151,7 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
         }
         try {
           rcm[1] = knn_list(c, 1, a.qpos[1], a.qshade[1], nq[1], c->qout[1].as<double>(),
-                            rs ? &knn_ms[1] : nullptr);
+                            rs ? &knn_ms[1] : nullptr, mperm[1]);
         } catch (const std::bad_alloc &) {
           rcm[1] = fail(c, GI_ERR_ALLOC, "k-NN worker: host allocation failed");
         } catch (...) {
@@ -1136,7 +1162,7 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     for (int l = 0; l < 2; l++) {
       if (!run[l] || (side && l == 1)) continue;
       rcm[l] = knn_list(c, l, a.qpos[l], a.qshade[l], nq[l], c->qout[l].as<double>(),
-                        rs ? &knn_ms[l] : nullptr);
+                        rs ? &knn_ms[l] : nullptr, mperm[l]);
       if (rcm[l]) break;
     }
     if (side) {
@@ -1288,6 +1314,8 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_CHUNK_MINSUB_BIG2")) c->chunk_minsub_big2 = std::min(64, std::max(1, atoi(s)));
   if (const char *s = getenv("GI_OVERLAP_MC")) c->overlap_mc = atoi(s) != 0;
   if (const char *s = getenv("GI_OVERLAP_MAPS")) c->overlap_maps = atoi(s) != 0;
+  if (const char *s = getenv("GI_FORK_AFTER_SORT")) c->fork_after_sort = atoi(s) != 0;
+  if (const char *s = getenv("GI_KNN_LOG")) c->knn_log = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_FB_ALL")) c->chunk_fb_all = atoi(s) != 0;
   if (const char *s = getenv("GI_IND_FRAC")) c->ind_frac = std::min(1.0, std::max(1e-6, atof(s)));
   if (const char *s = getenv("GI_SORT_QUERIES")) c->sort_queries = atoi(s) != 0;
@@ -1562,6 +1590,7 @@ static int render_common(gi_ctx *c, int aa, int w, int h, const std::vector<int3
   HIPCHK(c, hipMemsetAsync(c->d_stats.p, 0, ST_BYTES, c->stream));
   c->fb_ms[0] = c->fb_ms[1] = 0;
   c->fb_q[0] = c->fb_q[1] = 0;
+  c->last_kind[0] = c->last_kind[1] = -1;
   gi_render_stats local;
   memset(&local, 0, sizeof local);
   rc = render_pixels(c, aa, w, h, pix, &local);
@@ -1591,6 +1620,7 @@ static int render_common(gi_ctx *c, int aa, int w, int h, const std::vector<int3
       st->knn_map_launches[m] = local.knn_map_launches[m];
       st->knn_map_fallback_ms[m] = c->fb_ms[m];
       st->knn_map_fallback_queries[m] = c->fb_q[m];
+      st->knn_map_kind[m] = c->last_kind[m];
     }
     st->knn_queries = st->knn_map_queries[0] + st->knn_map_queries[1];
     st->knn_photons = st->knn_map_photons[0] + st->knn_map_photons[1];
@@ -1698,6 +1728,7 @@ static int render_multi(gi_ctx *c, int aa, int w, int h, uint8_t *rgb8, float *r
         st->knn_map_launches[m] += a.knn_map_launches[m];
         st->knn_map_fallback_ms[m] += a.knn_map_fallback_ms[m];
         st->knn_map_fallback_queries[m] += a.knn_map_fallback_queries[m];
+        if (k == 0) st->knn_map_kind[m] = a.knn_map_kind[m];
       }
     }
     st->render_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

@@ -81,7 +81,7 @@ class RenderStats(C.Structure):
         ("knn_map_queries", C.c_uint64 * 2), ("knn_map_photons", C.c_uint64 * 2),
         ("knn_map_visited", C.c_uint64 * 2), ("knn_map_kernel_ms", C.c_double * 2),
         ("knn_map_launches", C.c_double * 2), ("knn_map_fallback_ms", C.c_double * 2),
-        ("knn_map_fallback_queries", C.c_uint64 * 2)]
+        ("knn_map_fallback_queries", C.c_uint64 * 2), ("knn_map_kind", C.c_int32 * 2)]
 
 
 def _stats_dict(st):

@@ -142,6 +142,10 @@ typedef struct gi_render_stats {
   /* chunk k-NN path: time and queries of the per-lane fallback within knn_map_kernel_ms */
   double knn_map_fallback_ms[2];
   uint64_t knn_map_fallback_queries[2];
+  /* k-NN launch sequence the last batch ran per map (-1 none): 7 lane-select chunk kernel +
+   * per-lane fallback, 8 large-K chunk kernel (+ second chunk pass) + query-per-wave fallback,
+   * 3 per-lane, 1 query-per-wave, 0 per-lane with global heaps, 9 irradiance-cache lookup */
+  int32_t knn_map_kind[2];
 } gi_render_stats;
 
 typedef struct gi_ctx gi_ctx;

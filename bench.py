@@ -72,7 +72,7 @@ CPU_CALIBRATION = {"ratio": round(52.70 / 72.62, 3), "restatement_s": 52.70, "re
                    "sample": "cornell 64x64 aa=0 1M+1M photons, 8 threads, build container"}
 
 
-def load_traffic(a):
+def load_traffic(a, qpl):
     """HBM bytes per launch of the roofline kernel from a committed PMC pass
     (tools/pmc_traffic.py -> profiles/knn_traffic.json), if it was taken on this workload."""
     path = os.path.join(ROOT, "profiles", "knn_traffic.json")
@@ -87,7 +87,10 @@ def load_traffic(a):
         return None
     if t.get("kernel") != " + ".join(ROOFLINE_KERNELS):
         return None  # measured on an earlier kernel
-    return t.get("bytes_per_launch")
+    bpq = t.get("bytes_per_query")
+    if not bpq:
+        return None
+    return bpq * qpl  # the PMC pass's bytes per query, at this run's launch size
 
 
 def cpu_baseline(a):
@@ -214,7 +217,7 @@ def main():
                     "fallback_query_frac": round(agg[f"fbq{m}"] / max(1.0, agg[f"q{m}"]), 4),
                     "ms_per_frame": ms / a.steps / max(1, world)}
         g, c = kstats(0), kstats(1)
-        traffic = load_traffic(a)
+        traffic = load_traffic(a, g["queries_per_launch"])
         roofline = {"bound": "hbm", "achieved": g["achieved_GBps"], "peak": HBM_PEAK_GBPS,
                     "unit": "GB/s", "frac": round(g["achieved_GBps"] / HBM_PEAK_GBPS, 5),
                     "traffic": traffic,

@@ -19,6 +19,7 @@
 #include <thread>
 #include <vector>
 #include "../../include/gi.h"
+#include "gi_kdbuild.h"
 #include "gi_kernels.h"
 #include "gi_scene.h"
 #include "gi_sort.h"
@@ -277,6 +278,9 @@ struct gi_ctx {
   DevMap dmap[2];
   bool map_valid[2] = {false, false};
   int leaf_size[2] = {64, 256};  // photons per kd leaf, per map (global, caustic)
+  bool gpu_kd = true;            // kd trees built on the device (gi_kdbuild.hip); GI_KD_BUILD=host
+  KdBuildScratch kdb;            // its scratch
+  DBuf kd_ph;                    // emission-ordered photons uploaded for the device build
   int wave_cap_mul = 1;
   int chunk_cap_big = 512;        // large-K chunk kernel: the same (384 or 512)
   int chunk_minsub_big = 64;      // large-K chunk kernel: overflowing chunks retried down to this (64: none, measured best)
@@ -456,12 +460,48 @@ int upload_map(gi_ctx *c, int mi) {
   return GI_OK;
 }
 
+// the device build (f1): the emission-ordered photons go up once, the tree, the kd-order
+// arrays and the permutation come back (perm only to the host, for the test seams' indices)
+int build_map_device(gi_ctx *c, int mi) {
+  HostMap &H = c->hmap[mi];
+  DevMap &D = c->dmap[mi];
+  const int64_t n = (int64_t)H.storage.size();
+  static_assert(sizeof(gi_photon) == sizeof(KdPhoton), "photon record layout");
+  HIPCHK(c, upload(c->kd_ph, H.storage.data(), (size_t)n * sizeof(gi_photon), c->stream));
+  int64_t L = 1;
+  while (L * c->leaf_size[mi] < n) L *= 2;
+  HIPCHK(c, D.pos4.ensure((size_t)n * 16));
+  HIPCHK(c, D.rgbe.ensure((size_t)n * 4));
+  HIPCHK(c, D.nodes.ensure((size_t)L * 16 * 4));
+  H.perm.resize(n);
+  H.pos4.clear();
+  H.rgbe.clear();
+  H.nodes.clear();
+  HIPCHK(c, kd_build_device(c->kd_ph.as<KdPhoton>(), n, c->leaf_size[mi], c->kdb, D.pos4.as<float>(),
+                            D.rgbe.as<uint32_t>(), D.nodes.as<float>(),
+                            reinterpret_cast<uint32_t *>(H.perm.data()), &H.nleaves, &H.levels,
+                            c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  D.n = n;
+  D.nleaves = H.nleaves;
+  D.levels = H.levels;
+  D.dk_k = -1;
+  c->map_valid[mi] = n > 0;
+  return GI_OK;
+}
+
+// kd tree + device arrays of map mi from its emission-ordered photons (hmap[mi].storage)
+int build_map(gi_ctx *c, int mi) {
+  if (c->gpu_kd) return build_map_device(c, mi);
+  kd_build(c->hmap[mi], c->leaf_size[mi], std::max(1, c->P.threads));
+  return upload_map(c, mi);
+}
+
 int set_map(gi_ctx *c, int mi, const gi_photon *ph, int64_t n) {
   HostMap &H = c->hmap[mi];
   H = HostMap();
   H.storage.assign(ph, ph + n);
-  kd_build(H, c->leaf_size[mi], std::max(1, c->P.threads));
-  return upload_map(c, mi);
+  return build_map(c, mi);
 }
 
 // LightPower, graphics_utils.cpp:223-258
@@ -1246,7 +1286,10 @@ int replicate_maps(gi_ctx *c) {
     d->P = c->P;
     for (int m = 0; m < 2; m++) {
       d->hmap[m] = c->hmap[m];
-      int rc = upload_map(d, m);
+      // a host-built tree is uploaded; a device-built one is rebuilt on each device (the build
+      // is a deterministic function of the photons: the same tree everywhere)
+      int rc = d->hmap[m].pos4.empty() && !d->hmap[m].storage.empty() ? build_map_device(d, m)
+                                                                        : upload_map(d, m);
       if (rc) return rc;
     }
     return (int)GI_OK;
@@ -1301,6 +1344,7 @@ int gi_create(gi_ctx **out, int dev) {
   // tuning knobs (measurement only; defaults are the measured best)
   if (const char *s = getenv("GI_LEAF_SIZE")) c->leaf_size[0] = c->leaf_size[1] = std::max(1, atoi(s));
   if (const char *s = getenv("GI_LEAF_SIZE_C")) c->leaf_size[1] = std::max(1, atoi(s));
+  if (const char *s = getenv("GI_KD_BUILD")) c->gpu_kd = strcmp(s, "host") != 0;
   if (const char *s = getenv("GI_WAVE_CAP_MUL")) c->wave_cap_mul = std::max(1, atoi(s));
   if (const char *s = getenv("GI_SEL_SLACK")) c->sel_slack = std::max(1, atoi(s));
   if (const char *s = getenv("GI_CHUNK_CAP_BIG")) c->chunk_cap_big = atoi(s) <= 384 ? 384 : 512;
@@ -1397,6 +1441,8 @@ void gi_destroy(gi_ctx *c) {
     c->dmap[m].nodes.release();
     c->dmap[m].dk.release();
   }
+  c->kdb.release();
+  c->kd_ph.release();
   if (c->ev_fork) hipEventDestroy(c->ev_fork);
   if (c->ev_fork2) hipEventDestroy(c->ev_fork2);
   if (c->ev_join2) hipEventDestroy(c->ev_join2);
@@ -1568,6 +1614,32 @@ int gi_get_photon_map(gi_ctx *c, int map, gi_photon *out, int64_t cap, int64_t *
   if (out) {
     if ((int64_t)v.size() > cap) return fail(c, GI_ERR_ARG, "capacity too small");
     memcpy(out, v.data(), v.size() * sizeof(gi_photon));
+  }
+  return GI_OK;
+}
+
+int gi_get_kd_tree(gi_ctx *c, int map, float *nodes, int64_t node_floats, int32_t *perm,
+                   int64_t perm_cap, int32_t *nleaves, int64_t *n) {
+  if (!c || map < 0 || map > 1) return GI_ERR_ARG;
+  hipSetDevice(c->device);
+  const HostMap &H = c->hmap[map];
+  const DevMap &D = c->dmap[map];
+  const int64_t nn = (int64_t)H.storage.size();
+  if (n) *n = nn;
+  if (nleaves) *nleaves = H.nleaves;
+  const int64_t nf = (int64_t)16 * H.nleaves;
+  if (nodes) {
+    if (node_floats < nf) return fail(c, GI_ERR_ARG, "node capacity too small");
+    if (D.nodes.p && D.nodes.cap >= (size_t)nf * 4) {
+      HIPCHK(c, hipMemcpyAsync(nodes, D.nodes.p, (size_t)nf * 4, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+    } else {
+      memset(nodes, 0, (size_t)nf * 4);
+    }
+  }
+  if (perm) {
+    if (perm_cap < nn) return fail(c, GI_ERR_ARG, "capacity too small");
+    memcpy(perm, H.perm.data(), (size_t)nn * 4);
   }
   return GI_OK;
 }

@@ -28,7 +28,7 @@ EXPORTED = [
     "gi_params_default", "gi_parse_args", "gi_create", "gi_create_devices", "gi_destroy",
     "gi_last_error",
     "gi_set_params", "gi_read_scene", "gi_scene_info", "gi_map_photons", "gi_set_photon_map",
-    "gi_get_photon_map", "gi_render_image", "gi_render_tiles", "gi_quantize",
+    "gi_get_photon_map", "gi_get_kd_tree", "gi_render_image", "gi_render_tiles", "gi_quantize",
     "gi_estimate_radiance_batch", "gi_knn_batch", "gi_knn_bench", "gi_intersect_batch",
     "gi_write_image",
 ]
@@ -121,6 +121,8 @@ def lib():
         L.gi_set_photon_map.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64]
         L.gi_get_photon_map.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64,
                                         P(C.c_int64)]
+        L.gi_get_kd_tree.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64, C.c_void_p,
+                                     C.c_int64, P(C.c_int32), P(C.c_int64)]
         L.gi_render_image.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                       C.c_void_p, P(RenderStats)]
         L.gi_render_tiles.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
@@ -227,6 +229,16 @@ class Renderer:
         self._check(lib().gi_get_photon_map(self._ctx, which, out.ctypes.data, n.value,
                                             C.byref(n)))
         return out
+
+    def kd_tree(self, which):
+        """(nodes [2L, 8] float32, perm [n] int32 kd position -> emission index, nleaves)"""
+        nl, n = C.c_int32(), C.c_int64()
+        self._check(lib().gi_get_kd_tree(self._ctx, which, None, 0, None, 0, C.byref(nl), C.byref(n)))
+        nodes = np.zeros((2 * nl.value, 8), dtype=np.float32)
+        perm = np.zeros(n.value, dtype=np.int32)
+        self._check(lib().gi_get_kd_tree(self._ctx, which, nodes.ctypes.data, nodes.size,
+                                         perm.ctypes.data, n.value, C.byref(nl), C.byref(n)))
+        return nodes, perm, nl.value
 
     def set_photon_map(self, which, photons):
         photons = np.ascontiguousarray(photons, dtype=PHOTON_DTYPE)

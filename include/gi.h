@@ -184,6 +184,12 @@ int gi_map_photons(gi_ctx *ctx, gi_photon_stats *stats);
 int gi_set_photon_map(gi_ctx *ctx, int map, const gi_photon *photons, int64_t n);
 /* Copy a photon map back in storage (emission) order. */
 int gi_get_photon_map(gi_ctx *ctx, int map, gi_photon *out, int64_t capacity, int64_t *n);
+/* Test seam: the map's kd tree as the k-NN kernels read it (the R3Kdtree the reference builds
+ * in R3Kdtree.cpp:1552-1671). nodes: 8 floats per node of the implicit tree (node v = 1 ..
+ * 2 * nleaves - 1; {lo.xyz, split}, {hi.xyz, axis bits}); perm: kd-order position -> emission
+ * index. Null outputs only report the sizes. */
+int gi_get_kd_tree(gi_ctx *ctx, int map, float *nodes, int64_t node_floats, int32_t *perm,
+                   int64_t perm_capacity, int32_t *nleaves, int64_t *n);
 
 /* ---- rendering ------------------------------------------------------------------------ */
 /* Full frame; rgb8 is W*H*3 bytes row-major with row 0 = image row y=0 (bottom, as R2Image);

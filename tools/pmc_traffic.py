@@ -7,7 +7,10 @@ Writes profiles/knn_traffic.json, read by bench.py for roofline.traffic when the
 matches.
 
 usage: pmc_traffic.py <counter_collection.csv> <kernel-substring[,substring...]> <res> <aa>
-                     <global> <caustic>
+                     <global> <caustic> [bench log of the PMC run]
+The bench log (of the PMC run itself, --warmup 0, so that its k-NN stats cover every dispatch
+the counters saw) gives the global map's query count: the traffic is kept as bytes per query,
+and bench.py scales it by its own queries per launch (launch sizes follow the batch size).
 Several substrings: the roofline "launch" is that sequence of kernels (e.g. the chunk kernel and
 its per-lane fallback); their per-dispatch averages are summed.
 """
@@ -20,8 +23,14 @@ import sys
 def main():
     path, knames = sys.argv[1], sys.argv[2].split(",")
     res, aa, glob, caus = (int(x) for x in sys.argv[3:7])
+    nq = None
+    if len(sys.argv) > 7:
+        for line in open(sys.argv[7]):
+            if line.startswith("{"):
+                g = json.loads(line)["roofline"]["global"]
+                nq = g["queries_per_launch"] * g["launches"]
     rows = list(csv.DictReader(open(path)))
-    kib, ndisp = 0.0, {}
+    kib, ndisp, kib_all = 0.0, {}, 0.0
     for kname in knames:
         per = {}
         for r in rows:
@@ -31,11 +40,14 @@ def main():
         if not per:
             sys.exit(f"no FETCH_SIZE rows for {kname!r} in {path}")
         kib += sum(per.values()) / len(per)
+        kib_all += sum(per.values())
         ndisp[kname] = len(per)
     out = {"kernel": " + ".join(knames), "dispatches": ndisp, "fetch_size_kib_per_launch": kib,
            "correction": "x2 (gfx950 FETCH_SIZE = 1/2 of bytes read, MI355X_MICROARCH.md) x1024",
            "bytes_per_launch": kib * 1024 * 2,
            "workload": {"res": res, "aa": aa, "global": glob, "caustic": caus},
+           "queries": nq,
+           "bytes_per_query": kib_all * 1024 * 2 / nq if nq else None,
            "source": os.path.relpath(path)}
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     with open(os.path.join(root, "profiles", "knn_traffic.json"), "w") as f:

@@ -11,17 +11,18 @@
 // Built level by level, one radix sort per level instead of a recursion:
 //   level d: (1) tight boxes of the 2^d nodes (segmented min/max over the current order),
 //            (2) each node's axis from its box (longest extent, the host rule),
-//            (3) a stable sort of all positions by (node, coordinate along the node's axis):
+//            (3) a radix sort of all positions by (node, coordinate along the node's axis):
 //                every node's range ends up ordered along its axis, so its lower half is the
 //                lower child's range,
 //            (4) split = the coordinate at the node's median position.
 //   then the leaves' tight boxes, and the kd-order position / rgbe arrays.
-// The stable sort keeps the previous level's order among equal coordinates, so the tree is a
+// Equal coordinates are ordered by a hash of the emission index (step 3), so the tree is a
 // deterministic function of the emission-ordered photons (the host build's nth_element gives
 // another equally valid order inside a node; the k-NN set is the same up to ties at the K-th
 // distance, which both orders break by kd-order index).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <algorithm>
 #include <stdint.h>
 #include "gi_kdbuild.h"
 
@@ -112,14 +113,22 @@ __global__ void kd_node_kernel(const uint32_t *box, int64_t n, int64_t L, int le
   if (axis) axis[j] = a;
 }
 
-// (3) sort keys of level d: node (d bits) above the coordinate along the node's axis
+// (3) sort keys of level d: node (d bits) above the coordinate along the node's axis, above tb
+//     bits of a hash of the photon's emission index. The hash scatters photons with equal
+//     coordinates over both halves of a median that falls inside their run (photons on an
+//     axis-aligned wall share its coordinate): kept in the previous level's order they would
+//     split by another axis, and a query on that plane, which the split-plane descents send to
+//     the upper child, would find its first leaf far away (measured: caustic chunk k-NN 670 ->
+//     842 candidates per query on cornell); the host's nth_element scatters them too.
 __global__ __launch_bounds__(256) void kd_key_kernel(const KdPhoton *ph, const uint32_t *perm, int64_t n,
-                                                     int64_t L, int levels, int d, const int32_t *axis,
-                                                     uint64_t *keys) {
+                                                     int64_t L, int levels, int d, int tb,
+                                                     const int32_t *axis, uint64_t *keys) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t j = ((L + leaf_of(i, n, L)) >> (levels - d)) - ((int64_t)1 << d);
-  keys[i] = ((uint64_t)j << 32) | (uint64_t)f2o(ph[perm[i]].pos[axis[j]]);
+  const uint32_t e = perm[i];
+  const uint64_t h = tb ? (uint64_t)((e * 0x9E3779B1u) >> (32 - tb)) : 0ull;
+  keys[i] = ((uint64_t)j << (32 + tb)) | ((uint64_t)f2o(ph[e].pos[axis[j]]) << tb) | h;
 }
 
 // (4) split of each level-d node: the coordinate at its median position (host kd_rec: the
@@ -184,9 +193,10 @@ hipError_t kd_build_device(const KdPhoton *ph, int64_t n, int leaf_size, KdBuild
     kd_box_kernel<<<blocks(n, 256), 256, 0, st>>>(ph, pa, n, L, levels, d, s.box);
     kd_node_kernel<<<blocks(nn, 256), 256, 0, st>>>(s.box, n, L, levels, d, nodes, s.axis);
     if (d == levels) break;
-    kd_key_kernel<<<blocks(n, 256), 256, 0, st>>>(ph, pa, n, L, levels, d, s.axis, ka);
+    const int hb = std::min(12, 32 - d);  // hash bits below the coordinate
+    kd_key_kernel<<<blocks(n, 256), 256, 0, st>>>(ph, pa, n, L, levels, d, hb, s.axis, ka);
     size_t tb = s.tmp_cap;
-    e = hipcub::DeviceRadixSort::SortPairs(s.tmp, tb, ka, kb, pa, pb, (int)n, 0, 32 + d, st);
+    e = hipcub::DeviceRadixSort::SortPairs(s.tmp, tb, ka, kb, pa, pb, (int)n, 0, 32 + d + hb, st);
     if (e != hipSuccess) return e;
     std::swap(pa, pb);
     kd_split_kernel<<<blocks(nn, 256), 256, 0, st>>>(ph, pa, n, L, d, nodes, s.axis);

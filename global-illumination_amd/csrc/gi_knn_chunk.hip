@@ -653,7 +653,12 @@ __device__ __forceinline__ void chunk_flush_stats(const KnnArgs &a, const ChunkP
 // ---------------------------------------------------------------------------------------------
 // lane select: one query per lane, counting passes over the LDS candidates
 // ---------------------------------------------------------------------------------------------
-constexpr int LS_BR = 4;       // bracket photons resolved by the collect pass (large-K kernel)
+#ifndef LS_BR_B
+#define LS_BR_B 16             // bracket photons resolved by the collect pass (large-K kernel)
+#endif
+#ifndef LS_NBB
+#define LS_NBB 32              // value-range bins per counting pass of the large-K kernel
+#endif
 #ifndef LS_BR_L
 #define LS_BR_L 12             // the same for the lane-select kernel (bracket kept in its LDS slot list; measured best)
 #endif
@@ -953,6 +958,8 @@ template <int CAPC, bool PROF>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
 void knn_chunk_big_kernel(KnnArgs a) {
   constexpr int NW = CAPC / 32;
+  // bracket list length: 8 keeps the 512-candidate kernel at 17.6 KB of LDS (9 waves per CU)
+  constexpr int BRB = CAPC <= 512 ? 8 : LS_BR_B;
   __shared__ float4 cpos_lds[CAPC];
   const Cands<CAPC> cpos{reinterpret_cast<float *>(cpos_lds)};
   __shared__ uint32_t cidx[CAPC];
@@ -960,8 +967,9 @@ void knn_chunk_big_kernel(KnnArgs a) {
   __shared__ uint32_t hist[4];       // unused by the dk bound (chunk_bound_gather signature)
   __shared__ uint32_t stk[64];
   // kept-candidate bitmask [word][lane] during the collect and the estimate; during the counting
-  // passes the lanes' 16 bin counters [bin][lane]
-  __shared__ uint32_t selw[(NW > 17 ? NW : 17) * 64];  // row 16: trash counters
+  // passes the lanes' LS_NBB 16-bit bin counters, two per word [w][lane]
+  __shared__ uint32_t selw[(NW > LS_NBB / 2 ? NW : LS_NBB / 2) * 64];
+  __shared__ uint16_t brl[(BRB + 1) * 64];  // bracket list [i][lane] of the collect
   const int lane = threadIdx.x;
   const int K = a.K;
   const int minsub = a.chunk_minsub > 0 ? a.chunk_minsub : 64;
@@ -993,7 +1001,8 @@ void knn_chunk_big_kernel(KnnArgs a) {
     pending &= ~gm;
     const uint32_t count = G.count;
     const float qx = qp.x, qy = qp.y, qz = qp.z;
-    // ---- lane select (see knn_chunk_lane_kernel), 16 bins x 16-bit counters
+    // ---- lane select (see knn_chunk_lane_kernel): LS_NBB value-range bins per counting pass,
+    //      16-bit counters packed two per LDS word [w][lane] (a chunk gathers <= 1024 photons)
     float A = 0.0f, B = query_lim2(a, G, qx, qy, qz);
     // bins from 0 unless GI_KNN_DBG & 64: dkc here is the dk upper bound, and the origin
     // (dkc - |q - c|)^2 from it can lie above the K-th key (measured 33.3 -> 32.1 ms/launch)
@@ -1012,39 +1021,44 @@ void knn_chunk_big_kernel(KnnArgs a) {
       if (P.on) P.c[8]++;
       const bool on = mode == 1;
       float sc, off;
-      bin_setup<16>(O, B, sc, off);
+      bin_setup<LS_NBB>(O, B, sc, off);
       const uint32_t ab = on ? __float_as_uint(A) : ~0u;
       const uint32_t span = on ? __float_as_uint(B) - __float_as_uint(A) : 0u;
 #pragma unroll
-      for (int b = 0; b < 16; b++) selw[b * 64 + lane] = 0u;
-      // branch-free groups, as in the lane kernel (non-members count into row 16)
+      for (int w = 0; w < LS_NBB / 2; w++) selw[w * 64 + lane] = 0u;
+      // branch-free groups of 8, as in the lane kernel (non-members and the +inf padding add 0)
       for (uint32_t s0 = 0; s0 < count; s0 += 8) {
         float dg[8];
         cand_d2x8(cpos, s0, qx, qy, qz, dg);
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-          const uint32_t b = in_bracket(dg[u], ab, span) ? binN<16>(dg[u], sc, off) : 16u;
-          atomicAdd(&selw[b * 64 + lane], 1u);
+          const uint32_t b = binN<LS_NBB>(dg[u], sc, off);
+          const uint32_t inc = in_bracket(dg[u], ab, span) ? (1u << ((b & 1u) << 4)) : 0u;
+          atomicAdd(&selw[(b >> 1) * 64 + lane], inc);
         }
       }
       if (on) {
-        uint32_t before = 0, bs = 16, cb = 0;
+        uint32_t before = 0, bs = LS_NBB, cb = 0;
 #pragma unroll
-        for (int b = 0; b < 16; b++) {
-          uint32_t c = selw[b * 64 + lane];
-          if (bs == 16) {
-            if (before + c >= (uint32_t)need) { bs = (uint32_t)b; cb = c; }
-            else before += c;
+        for (int w = 0; w < LS_NBB / 2; w++) {
+          const uint32_t c2 = selw[w * 64 + lane];
+#pragma unroll
+          for (int j = 0; j < 2; j++) {
+            const uint32_t c = (c2 >> (16 * j)) & 0xffffu;
+            if (bs == LS_NBB) {
+              if (before + c >= (uint32_t)need) { bs = (uint32_t)(2 * w + j); cb = c; }
+              else before += c;
+            }
           }
         }
-        if (bs == 16) {
+        if (bs == LS_NBB) {
           A = next_up(B);
           need = 0;
           mode = 0;
         } else {
           need -= (int)before;
-          float nA = (bs == 0) ? A : bin_floor<16>(bs, O, B, sc, off);
-          float nB = (bs == 15) ? B : next_down(bin_floor<16>(bs + 1, O, B, sc, off));
+          float nA = (bs == 0) ? A : bin_floor<LS_NBB>(bs, O, B, sc, off);
+          float nB = (bs == LS_NBB - 1) ? B : next_down(bin_floor<LS_NBB>(bs + 1, O, B, sc, off));
           if (cb == (uint32_t)need) {
             A = next_up(nB);
             need = 0;
@@ -1052,7 +1066,7 @@ void knn_chunk_big_kernel(KnnArgs a) {
           } else {
             A = nA;
             B = nB;
-            if (cb <= (uint32_t)LS_BR) mode = 2;
+            if (cb <= (uint32_t)BRB) mode = 2;
             else if (!(B > A)) mode = 3;
           }
         }
@@ -1066,51 +1080,59 @@ void knn_chunk_big_kernel(KnnArgs a) {
       if (P.on) P.c[9] += (uint64_t)__popcll(fbm);
     }
     const bool col = act && !fb;
-    // ---- collect: bitmask of the candidates below A, plus the bracket's kept ones
+    // ---- collect, branch-free: bitmask words of the candidates below A; the bracket's photons
+    //      (<= BRB) to a per-lane LDS list, each candidate stored at the list's next free entry
+    //      (a member advances it), then sorted by (d2, kd index) in registers
     int n = 0;
     float km = 0.0f;
-    uint64_t br[LS_BR];
-#pragma unroll
-    for (int i = 0; i < LS_BR; i++) br[i] = ~0ull;
     const bool inb_on = col && need > 0;
+    const float acol = col ? A : 0.0f;
+    const uint32_t cab = inb_on ? __float_as_uint(A) : ~0u;
+    const uint32_t cspan = inb_on ? __float_as_uint(B) - __float_as_uint(A) : 0u;
+    int m = 0;
     for (uint32_t w0 = 0; w0 < (count + 31) / 32; w0++) {
       uint32_t bits = 0;
-#pragma unroll 4
-      for (uint32_t j = 0; j < 32; j++) {
-        uint32_t s = w0 * 32 + j;
-        if (s >= count) break;
-        float d2 = cpos.d2(qx, qy, qz, s);
-        if (col && d2 < A) {
-          bits |= 1u << j;
-          km = fmaxf(km, d2);
-        }
-        if (inb_on && d2 >= A && d2 <= B) {
 #pragma unroll
-          for (int i = LS_BR - 1; i > 0; i--) br[i] = br[i - 1];
-          br[0] = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)s;
+      for (uint32_t j0 = 0; j0 < 32; j0 += 8) {
+        const uint32_t s0 = w0 * 32 + j0;
+        if (s0 >= count) break;  // wave-uniform
+        float dg[8];
+        cand_d2x8(cpos, s0, qx, qy, qz, dg);
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const bool kf = dg[u] < acol;
+          const bool kb = in_bracket(dg[u], cab, cspan);
+          bits |= kf ? (1u << (j0 + u)) : 0u;
+          km = fmaxf(km, kf ? dg[u] : 0.0f);
+          brl[m * 64 + lane] = (uint16_t)(s0 + u);
+          m += kb ? 1 : 0;
         }
       }
       selw[w0 * 64 + lane] = bits;
       n += __popc(bits);
     }
     if (inb_on) {
-      uint64_t fk[LS_BR];
-      uint32_t sl[LS_BR];
+      uint64_t fk[BRB];
+      uint32_t sl[BRB];
 #pragma unroll
-      for (int i = 0; i < LS_BR; i++) {
-        sl[i] = (uint32_t)br[i];
-        fk[i] = (br[i] == ~0ull) ? ~0ull : ((br[i] & 0xffffffff00000000ull) | (uint64_t)cidx[sl[i] % CAPC]);
+      for (int i = 0; i < BRB; i++) {
+        sl[i] = 0u;
+        fk[i] = ~0ull;
+        if (i < m) {
+          sl[i] = brl[i * 64 + lane];
+          fk[i] = ((uint64_t)__float_as_uint(cpos.d2(qx, qy, qz, sl[i])) << 32) | (uint64_t)cidx[sl[i]];
+        }
       }
 #pragma unroll
-      for (int i = 0; i < LS_BR; i++)
+      for (int i = 0; i < BRB; i++)
 #pragma unroll
-        for (int j = 0; j + 1 < LS_BR - i; j++)
+        for (int j = 0; j + 1 < BRB - i; j++)
           if (fk[j + 1] < fk[j]) {
             uint64_t t = fk[j]; fk[j] = fk[j + 1]; fk[j + 1] = t;
             uint32_t u = sl[j]; sl[j] = sl[j + 1]; sl[j + 1] = u;
           }
 #pragma unroll
-      for (int i = 0; i < LS_BR; i++)
+      for (int i = 0; i < BRB; i++)
         if (i < need) {
           selw[(sl[i] / 32) * 64 + lane] |= 1u << (sl[i] % 32);
           n++;
@@ -1193,7 +1215,8 @@ bool launch_knn_chunk(const KnnArgs &a, hipStream_t st) {
   if (a.nq == 0) return true;
   if (a.mode == KNN_MODE_LIST || a.K > 64) return false;
   unsigned grid = knn_chunk_grid(a.nq);
-  if (a.dbg & 16) knn_chunk_lane_kernel<3, true><<<grid, 64, 0, st>>>(a);
+  // GI_KNN_DBG & 128: phase counters from the large-K kernel only
+  if ((a.dbg & 16) && !(a.dbg & 128)) knn_chunk_lane_kernel<3, true><<<grid, 64, 0, st>>>(a);
   else knn_chunk_lane_kernel<4, false><<<grid, 64, 0, st>>>(a);
   return true;
 }

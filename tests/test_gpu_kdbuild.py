@@ -155,3 +155,22 @@ def test_cornell_maps_device_tree(renderer):
         check_tree(nodes, perm, L, renderer.photon_map(m))
     ref, _ = oracle_lib.render(args, 40, 40)
     gpu_util.compare(rgb, ref, 0.97, 0.99, 0.5)
+
+
+@pytest.mark.parametrize("n,which", [(5000, GLOBAL), (70001, CAUSTIC)])
+def test_device_tree_equals_host_tree_without_ties(renderer, host_renderer, n, which):
+    """tie-free photons: the same median splits, axes, boxes and leaf sets from both builds"""
+    rng = np.random.default_rng(n)
+    ph = synth.photon_map(n, seed=n)
+    # distinct coordinates along every axis
+    ph["pos"] = np.stack([(rng.permutation(n) + 0.25) / n for _ in range(3)], 1).astype(np.float32)
+    assert all(len(np.unique(ph["pos"][:, k])) == n for k in range(3))
+    renderer.set_photon_map(which, ph)
+    host_renderer.set_photon_map(which, ph)
+    dn, dp, dl = renderer.kd_tree(which)
+    hn, hp, hl = host_renderer.kd_tree(which)
+    assert dl == hl
+    np.testing.assert_array_equal(dn, hn)
+    for l in range(dl):  # the same photons in every leaf (order inside a leaf may differ)
+        s0, s1 = l * n // dl, (l + 1) * n // dl
+        assert sorted(dp[s0:s1].tolist()) == sorted(hp[s0:s1].tolist())

@@ -47,6 +47,9 @@ __device__ __forceinline__ double wmax(double v) {
 #ifndef CHUNK_EST_EB
 #define CHUNK_EST_EB 4         // photons per LDS/LUT round trip in the chunk estimate
 #endif
+#ifndef CHUNK_EST_V
+#define CHUNK_EST_V 0          // diffuse estimate form (experiments: 1 branch-free, 2 kd per query)
+#endif
 
 // ascending bitonic sort of one float per lane across the wave
 __device__ __forceinline__ float wave_sort(float v, int lane) {
@@ -525,6 +528,26 @@ __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, flo
             lg[u][1] = a.lut[3 * dc + 1];
             lg[u][2] = a.lut[3 * dc + 2];
           }
+#if CHUNK_EST_V == 1
+          // per photon: w = |perp| * 2^(e - 136) (exact: a power-of-two scaling), the channel
+          // terms byte * w equal (byte * 2^(e - 136)) * |perp| bit for bit, and kd multiplies
+          // the sums once per query (re-associated like the sum order: relative 1e-16 per term)
+#pragma unroll
+          for (int u = 0; u < EB; u++) {
+            if (s0 + u >= num) break;
+            double ix = lg[u][0], iy = lg[u][1], iz = lg[u][2];
+            double perp = N0 * ix + N1 * iy + N2 * iz;
+            const bool skip = (sign == 2u && perp < 0) || (sign == 1u && perp > 0);
+            uint32_t e = eg[u];
+            uint32_t ee = e >> 24;
+            double w = (skip || !ee) ? 0.0 : ldexp(fabs(perp), (int)ee - 128 - 8);
+            o0 += (double)(e & 255u) * w;
+            o1 += (double)((e >> 8) & 255u) * w;
+            o2 += (double)((e >> 16) & 255u) * w;
+          }
+        }
+        o0 *= kd0; o1 *= kd1; o2 *= kd2;
+#else
 #pragma unroll
           for (int u = 0; u < EB; u++) {
             if (s0 + u >= num) break;
@@ -538,12 +561,21 @@ __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, flo
             double p1 = ee ? (double)((e >> 8) & 255u) * inv : 0.0;
             double p2 = ee ? (double)((e >> 16) & 255u) * inv : 0.0;
             double ap = fabs(perp);
+#if CHUNK_EST_V == 2
+            // kd multiplies the sums once per query (re-associated, relative 1e-16 per term)
+            p0 *= ap; p1 *= ap; p2 *= ap;
+#else
             p0 *= ap * kd0;
             p1 *= ap * kd1;
             p2 *= ap * kd2;
+#endif
             o0 += p0; o1 += p1; o2 += p2;
           }
         }
+#if CHUNK_EST_V == 2
+        o0 *= kd0; o1 *= kd1; o2 *= kd2;
+#endif
+#endif
       } else {
       const double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
       for (int s0 = 0; s0 < num; s0 += EB) {

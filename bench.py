@@ -5,8 +5,8 @@ photons (BASELINE.json configs[1] = SURVEY.md C2).
 A step = one full frame (RenderImage, render.cpp:155-259) over the resident scene and photon
 maps. With N ranks (torchrun, one process per GPU) the frame's 16x16-pixel tiles are dealt
 round-robin (tile % N, the reference's column interleave render.cpp:90 re-cut as tiles); each
-rank renders its tiles and the image is gathered to rank 0 with one RCCL reduce over xGMI
-(disjoint tiles, so the sum is a gather). Total work per step is fixed -> "scaling": "strong".
+rank renders its tiles and sends only its own packed pixels to rank 0 in one RCCL gather over
+xGMI (gi_dist.py). Total work per step is fixed -> "scaling": "strong".
 The photon maps are built once per rank from the same seed (identical, no communication) and
 their build time is reported separately (photon_map_s), as SURVEY.md §8(d) prescribes.
 

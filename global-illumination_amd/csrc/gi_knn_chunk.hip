@@ -47,8 +47,8 @@ __device__ __forceinline__ double wmax(double v) {
 #ifndef CHUNK_EST_EB
 #define CHUNK_EST_EB 4         // photons per LDS/LUT round trip in the chunk estimate
 #endif
-#ifndef CHUNK_EST_V
-#define CHUNK_EST_V 0          // diffuse estimate form (experiments: 1 branch-free, 2 kd per query)
+#ifndef EST_GROUPS
+#define EST_GROUPS 3           // (normal, side) groups per chunk estimated from shared photon terms
 #endif
 
 // ascending bitonic sort of one float per lane across the wave
@@ -528,26 +528,9 @@ __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, flo
             lg[u][1] = a.lut[3 * dc + 1];
             lg[u][2] = a.lut[3 * dc + 2];
           }
-#if CHUNK_EST_V == 1
-          // per photon: w = |perp| * 2^(e - 136) (exact: a power-of-two scaling), the channel
-          // terms byte * w equal (byte * 2^(e - 136)) * |perp| bit for bit, and kd multiplies
-          // the sums once per query (re-associated like the sum order: relative 1e-16 per term)
-#pragma unroll
-          for (int u = 0; u < EB; u++) {
-            if (s0 + u >= num) break;
-            double ix = lg[u][0], iy = lg[u][1], iz = lg[u][2];
-            double perp = N0 * ix + N1 * iy + N2 * iz;
-            const bool skip = (sign == 2u && perp < 0) || (sign == 1u && perp > 0);
-            uint32_t e = eg[u];
-            uint32_t ee = e >> 24;
-            double w = (skip || !ee) ? 0.0 : ldexp(fabs(perp), (int)ee - 128 - 8);
-            o0 += (double)(e & 255u) * w;
-            o1 += (double)((e >> 8) & 255u) * w;
-            o2 += (double)((e >> 16) & 255u) * w;
-          }
-        }
-        o0 *= kd0; o1 *= kd1; o2 *= kd2;
-#else
+          // per photon (byte * 2^(e - 136)) * |perp|; kd multiplies the sums once per query
+          // (re-associated like the sum order: relative 1e-16 per term). The same terms as
+          // chunk_estimate_shared's, bit for bit.
 #pragma unroll
           for (int u = 0; u < EB; u++) {
             if (s0 + u >= num) break;
@@ -561,21 +544,11 @@ __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, flo
             double p1 = ee ? (double)((e >> 8) & 255u) * inv : 0.0;
             double p2 = ee ? (double)((e >> 16) & 255u) * inv : 0.0;
             double ap = fabs(perp);
-#if CHUNK_EST_V == 2
-            // kd multiplies the sums once per query (re-associated, relative 1e-16 per term)
             p0 *= ap; p1 *= ap; p2 *= ap;
-#else
-            p0 *= ap * kd0;
-            p1 *= ap * kd1;
-            p2 *= ap * kd2;
-#endif
             o0 += p0; o1 += p1; o2 += p2;
           }
         }
-#if CHUNK_EST_V == 2
         o0 *= kd0; o1 *= kd1; o2 *= kd2;
-#endif
-#endif
       } else {
       const double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
       for (int s0 = 0; s0 < num; s0 += EB) {
@@ -656,6 +629,139 @@ __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, flo
   a.out[3 * qi + 2] = o2;
   if (a.out_n) a.out_n[qi] = num;
   if (a.out_maxd2) a.out_maxd2[qi] = (num > 0) ? (float)maxd2 : 0.0f;
+}
+
+// ---- 4b. the estimate of the chunk's queries that share a surface normal and side, on the
+//          common path (disk filter, materials without a specular term). For such queries a
+//          photon's term (byte * 2^(e - 136)) * |N . I| does not depend on the query, so it is
+//          computed once per candidate (lanes over candidates, 4 per lane) into LDS over the
+//          candidate arrays (tp, [3][CAPC] doubles: the arrays are no longer needed), and each
+//          query sums its kept slots: 3 LDS reads and 3 adds per photon instead of ~45
+//          instructions. Up to EST_GROUPS groups (a chunk on one wall: one); the other queries
+//          estimate per lane first (they still read the candidate arrays). Bit-identical to
+//          chunk_estimate's per-lane sums (same terms, same slot order); GI_KNN_DBG & 256 turns
+//          the sharing off.
+template <int CAPC, typename SlotAt, typename PerLane>
+__device__ __forceinline__ void chunk_estimate_shared(const KnnArgs &a, int lane, bool col, int64_t qi,
+                                                      float4 qp, int num, float km, uint32_t count,
+                                                      const Cands<CAPC> &cpos, const uint32_t *crgbe,
+                                                      double *tp, SlotAt slot_at, PerLane per_lane) {
+  bool shp = false;
+  double N0 = 0.0, N1 = 0.0, N2 = 0.0;
+  uint32_t sign = 0u;
+  const DMaterial *mt = nullptr;
+  if (col && num > 0 && a.mode == KNN_MODE_RADIANCE && a.filter == 0 && !(a.dbg & 256)) {
+    const uint32_t meta = __float_as_uint(qp.w);
+    mt = &a.mats[meta >> 2];
+    const bool spec = (mt->flags & MF_SPECULAR) || (mt->n < 0);
+    shp = !spec && isfinite(mt->ks[0]) && isfinite(mt->ks[1]) && isfinite(mt->ks[2]);
+    if (shp) {
+      const QShade &sh = a.qshade[qi];
+      N0 = sh.n[0]; N1 = sh.n[1]; N2 = sh.n[2];
+      sign = meta & 3u;
+    }
+  }
+  // groups: equal normal bits and side flags (a NaN normal never forms a group: bounded loop)
+  uint64_t rem = __ballot(shp);
+  int gi = -1, ng = 0;
+  int lead[EST_GROUPS];
+#pragma unroll
+  for (int g = 0; g < EST_GROUPS; g++) {
+    lead[g] = 0;
+    if (!rem) continue;  // wave-uniform
+    const int L0 = __ffsll((long long)rem) - 1;
+    const long long l0 = __shfl(__double_as_longlong(N0), L0, 64);
+    const long long l1 = __shfl(__double_as_longlong(N1), L0, 64);
+    const long long l2 = __shfl(__double_as_longlong(N2), L0, 64);
+    const uint32_t ls = (uint32_t)__shfl((int)sign, L0, 64);
+    const bool in = ((rem >> lane) & 1ull) && __double_as_longlong(N0) == l0 &&
+                    __double_as_longlong(N1) == l1 && __double_as_longlong(N2) == l2 && sign == ls;
+    const uint64_t m = __ballot(in);
+    if (in) gi = g;
+    lead[g] = L0;
+    rem &= ~m;
+    rem &= ~(1ull << L0);
+    ng = g + 1;
+  }
+  if (col && gi < 0) per_lane();
+  if (ng == 0) return;
+  constexpr int PC = (CAPC + 63) / 64;
+  uint32_t cw[PC], ce[PC];
+#pragma unroll
+  for (int i = 0; i < PC; i++) {
+    const uint32_t s = (uint32_t)(i * 64 + lane);
+    cw[i] = s < count ? (__float_as_uint(cpos.wbits(s)) & 0xffffu) : 0u;
+    ce[i] = s < count ? crgbe[s] : 0u;
+  }
+  double o0 = 0.0, o1 = 0.0, o2 = 0.0;
+#pragma unroll
+  for (int g = 0; g < EST_GROUPS; g++) {
+    if (g >= ng) break;  // wave-uniform
+    const int L0 = lead[g];
+    const double g0 = __shfl(N0, L0, 64), g1 = __shfl(N1, L0, 64), g2 = __shfl(N2, L0, 64);
+    const uint32_t gs = (uint32_t)__shfl((int)sign, L0, 64);
+    __syncthreads();  // readers of the candidate arrays / of the previous group's terms are done
+#pragma unroll
+    for (int i = 0; i < PC; i++) {
+      const uint32_t s = (uint32_t)(i * 64 + lane);
+      if (s < count) {
+        const double ix = a.lut[3 * cw[i]], iy = a.lut[3 * cw[i] + 1], iz = a.lut[3 * cw[i] + 2];
+        const double perp = g0 * ix + g1 * iy + g2 * iz;
+        double p0 = 0.0, p1 = 0.0, p2 = 0.0;
+        const uint32_t e = ce[i], ee = e >> 24;
+        if (!((gs == 2u && perp < 0) || (gs == 1u && perp > 0)) && ee) {
+          const double inv = ldexp(1.0, (int)ee - 128 - 8), ap = fabs(perp);
+          p0 = (double)(e & 255u) * inv;
+          p1 = (double)((e >> 8) & 255u) * inv;
+          p2 = (double)((e >> 16) & 255u) * inv;
+          p0 *= ap; p1 *= ap; p2 *= ap;
+        }
+        tp[s] = p0;
+        tp[CAPC + s] = p1;
+        tp[2 * CAPC + s] = p2;
+      }
+    }
+    __syncthreads();
+    if (gi == g) {
+      constexpr int EB = 4;  // slots, then their terms, four photons per LDS round trip
+      for (int k0 = 0; k0 < num; k0 += EB) {
+        uint32_t sl[EB];
+#pragma unroll
+        for (int u = 0; u < EB; u++) sl[u] = slot_at(k0 + u < num ? k0 + u : k0);
+        double t[EB][3];
+#pragma unroll
+        for (int u = 0; u < EB; u++) {
+          t[u][0] = tp[sl[u]];
+          t[u][1] = tp[CAPC + sl[u]];
+          t[u][2] = tp[2 * CAPC + sl[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < EB; u++) {
+          if (k0 + u >= num) break;
+          o0 += t[u][0]; o1 += t[u][1]; o2 += t[u][2];
+        }
+      }
+    }
+  }
+  if (gi >= 0) {
+    const int K = a.K;
+    double maxd2 = (num < K) ? a.rmax * a.rmax : (double)km;
+    if (num == K && maxd2 < kEps) maxd2 = kEps;
+    o0 *= mt->kd[0]; o1 *= mt->kd[1]; o2 *= mt->kd[2];
+    if (maxd2 > 0) {
+      const double den = kPi * maxd2;
+      o0 /= den; o1 /= den; o2 /= den;
+      const QShade &sh = a.qshade[qi];
+      o0 *= sh.w[0]; o1 *= sh.w[1]; o2 *= sh.w[2];
+    } else {
+      o0 = o1 = o2 = 0.0;
+    }
+    a.out[3 * qi] = o0;
+    a.out[3 * qi + 1] = o1;
+    a.out[3 * qi + 2] = o2;
+    if (a.out_n) a.out_n[qi] = num;
+    if (a.out_maxd2) a.out_maxd2[qi] = (float)maxd2;
+  }
 }
 
 __device__ __forceinline__ void chunk_load_query(const KnnArgs &a, int64_t chunk, int lane, bool &valid,
@@ -752,10 +858,13 @@ void knn_chunk_lane_kernel(KnnArgs a) {
   // 240 candidates: 10,112 B of LDS per wave, so 16 waves (4 per SIMD, the VGPR limit) fit
   // in a CU's 160 KiB (256 candidates took 10,752 B: 14 waves)
   constexpr int CAPC = 240;
-  __shared__ float4 cpos_lds[CAPC];
-  const Cands<CAPC> cpos{reinterpret_cast<float *>(cpos_lds)};
-  __shared__ uint32_t cidx[CAPC];
-  __shared__ uint32_t crgbe[CAPC];
+  // candidates: x, y, z, w [4][CAPC], index, rgbe; the shared estimate's terms reuse the same
+  // 24 B per candidate ([3][CAPC] doubles, chunk_estimate_shared)
+  __shared__ __attribute__((aligned(16))) double cand_lds[3 * CAPC];
+  float *const cbase = reinterpret_cast<float *>(cand_lds);
+  const Cands<CAPC> cpos{cbase};
+  uint32_t *const cidx = reinterpret_cast<uint32_t *>(cbase + 4 * CAPC);
+  uint32_t *const crgbe = cidx + CAPC;
   __shared__ uint32_t stk[64];  // kd walk stack (walk_within)
   // kept LDS slots [s][lane] (K <= 64, u8) during the collect and the estimate; during the
   // counting passes the lanes' bin counters [w][lane] (u32, four u8 bins each), and during the
@@ -960,9 +1069,11 @@ void knn_chunk_lane_kernel(KnnArgs a) {
     }
     P.lap(2);
     // ---- 4. estimate
-    if (col && !(a.dbg & 2))
-      chunk_estimate(a, qi, qp, n, km, cpos, crgbe,
-                     [&](int s) { return (uint32_t)sel[s * 64 + lane]; });
+    if (!(a.dbg & 2)) {
+      auto slot_at = [&](int s) { return (uint32_t)sel[s * 64 + lane]; };
+      chunk_estimate_shared<CAPC>(a, lane, col, qi, qp, n, km, count, cpos, crgbe, cand_lds, slot_at,
+                                  [&]() { chunk_estimate(a, qi, qp, n, km, cpos, crgbe, slot_at); });
+    }
     if (col) {
       st_q += 1;
       st_found += (uint64_t)n;
@@ -992,10 +1103,11 @@ void knn_chunk_big_kernel(KnnArgs a) {
   constexpr int NW = CAPC / 32;
   // bracket list length: 8 keeps the 512-candidate kernel at 17.6 KB of LDS (9 waves per CU)
   constexpr int BRB = CAPC <= 512 ? 8 : LS_BR_B;
-  __shared__ float4 cpos_lds[CAPC];
-  const Cands<CAPC> cpos{reinterpret_cast<float *>(cpos_lds)};
-  __shared__ uint32_t cidx[CAPC];
-  __shared__ uint32_t crgbe[CAPC];
+  __shared__ __attribute__((aligned(16))) double cand_lds[3 * CAPC];  // as in the lane kernel
+  float *const cbase = reinterpret_cast<float *>(cand_lds);
+  const Cands<CAPC> cpos{cbase};
+  uint32_t *const cidx = reinterpret_cast<uint32_t *>(cbase + 4 * CAPC);
+  uint32_t *const crgbe = cidx + CAPC;
   __shared__ uint32_t hist[4];       // unused by the dk bound (chunk_bound_gather signature)
   __shared__ uint32_t stk[64];
   // kept-candidate bitmask [word][lane] during the collect and the estimate; during the counting
@@ -1173,9 +1285,9 @@ void knn_chunk_big_kernel(KnnArgs a) {
     }
     P.lap(2);
     // ---- estimate: the lane walks its bitmask in slot order
-    if (col) {
+    {
       uint32_t wi = 0, bits = selw[lane];
-      chunk_estimate(a, qi, qp, n, km, cpos, crgbe, [&](int) -> uint32_t {
+      auto slot_at = [&](int) -> uint32_t {
         while (!bits && wi + 1 < (uint32_t)NW) {
           wi++;
           bits = selw[wi * 64 + lane];
@@ -1184,7 +1296,11 @@ void knn_chunk_big_kernel(KnnArgs a) {
         uint32_t b = (uint32_t)__ffs(bits) - 1u;
         bits &= bits - 1u;
         return wi * 32u + b;
-      });
+      };
+      chunk_estimate_shared<CAPC>(a, lane, col, qi, qp, n, km, count, cpos, crgbe, cand_lds, slot_at,
+                                  [&]() { chunk_estimate(a, qi, qp, n, km, cpos, crgbe, slot_at); });
+    }
+    if (col) {
       st_q += 1;
       st_found += (uint64_t)n;
       st_vis += count;

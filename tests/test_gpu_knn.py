@@ -60,3 +60,20 @@ def test_estimate_radiance_matches_oracle(renderer, filt, k, r, spec):
     np.testing.assert_allclose(g, o, rtol=1e-10, atol=1e-300)
     p.filter_const_k = 1.0
     renderer.set_params(p)
+
+
+@pytest.mark.parametrize("scene,extra", [("cornell.scn", []), ("jensen.scn", ["-caustic", "400000"])])
+def test_shared_term_estimate_is_bit_identical(renderer, scene, extra, monkeypatch):
+    """chunk_estimate_shared (queries sharing a normal and side sum per-candidate terms computed
+    once per chunk) gives the per-lane estimate's f32 image bit for bit (GI_KNN_DBG & 256 turns
+    the sharing off)."""
+    import gpu_util
+    args = [gpu_util.scene(scene), "/tmp/sh.png", "-resolution", "48", "48", "-aa", "0",
+            "-global", "200000", "-caustic", "200000", "-it", "8", "-tt", "4", "-st", "4",
+            "-seed", "5"] + extra
+    monkeypatch.delenv("GI_KNN_DBG", raising=False)
+    _, f_shared, st, _ = gpu_util.run_gpu(renderer, args, want_float=True)
+    assert st["knn_queries"] > 0
+    monkeypatch.setenv("GI_KNN_DBG", "256")
+    _, f_lane, _, _ = gpu_util.run_gpu(renderer, args, want_float=True)
+    np.testing.assert_array_equal(f_shared, f_lane)

@@ -262,7 +262,9 @@ struct gi_ctx {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;  // caustic k-NN on the side stream
   bool overlap_mc = true;
-  bool overlap_maps = true;         // caustic k-NN on the side stream beside the global k-NN
+  bool overlap_maps = false;        // caustic k-NN on the side stream beside the global k-NN
+                                    // (GI_OVERLAP_MAPS=1; r02: equal frame time either way, and
+                                    // alone each map's kernels are timed without the other's)
   bool fork_after_sort = true;      // ... forked after the global queries' Morton sort (a radix
                                     // sort pass co-running with the caustic kernels stalled)
   MapExec mx[2];

@@ -240,10 +240,10 @@ struct ChunkProf {
 // collect every photon within a fixed bound). Returns the number of node records read.
 template <typename BoxD, typename Leaf>
 __device__ __forceinline__ uint32_t walk_within(const float *nodes, int L, float bound, uint32_t *stk,
-                                                BoxD boxd, Leaf leaf) {
+                                                BoxD boxd, Leaf leaf, int root = 1) {
   uint32_t reads = 1;
   int sp = 0;
-  int node = (boxd(ld_node(nodes, 1)) <= bound) ? 1 : 0;
+  int node = (boxd(ld_node(nodes, root)) <= bound) ? root : 0;
   while (node) {
     node = __builtin_amdgcn_readfirstlane(node);
     if (node < L) {
@@ -294,14 +294,21 @@ __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, b
   double U = a.rmax;
   G.dkc = -1.0;
   G.dkc_exact = false;
+  // the descent's splits, lane k holding depth k's (for the gather's subtree root below)
+  float path_split = 0.0f;
+  int path_axis = 0, depth = 0, cleaf = 1;
   if (N > 0 && K > 0) {
     int node = 1;
     while (node < L) {
       KdNode nd = ld_node(a.map.nodes, node);
-      float qa = kd_axis_q(__float_as_int(nd.hi.w), cx, cy, cz);
+      const int ax = __float_as_int(nd.hi.w);
+      if (lane == depth) { path_split = nd.lo.w; path_axis = ax; }
+      float qa = kd_axis_q(ax, cx, cy, cz);
       node = 2 * node + ((qa - nd.lo.w >= 0.0f) ? 1 : 0);
+      depth++;
       if (P.on) P.c[5]++;
     }
+    cleaf = node;
     int leaf = node - L;
     int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
     if (a.map.dk) {
@@ -386,6 +393,23 @@ __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, b
     }
   }
   const float U2 = __double2float_ru(U * U * (1.0 + 1e-5));
+  // Subtree root of the gather: the first node on c's descent whose split plane the region
+  // {x : |x - B| <= U} touches. Above it the region lies strictly on the descent's side of every
+  // split, so no photon of the region (a photon equal to a split may sit on either side, but
+  // none lies in the region) is outside that subtree; the walk starts there instead of at the
+  // root (saving two node reads per level above it). The test margin covers the fp32 metric.
+  int groot = 1;
+  if (N > 0 && K > 0 && depth <= 64) {
+    const double Ut = U * (1.0 + 1e-4) + 1e-6;
+    const float lo_ax = path_axis == 0 ? bl[0] : (path_axis == 1 ? bl[1] : bl[2]);
+    const float hi_ax = path_axis == 0 ? bh[0] : (path_axis == 1 ? bh[1] : bh[2]);
+    const bool touch = lane < depth && (double)lo_ax - Ut <= (double)path_split &&
+                       (double)hi_ax + Ut >= (double)path_split;
+    const uint64_t tm = __ballot(touch);
+    const int kr = tm ? __ffsll((long long)tm) - 1 : depth;
+    groot = cleaf >> (depth - kr);
+    if (a.dbg & 512) groot = 1;
+  }
   P.lap(0);
   // ---- 2. gather every photon within U of the chunk's box into LDS
   uint32_t count = 0;
@@ -422,7 +446,7 @@ __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, b
             count += nn;
           }
           return false;
-        });
+        }, groot);
     if (P.on) P.c[6] += rd;
   }
   // +inf positions after the last candidate, up to the next multiple of 8: the select loops

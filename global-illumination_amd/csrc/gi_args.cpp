@@ -3,7 +3,7 @@
 //   gi_params_default   defaults of photonmap.cpp:27-106
 //   gi_parse_args       ParseArgs, utils/io_utils.cpp:16-212 (same flags, clamps, messages;
 //                       extensions: -seed S, -gpus N)
-//   gi_write_image      R2Image::Write: .png (bottom-up rows, R2Image.cpp:1430) / .ppm
+//   (gi_write_image, R2Image::Write, is in gi_image.cpp)
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -157,56 +157,6 @@ int gi_parse_args(int argc, char **argv, gi_params *P, const char **scene, const
     if (err) *err = msg.c_str();
     return GI_ERR_STATE;
   }
-  return GI_OK;
-}
-
-int gi_write_image(const char *path, int w, int h, const uint8_t *rgb) {
-  if (!path || !rgb || w <= 0 || h <= 0) return GI_ERR_ARG;
-  const char *ext = strrchr(path, '.');
-  if (!ext) return GI_ERR_ARG;
-  FILE *fp = fopen(path, "wb");
-  if (!fp) return GI_ERR_IO;
-  if (!strcmp(ext, ".ppm")) {
-    fprintf(fp, "P6\n%d %d\n255\n", w, h);
-    for (int r = h - 1; r >= 0; r--) fwrite(rgb + (size_t)r * w * 3, 1, (size_t)w * 3, fp);
-    fclose(fp);
-    return GI_OK;
-  }
-  if (strcmp(ext, ".png")) { fclose(fp); return GI_ERR_UNSUPPORTED; }
-  auto be32 = [](uint8_t *p, uint32_t v) { p[0] = v >> 24; p[1] = v >> 16; p[2] = v >> 8; p[3] = v; };
-  auto chunk = [&](const char *type, const uint8_t *data, size_t n) {
-    uint8_t hd[8];
-    be32(hd, (uint32_t)n);
-    memcpy(hd + 4, type, 4);
-    fwrite(hd, 1, 8, fp);
-    if (n) fwrite(data, 1, n, fp);
-    uLong crc = crc32(0, (const Bytef *)type, 4);
-    if (n) crc = crc32(crc, data, (uInt)n);
-    uint8_t cb[4];
-    be32(cb, (uint32_t)crc);
-    fwrite(cb, 1, 4, fp);
-  };
-  const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
-  fwrite(sig, 1, 8, fp);
-  uint8_t ihdr[13] = {0};
-  be32(ihdr, w);
-  be32(ihdr + 4, h);
-  ihdr[8] = 8;
-  ihdr[9] = 2;
-  chunk("IHDR", ihdr, 13);
-  std::vector<uint8_t> raw;
-  raw.reserve((size_t)(w * 3 + 1) * h);
-  for (int r = 0; r < h; r++) {
-    raw.push_back(0);
-    const uint8_t *row = rgb + (size_t)(h - 1 - r) * w * 3;  // R2Image.cpp:1430 row flip
-    raw.insert(raw.end(), row, row + (size_t)w * 3);
-  }
-  uLongf zl = compressBound(raw.size());
-  std::vector<uint8_t> z(zl);
-  compress2(z.data(), &zl, raw.data(), raw.size(), 6);
-  chunk("IDAT", z.data(), zl);
-  chunk("IEND", nullptr, 0);
-  fclose(fp);
   return GI_OK;
 }
 

@@ -290,7 +290,10 @@ struct gi_ctx {
   double fb_ms[2] = {0, 0};       // fallback time and queries per map (since the last reset)
   uint64_t fb_q[2] = {0, 0};
   int last_kind[2] = {-1, -1};
-  bool knn_log = false;            // GI_KNN_LOG: one stderr line per chunk k-NN launch     // k-NN kind run_knn chose last, per map (gi_render_stats)
+  bool knn_log = false;            // GI_KNN_LOG: one stderr line per chunk k-NN launch
+  gi_progress_fn progress = nullptr;  // gi_set_progress
+  void *progress_user = nullptr;
+  int64_t progress_done = 0, progress_total = 0;  // output pixels of the current RenderImage     // k-NN kind run_knn chose last, per map (gi_render_stats)
   int sel_slack = 64;
   int knn_qpl = 1;
   int ind_waves = 3;              // indirect-path kernel occupancy target (waves per SIMD)
@@ -644,6 +647,7 @@ int trace_map(gi_ctx *c, int caustic, int64_t goal, const std::vector<double> &p
     }
     emitted += assigned;
     stored = (int64_t)map.size();
+    if (c->progress && goal > 0) c->progress(caustic ? 2 : 1, (double)stored / goal, c->progress_user);
     if (stored > 0 && emitted > 0) {
       rate = (double)stored / emitted;
       double frac = caustic ? (double)stored / goal : (double)stored / emitted;
@@ -1247,6 +1251,7 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     a.prim_rgb = c->prim_rgb.as<double>();
     launch_reduce(a, c->stream);
     HIPCHK(c, hipGetLastError());
+    if (c->progress) c->progress(0, (double)(p0 + npix) / (double)npix_total, c->progress_user);
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (rs) {
@@ -1455,6 +1460,13 @@ void gi_destroy(gi_ctx *c) {
 }
 
 const char *gi_last_error(const gi_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int gi_set_progress(gi_ctx *c, gi_progress_fn fn, void *user) {
+  if (!c) return GI_ERR_ARG;
+  c->progress = fn;  // device 0 reports for a device set (its share of the pixels)
+  c->progress_user = user;
+  return GI_OK;
+}
 
 int gi_set_params(gi_ctx *c, const gi_params *p) {
   if (!c || !p) return GI_ERR_ARG;

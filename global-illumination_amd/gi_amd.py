@@ -28,7 +28,7 @@ EXPORTED = [
     "gi_params_default", "gi_parse_args", "gi_create", "gi_create_devices", "gi_destroy",
     "gi_last_error",
     "gi_set_params", "gi_read_scene", "gi_scene_info", "gi_map_photons", "gi_set_photon_map",
-    "gi_get_photon_map", "gi_get_kd_tree", "gi_render_image", "gi_render_tiles", "gi_quantize",
+    "gi_get_photon_map", "gi_get_kd_tree", "gi_set_progress", "gi_render_image", "gi_render_tiles", "gi_quantize",
     "gi_estimate_radiance_batch", "gi_knn_batch", "gi_knn_bench", "gi_intersect_batch",
     "gi_write_image",
 ]

@@ -11,6 +11,29 @@
 #include <vector>
 #include "../../include/gi.h"
 
+// PrintProgress (io_utils.cpp:257-268) with the reference's bar width (photonmap.cpp:132);
+// a bar is redrawn when its percentage changes (render.cpp:82-86, photontracer.cpp:168-173)
+static const int PROGRESS_BAR_WIDTH = 50;
+static void PrintProgress(double progress, int width) {
+  printf("[");
+  int pos = (int)(width * progress);
+  for (int j = 0; j < width; j++) printf("%s", j < pos ? "=" : (j == pos ? ">" : " "));
+  printf("] %d%%\r", (int)(progress * 100.0));
+  fflush(stdout);
+}
+struct ProgressState {
+  bool verbose;
+  int last[3];
+};
+static void OnProgress(int stage, double progress, void *user) {
+  ProgressState *s = (ProgressState *)user;
+  if (stage > 0 && !s->verbose) return;  // photon-map bars only with -v (photonmap.cpp:193)
+  const int v = (int)(progress * 100.0);
+  if (v == s->last[stage]) return;
+  s->last[stage] = v;
+  PrintProgress(progress, PROGRESS_BAR_WIDTH);
+}
+
 int main(int argc, char **argv) {
   gi_params P;
   gi_params_default(&P);
@@ -50,6 +73,8 @@ int main(int argc, char **argv) {
     return -1;
   }
   gi_set_params(ctx, &P);
+  ProgressState prog = {P.verbose != 0, {-1, -1, -1}};
+  gi_set_progress(ctx, OnProgress, &prog);
   auto t0 = std::chrono::steady_clock::now();
   if (gi_read_scene(ctx, scene, real) != GI_OK) {
     fprintf(stderr, "%s\n", gi_last_error(ctx));
@@ -73,6 +98,7 @@ int main(int argc, char **argv) {
       gi_destroy(ctx);
       return -1;
     }
+    if (prog.last[1] >= 0 || prog.last[2] >= 0) printf("\n");  // photonmap.cpp:196
     if (P.verbose) {
       printf("Built photon map ...\n");
       printf("  Total Time = %.2f seconds\n", ps.total_s);
@@ -94,6 +120,9 @@ int main(int argc, char **argv) {
     gi_destroy(ctx);
     return -1;
   }
+  PrintProgress(1.0, PROGRESS_BAR_WIDTH);  // render.cpp:201-202
+  printf("\n");
+  fflush(stdout);
   if (P.verbose) {
     unsigned long long total = rs.screen_rays;
     printf("Rendered image ...\n");
@@ -111,7 +140,9 @@ int main(int argc, char **argv) {
   gi_destroy(ctx);
   auto tw = std::chrono::steady_clock::now();
   if (gi_write_image(out, w, h, rgb.data()) != GI_OK) {
-    fprintf(stderr, "Unable to write image %s\n", out);
+    const char *ext = strrchr(out, '.');
+    if (ext && !strncmp(ext, ".tif", 4)) fprintf(stderr, "TIFF not supported\n");  // R2Image.cpp:1300
+    else fprintf(stderr, "Unable to write image %s\n", out);
     return -1;
   }
   if (P.verbose) {

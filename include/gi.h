@@ -174,6 +174,12 @@ int gi_create_devices(gi_ctx **out, const gi_device_set *set);
 void gi_destroy(gi_ctx *ctx);
 const char *gi_last_error(const gi_ctx *ctx);
 int gi_set_params(gi_ctx *ctx, const gi_params *p);
+/* Progress reports (the reference's PrintProgress calls, io_utils.cpp:257-268): stage 0 =
+ * RenderImage, progress = output pixels done / total after each batch (render.cpp:80-87, 201);
+ * stage 1 / 2 = the global / caustic map's emission rounds, progress = stored / goal
+ * (photonmap.cpp:193-197, 244-248). Called on the thread that made the gi_ call; null = off. */
+typedef void (*gi_progress_fn)(int stage, double progress, void *user);
+int gi_set_progress(gi_ctx *ctx, gi_progress_fn fn, void *user);
 int gi_read_scene(gi_ctx *ctx, const char *path, int real_material);
 /* scene summary: nodes, lights, radius, ambient/background */
 int gi_scene_info(gi_ctx *ctx, int *nnodes, int *nlights, int *nprims, double *radius);

@@ -174,6 +174,28 @@ __device__ __forceinline__ bool ray_box(V o, V d, const double *mn, const double
   return false;
 }
 
+// Division-free pre-test of an element's box (R3SceneElement::Intersects, R3SceneElement.cpp:
+// 209-243, tests R3Contains(bbox, start) || R3Intersects(ray, bbox) with t <= closest). Slab
+// test of t in [-2e-6, maxt + 1e-5 + 1e-9 maxt] against the box grown by 1e-5 + 1e-9 |x|
+// (DElement::pmin/pmax), with inv = 1 / direction (+-inf on a zero component: the slab then
+// spans everything or nothing; a NaN from 0 * inf drops out of fmin/fmax). Every element the
+// exact test keeps passes: its hit point, or the ray origin when inside, lies within 1e-6 (the
+// RN_EPSILON tolerances of ray_box / box_contains) plus rounding of the box, at a parameter
+// within 1e-6 of [0, maxt]. A false here skips the exact test and its three divisions.
+__device__ __forceinline__ bool elem_maybe_hit(const DElement &el, V o, V inv, double maxt) {
+  double t0 = -2.0e-6, t1 = maxt + 1e-5 + 1e-9 * fabs(maxt);
+  double ta = (el.pmin[0] - o.x) * inv.x, tb = (el.pmax[0] - o.x) * inv.x;
+  t0 = fmax(t0, fmin(ta, tb));
+  t1 = fmin(t1, fmax(ta, tb));
+  ta = (el.pmin[1] - o.y) * inv.y; tb = (el.pmax[1] - o.y) * inv.y;
+  t0 = fmax(t0, fmin(ta, tb));
+  t1 = fmin(t1, fmax(ta, tb));
+  ta = (el.pmin[2] - o.z) * inv.z; tb = (el.pmax[2] - o.z) * inv.z;
+  t0 = fmax(t0, fmin(ta, tb));
+  t1 = fmin(t1, fmax(ta, tb));
+  return t0 <= t1;
+}
+
 // R3Intersects(ray, triangle) = plane (R3Isect.cpp:700-732) + R3Contains(triangle)
 // (R3Cont.cpp:491-512); edge planes precomputed on the host with the same arithmetic.
 // tmax: the caller's current closest t. A plane hit beyond it could not be taken by the caller
@@ -505,9 +527,11 @@ __device__ __forceinline__ bool scene_intersect(const SceneView &S, V org, V dir
       if (!isZero(lv - 1.0)) scale *= lv;
     }
     if (!ok) continue;
+    const V linv = mk(1.0 / ldir.x, 1.0 / ldir.y, 1.0 / ldir.z);
     for (int ei = 0; ei < nd.elem_count; ei++) {
       const DElement &el = S.elems[nd.elem_first + ei];
       double maxt = closest / scale;
+      if (!elem_maybe_hit(el, lo, linv, maxt)) continue;
       if (!box_contains(el.bmin, el.bmax, lo)) {
         double bt;
         if (!ray_box(lo, ldir, el.bmin, el.bmax, &bt, nullptr)) continue;

@@ -1580,6 +1580,11 @@ int gi_map_photons(gi_ctx *c, gi_photon_stats *st) {
     k.qpos = dq.as<float4>();
     k.out = dout.as<double>();
     k.stats = nullptr;
+    // Morton order, as for the render's queries: the chunk kernel's 64-query chunks are then
+    // spatial neighbourhoods (emission order scatters them over the scene)
+    uint32_t *iperm = nullptr;
+    HIPCHK(c, morton_order(dq.as<float4>(), n, c->sbmin, c->sbmax, c->mx[0].sorter, &iperm, c->stream));
+    k.perm = iperm;
     rc = run_knn(c, k, n, nullptr);
     if (rc) return rc;
     std::vector<double> irr(3 * n);

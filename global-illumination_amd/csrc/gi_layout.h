@@ -64,6 +64,10 @@ struct DElement {
   int32_t node;        // owning node
   int32_t shape_first, shape_count;
   double bmin[3], bmax[3];  // element bbox in node-local coordinates
+  // the bbox grown by 1e-5 + 1e-9 |x| per side: a division-free slab test against it rejects
+  // only elements R3Intersects(ray, box) + the t <= closest rule would reject too (gi_device.h
+  // elem_maybe_hit)
+  double pmin[3], pmax[3];
 };
 
 constexpr int GI_MAX_DEPTH = 16;  // scene-graph depth supported on the device

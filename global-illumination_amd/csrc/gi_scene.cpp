@@ -607,7 +607,13 @@ static Bx flatten(Graph &G, int gi_idx, int parent, HostScene &S) {
       eb.add(s.s.bmin);
       eb.add(s.s.bmax);
     }
-    for (int i = 0; i < 3; i++) { de.bmin[i] = eb.mn[i]; de.bmax[i] = eb.mx[i]; }
+    for (int i = 0; i < 3; i++) {
+      de.bmin[i] = eb.mn[i];
+      de.bmax[i] = eb.mx[i];
+      const double m = 1e-5 + 1e-9 * std::max(std::fabs(eb.mn[i]), std::fabs(eb.mx[i]));
+      de.pmin[i] = eb.mn[i] - m;  // an empty box (+inf, -inf) stays empty
+      de.pmax[i] = eb.mx[i] + m;
+    }
     S.elems.push_back(de);
     local.add(eb);
   }

@@ -29,6 +29,7 @@ static void OnProgress(int stage, double progress, void *user) {
   ProgressState *s = (ProgressState *)user;
   if (stage > 0 && !s->verbose) return;  // photon-map bars only with -v (photonmap.cpp:193)
   const int v = (int)(progress * 100.0);
+  if (stage == 0 && v >= 100) return;  // the final bar is printed after RenderImage returns
   if (v == s->last[stage]) return;
   s->last[stage] = v;
   PrintProgress(progress, PROGRESS_BAR_WIDTH);

@@ -118,6 +118,7 @@ struct SceneView {
   int32_t nnodes, nelems, nlights;
   uint32_t kinds;  // bit k set: the scene holds shapes of ShapeKind k
   int32_t hard_lights;  // every light is a point, spot or directional light
+  int32_t elem_pretest; // scene_intersect runs elem_maybe_hit before each element's box test
   double radius;
   double centroid[3];
   double ambient[3];
@@ -531,7 +532,7 @@ __device__ __forceinline__ bool scene_intersect(const SceneView &S, V org, V dir
     for (int ei = 0; ei < nd.elem_count; ei++) {
       const DElement &el = S.elems[nd.elem_first + ei];
       double maxt = closest / scale;
-      if (!elem_maybe_hit(el, lo, linv, maxt)) continue;
+      if (S.elem_pretest && !elem_maybe_hit(el, lo, linv, maxt)) continue;
       if (!box_contains(el.bmin, el.bmax, lo)) {
         double bt;
         if (!ray_box(lo, ldir, el.bmin, el.bmax, &bt, nullptr)) continue;

@@ -1074,25 +1074,32 @@ __global__ __launch_bounds__(64) void cached_kernel(KnnArgs a) {
   if (a.stats) wave_add(&a.stats[ST_KNN + a.stat_off], nq_done);
 }
 
-// CSR offsets of the key-sorted query list by primary sample: thread i fills seg[b] = i for
-// every primary b in (b(i-1), b(i)]; empty slots (key ~0) and i = n close the array.
+// CSR offsets of the key-sorted query list by primary sample: seg[b] = the first position whose
+// primary is >= b (empty slots, key ~0, count as primary nprim), b = 0 .. nprim. One thread per
+// primary, a binary search over the sorted keys: the Monte Carlo appends of a batch cluster on
+// the few rows through glass, and filling the gaps from the positions' side left one thread
+// writing every primary after the last append (27 ms in the r02 trace).
 __global__ void segments_kernel(const uint64_t *skeys, uint32_t n, uint32_t nprim, uint32_t *seg) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i > (int64_t)n) return;
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > (int64_t)nprim) return;
   auto prim_of = [&](int64_t k) -> int64_t {
     uint64_t key = skeys[k];
     if (key == ~0ull) return nprim;
-    uint64_t b = key >> 32;
-    return b < nprim ? (int64_t)b : (int64_t)nprim;
+    uint64_t p = key >> 32;
+    return p < nprim ? (int64_t)p : (int64_t)nprim;
   };
-  int64_t bi = (i < (int64_t)n) ? prim_of(i) : (int64_t)nprim;
-  int64_t bp = (i == 0) ? -1 : prim_of(i - 1);
-  for (int64_t b = bp + 1; b <= bi; b++) seg[b] = (uint32_t)i;
+  int64_t lo = 0, hi = n;  // first k in [0, n] with prim_of(k) >= b (prim_of(n) = nprim)
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (prim_of(mid) >= b) hi = mid;
+    else lo = mid + 1;
+  }
+  seg[b] = (uint32_t)lo;
 }
 
 void launch_segments(const uint64_t *skeys, uint32_t n, uint32_t nprim, uint32_t *seg,
                      hipStream_t st) {
-  segments_kernel<<<(unsigned)(((int64_t)n + 1 + 255) / 256), 256, 0, st>>>(skeys, n, nprim, seg);
+  segments_kernel<<<(unsigned)(((int64_t)nprim + 1 + 255) / 256), 256, 0, st>>>(skeys, n, nprim, seg);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -191,3 +191,24 @@ def test_indirect_continuation_queue_is_exact(name, extra):
                   "specular_samples", "indirect_samples", "caustic_samples", "knn_queries"):
             assert out[0][1][k] == other[1][k], k
     assert out[1][1]["transmissive_samples"] > 0
+
+
+@pytest.mark.parametrize("scene", ["cornell.scn", "jensen.scn", "stilllife.scn", "transform.scn"])
+def test_element_pretest_is_exact(scene, monkeypatch):
+    """scene_intersect's division-free element box pre-test (elem_maybe_hit) only skips elements
+    the reference's box test would skip: renders with it forced on and off are identical."""
+    import gi_amd
+    import gpu_util
+    args = [gpu_util.scene(scene), "/tmp/pt.png", "-resolution", "40", "32", "-aa", "0",
+            "-global", "30000", "-caustic", "30000", "-it", "4", "-tt", "4", "-st", "4",
+            "-seed", "9"]
+    out = []
+    for v in ("1", "0"):
+        monkeypatch.setenv("GI_ELEM_PRETEST", v)
+        r = gi_amd.Renderer(0)
+        try:
+            _, f, _, _ = gpu_util.run_gpu(r, args, want_float=True)
+        finally:
+            r.close()
+        out.append(f)
+    np.testing.assert_array_equal(out[0], out[1])

@@ -308,6 +308,7 @@ struct gi_ctx {
   DBuf spawn, npaths, path_off, nmc, mc_off, nind, ind_off, base, pixels, rgbf, rgb8, qcount, stats_bak;
   DBuf qpos[2], qshade[2], qkey[2], qout[2];
   bool chunk_big2 = true;            // large-K chunk k-NN: second chunk pass (1024 candidates)
+  bool chunk_lane2 = true;           // lane-select chunk k-NN: second pass (480, GI_CHUNK_LANE2)
   int chunk_minsub_big2 = 64;        // ... its overflowing chunks retried down to this group size
   bool chunk_dk = true;            // chunk kernel (K <= 64): centre bound from the dk bounds (measured: fewer fallbacks)
   bool chunk_fb_all = false;       // test knob: the lane-select chunk kernel hands every query to its fallback
@@ -879,10 +880,37 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
     HIPCHK(c, hipMemcpyAsync(&nfb, dense + nq, 4, hipMemcpyDeviceToHost, X.st));
     HIPCHK(c, hipStreamSynchronize(X.st));
     X.fb_total += nfb;
-    if (nfb) {
+    uint32_t nfb2 = nfb;
+    if (nfb && c->chunk_lane2 && !c->chunk_fb_all) {
+      // second chunk pass, 480 LDS candidates, over the overflowing chunks' queries (the
+      // compacted list keeps each chunk's queries together, in Morton order)
+      int64_t chunks2 = ((int64_t)nfb + 63) / 64;
+      int64_t grid2 = knn_chunk_grid(nfb);
+      uint32_t cap2 = (uint32_t)(64 * ((chunks2 + grid2 - 1) / grid2) * ((grid2 + FB_QS - 1) / FB_QS));
+      HIPCHK(c, X.fb_list2.ensure((size_t)FB_QS * cap2 * 4));
+      HIPCHK(c, X.fb_dense2.ensure((size_t)nfb * 4 + 4));
+      HIPCHK(c, X.fb_count2.ensure(FB_QS * 32 * 4));
+      HIPCHK(c, hipMemsetAsync(X.fb_count2.p, 0, FB_QS * 32 * 4, X.st));
+      KnnArgs s2 = k;
+      s2.perm = dense;
+      s2.nq = nfb;
+      s2.q0 = 0;
+      s2.fb_list = X.fb_list2.as<uint32_t>();
+      s2.fb_count = X.fb_count2.as<uint32_t>();
+      s2.fb_cap_s = cap2;
+      s2.dbg &= ~16;
+      launch_knn_chunk2(s2, X.st);
+      HIPCHK(c, hipGetLastError());
+      dense = X.fb_dense2.as<uint32_t>();
+      launch_fb_compact(s2.fb_list, s2.fb_count, cap2, dense, dense + nfb, X.st);
+      HIPCHK(c, hipGetLastError());
+      HIPCHK(c, hipMemcpyAsync(&nfb2, dense + nfb, 4, hipMemcpyDeviceToHost, X.st));
+      HIPCHK(c, hipStreamSynchronize(X.st));
+    }
+    if (nfb2) {
       KnnArgs f = k;
       f.perm = dense;
-      f.nq = nfb;
+      f.nq = nfb2;
       f.q0 = 0;
       f.map.dk = fb_dk;
       launch_knn_lane(f, X.st);
@@ -899,8 +927,8 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
       c->fb_ms[mi] += tf;
       c->fb_q[mi] += nfb;
       if (c->knn_log)
-        fprintf(stderr, "[gi] knn map %d kind 7: nq %lld chunk %.2f ms, fallback %u in %.2f ms\n", mi,
-                (long long)nq, t - tf, nfb, tf);
+        fprintf(stderr, "[gi] knn map %d kind 7: nq %lld chunk %.2f ms, second pass %u, per-lane %u, fallback %.2f ms\n",
+                mi, (long long)nq, t - tf, nfb, nfb2, tf);
     }
     return GI_OK;
   }
@@ -1366,6 +1394,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_KNN_DK")) c->use_dk = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_DK")) c->chunk_dk = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_BIG2")) c->chunk_big2 = atoi(s) != 0;
+  if (const char *s = getenv("GI_CHUNK_LANE2")) c->chunk_lane2 = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_MINSUB_BIG2")) c->chunk_minsub_big2 = std::min(64, std::max(1, atoi(s)));
   if (const char *s = getenv("GI_OVERLAP_MC")) c->overlap_mc = atoi(s) != 0;
   if (const char *s = getenv("GI_OVERLAP_MAPS")) c->overlap_maps = atoi(s) != 0;

@@ -330,6 +330,7 @@ void launch_knn(const KnnArgs &a, hipStream_t st);
 bool launch_knn_wave(const KnnArgs &a, int cap_mul, hipStream_t st);
 bool launch_knn_lane(const KnnArgs &a, hipStream_t st);
 bool launch_knn_chunk(const KnnArgs &a, hipStream_t st);  // K <= 64, lane select
+bool launch_knn_chunk2(const KnnArgs &a, hipStream_t st);  // its 480-candidate second pass
 bool launch_knn_chunk_big(const KnnArgs &a, int cap, hipStream_t st);  // K > 64, needs a.map.dk
 // blocks of the chunk kernels (one 64-query chunk each, grid-stride)
 unsigned knn_chunk_grid(int64_t nq);

@@ -876,12 +876,15 @@ __device__ __forceinline__ bool in_bracket(float d2, uint32_t ab, uint32_t span)
 __device__ __forceinline__ float next_up(float x) { return __uint_as_float(__float_as_uint(x) + 1u); }
 __device__ __forceinline__ float next_down(float x) { return __uint_as_float(__float_as_uint(x) - 1u); }
 
-template <int WPE, bool PROF>
+// CAPC = 240 (first pass): 10,112 B of LDS per wave, so 16 waves (4 per SIMD, the VGPR limit)
+// fit in a CU's 160 KiB (256 candidates took 10,752 B: 14 waves); u8 slots and u8 counters.
+// CAPC = 480 (second pass over the first's overflowing chunks): u16 slots and counters, 19.8 KB.
+template <int WPE, bool PROF, int CAPC = 240>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE)))
 void knn_chunk_lane_kernel(KnnArgs a) {
-  // 240 candidates: 10,112 B of LDS per wave, so 16 waves (4 per SIMD, the VGPR limit) fit
-  // in a CU's 160 KiB (256 candidates took 10,752 B: 14 waves)
-  constexpr int CAPC = 240;
+  using SlotT = typename std::conditional<(CAPC < 256), uint8_t, uint16_t>::type;
+  constexpr int SB = sizeof(SlotT);      // bytes per slot and per bin counter
+  constexpr int NWC = LS_NB * SB / 4;    // counter words per lane (64 bins)
   // candidates: x, y, z, w [4][CAPC], index, rgbe; the shared estimate's terms reuse the same
   // 24 B per candidate ([3][CAPC] doubles, chunk_estimate_shared)
   __shared__ __attribute__((aligned(16))) double cand_lds[3 * CAPC];
@@ -893,8 +896,8 @@ void knn_chunk_lane_kernel(KnnArgs a) {
   // kept LDS slots [s][lane] (K <= 64, u8) during the collect and the estimate; during the
   // counting passes the lanes' bin counters [w][lane] (u32, four u8 bins each), and during the
   // bound phase the centre select's 256-bin histogram
-  __shared__ uint32_t selh[16 * 64];
-  uint8_t *sel = reinterpret_cast<uint8_t *>(selh);
+  __shared__ uint32_t selh[16 * SB * 64];
+  SlotT *sel = reinterpret_cast<SlotT *>(selh);
   uint32_t *hist = selh;
   const int lane = threadIdx.x;
   const int K = a.K;
@@ -960,33 +963,35 @@ void knn_chunk_lane_kernel(KnnArgs a) {
         // LS_NB = 64 bins per lane: u8 counters packed four per LDS word [w][lane] (w = bin / 4;
         // conflict-free, one ds_add per candidate; at most 255 members, so no byte carries)
 #pragma unroll
-        for (int w = 0; w < 16; w++) selh[w * 64 + lane] = 0u;
+        for (int w = 0; w < NWC; w++) selh[w * 64 + lane] = 0u;
         // groups of 8 candidates: the group's (broadcast) LDS reads are issued together and the
         // loop body has no branches (non-members, and the +inf padding past `count`, add 0)
+        constexpr uint32_t PERW = 4 / SB;  // counters per word
         for (uint32_t s0 = 0; s0 < count; s0 += 8) {
           float dg[8];
           cand_d2x8(cpos, s0, qx, qy, qz, dg);
 #pragma unroll
           for (int u = 0; u < 8; u++) {
             const uint32_t b = binN<LS_NB>(dg[u], sc, off);
-            const uint32_t inc = in_bracket(dg[u], ab, span) ? (1u << ((b & 3u) << 3)) : 0u;
-            atomicAdd(&selh[(b >> 2) * 64 + lane], inc);
+            const uint32_t inc = in_bracket(dg[u], ab, span) ? (1u << ((b & (PERW - 1u)) * 8u * SB)) : 0u;
+            atomicAdd(&selh[(b / PERW) * 64 + lane], inc);
           }
         }
         if (on) {
-          // the K-th key's bin: word sums first (sum of four bytes), bytes inside the word
+          // the K-th key's bin: word sums first, counters inside the word
           uint32_t before = 0, bs = LS_NB, cb = 0;
+          constexpr uint32_t CM = SB == 1 ? 255u : 65535u;
 #pragma unroll
-          for (int w = 0; w < 16; w++) {
+          for (int w = 0; w < NWC; w++) {
             const uint32_t c4 = selh[w * 64 + lane];
-            const uint32_t ws = __builtin_amdgcn_sad_u8(c4, 0u, 0u);
+            const uint32_t ws = SB == 1 ? __builtin_amdgcn_sad_u8(c4, 0u, 0u) : (c4 & 65535u) + (c4 >> 16);
             if (bs == LS_NB) {
               if (before + ws >= (uint32_t)need) {
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                  const uint32_t c = (c4 >> (8 * j)) & 255u;
+                for (int j = 0; j < (int)PERW; j++) {
+                  const uint32_t c = (c4 >> (8 * SB * j)) & CM;
                   if (bs == LS_NB) {
-                    if (before + c >= (uint32_t)need) { bs = (uint32_t)(4 * w + j); cb = c; }
+                    if (before + c >= (uint32_t)need) { bs = (uint32_t)(PERW * w + j); cb = c; }
                     else before += c;
                   }
                 }
@@ -1053,8 +1058,8 @@ void knn_chunk_lane_kernel(KnnArgs a) {
         const bool kb = in_bracket(d2, ab, span);
         // (a lane without a bracket may fill all 64 entries: its bracket store goes to n too,
         // before the front store of the same value)
-        sel[(inb_on ? bm : n) * 64 + lane] = (uint8_t)s;
-        sel[n * 64 + lane] = (uint8_t)s;
+        sel[(inb_on ? bm : n) * 64 + lane] = (SlotT)s;
+        sel[n * 64 + lane] = (SlotT)s;
         n += kf ? 1 : 0;
         bm -= kb ? 1 : 0;
         km = fmaxf(km, kf ? d2 : 0.0f);
@@ -1086,7 +1091,7 @@ void knn_chunk_lane_kernel(KnnArgs a) {
 #pragma unroll
       for (int i = 0; i < LS_BR_L; i++)
         if (i < need) {
-          sel[n * 64 + lane] = (uint8_t)sl[i];
+          sel[n * 64 + lane] = (SlotT)sl[i];
           n++;
           km = fmaxf(km, __uint_as_float((uint32_t)(fk[i] >> 32)));
         }
@@ -1379,6 +1384,15 @@ bool launch_knn_chunk_big(const KnnArgs &a, int cap, hipStream_t st) {
     // second pass over the first pass's overflowing chunks: 32 KiB of LDS per wave
     knn_chunk_big_kernel<1024, false><<<grid, 64, 0, st>>>(a);
   }
+  return true;
+}
+
+// second lane-select pass (K <= 64) over the first pass's overflowing chunks' queries: 480 LDS
+// candidates, u16 slots and counters
+bool launch_knn_chunk2(const KnnArgs &a, hipStream_t st) {
+  if (a.nq == 0) return true;
+  if (a.mode == KNN_MODE_LIST || a.K > 64) return false;
+  knn_chunk_lane_kernel<2, false, 480><<<knn_chunk_grid(a.nq), 64, 0, st>>>(a);
   return true;
 }
 

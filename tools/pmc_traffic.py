@@ -23,12 +23,13 @@ import sys
 def main():
     path, knames = sys.argv[1], sys.argv[2].split(",")
     res, aa, glob, caus = (int(x) for x in sys.argv[3:7])
-    nq = None
+    nq = launches = None
     if len(sys.argv) > 7:
         for line in open(sys.argv[7]):
             if line.startswith("{"):
                 g = json.loads(line)["roofline"]["global"]
                 nq = g["queries_per_launch"] * g["launches"]
+                launches = g["launches"]
     rows = list(csv.DictReader(open(path)))
     kib, ndisp, kib_all = 0.0, {}, 0.0
     for kname in knames:
@@ -44,7 +45,8 @@ def main():
         ndisp[kname] = len(per)
     out = {"kernel": " + ".join(knames), "dispatches": ndisp, "fetch_size_kib_per_launch": kib,
            "correction": "x2 (gfx950 FETCH_SIZE = 1/2 of bytes read, MI355X_MICROARCH.md) x1024",
-           "bytes_per_launch": kib * 1024 * 2,
+           # one launch = the whole sequence (chunk passes + per-lane fallback) of one batch
+           "bytes_per_launch": kib_all * 1024 * 2 / launches if launches else kib * 1024 * 2,
            "workload": {"res": res, "aa": aa, "global": glob, "caustic": caus},
            "queries": nq,
            "bytes_per_query": kib_all * 1024 * 2 / nq if nq else None,

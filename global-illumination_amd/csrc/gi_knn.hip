@@ -323,8 +323,11 @@ __device__ __forceinline__ void wave_estimate(const KnnArgs &a, int64_t qi, floa
   }
 }
 
+#ifndef WAVE_WPE
+#define WAVE_WPE 6  // fused query-per-wave kernel: occupancy target (80 VGPRs)
+#endif
 template <int CAP, int LB, bool PROF, bool FUSE>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FUSE ? 6 : 1)))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FUSE ? WAVE_WPE : 1)))
 void knn_wave_kernel(KnnArgs a) {
   __shared__ uint64_t buf[CAP];
   __shared__ uint32_t hist[256];
@@ -873,12 +876,15 @@ void launch_list_estimate(const KnnArgs &a, hipStream_t st) {
   knn_list_estimate_kernel<<<(unsigned)grid, 64, 0, st>>>(a);
 }
 
+#ifndef WAVE_LB
+#define WAVE_LB 1  // leaf batches of 64 photons loaded together by the 512/1024 instances
+#endif
 template <bool PROF, bool FUSE>
 bool wave_launch(const KnnArgs &a, int need, unsigned grid, hipStream_t st) {
   if (need <= 128) knn_wave_kernel<128, 1, PROF, FUSE><<<grid, 64, 0, st>>>(a);
   else if (need <= 256) knn_wave_kernel<256, 1, PROF, FUSE><<<grid, 64, 0, st>>>(a);
-  else if (need <= 512) knn_wave_kernel<512, 1, PROF, FUSE><<<grid, 64, 0, st>>>(a);
-  else if (need <= 1024) knn_wave_kernel<1024, 1, PROF, FUSE><<<grid, 64, 0, st>>>(a);
+  else if (need <= 512) knn_wave_kernel<512, WAVE_LB, PROF, FUSE><<<grid, 64, 0, st>>>(a);
+  else if (need <= 1024) knn_wave_kernel<1024, WAVE_LB, PROF, FUSE><<<grid, 64, 0, st>>>(a);
   else return false;
   return true;
 }

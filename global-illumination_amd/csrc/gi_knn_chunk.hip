@@ -238,6 +238,16 @@ struct ChunkProf {
 // (scalar loads, ld_node) and pushes one, so backtracking reads nothing from memory. leaf(l)
 // returns true to stop the walk. The visiting order does not matter to the callers (they
 // collect every photon within a fixed bound). Returns the number of node records read.
+//
+// WALK2: an expansion whose children are internal also reads the four grandchildren (128
+// contiguous bytes, issued with the children's 64): two levels per dependent round trip. A
+// grandchild is taken when its parent and its own box pass, as two single-level expansions
+// would take it, and the in-grandchildren are pushed right to left, so leaves are still visited
+// left to right: the callers' LDS candidate order, and so every estimate sum, is unchanged.
+// Stack: at most three entries per two levels.
+#ifndef WALK2
+#define WALK2 1
+#endif
 template <typename BoxD, typename Leaf>
 __device__ __forceinline__ uint32_t walk_within(const float *nodes, int L, float bound, uint32_t *stk,
                                                 BoxD boxd, Leaf leaf, int root = 1) {
@@ -247,15 +257,31 @@ __device__ __forceinline__ uint32_t walk_within(const float *nodes, int L, float
   while (node) {
     node = __builtin_amdgcn_readfirstlane(node);
     if (node < L) {
-      KdNode c0 = ld_node(nodes, 2 * node), c1 = ld_node(nodes, 2 * node + 1);
-      reads += 2;
-      bool in0 = boxd(c0) <= bound, in1 = boxd(c1) <= bound;
-      if (in0 && in1) {
-        stk[sp] = (uint32_t)(2 * node + 1);  // every lane stores the same value
-        sp++;
+      const int c = 2 * node;
+      KdNode c0 = ld_node(nodes, c), c1 = ld_node(nodes, c + 1);
+      if (WALK2 && c < L) {
+        KdNode g0 = ld_node(nodes, 2 * c), g1 = ld_node(nodes, 2 * c + 1);
+        KdNode g2 = ld_node(nodes, 2 * c + 2), g3 = ld_node(nodes, 2 * c + 3);
+        reads += 6;
+        const bool in0 = boxd(c0) <= bound, in1 = boxd(c1) <= bound;
+        const bool i0 = in0 && boxd(g0) <= bound, i1 = in0 && boxd(g1) <= bound;
+        const bool i2 = in1 && boxd(g2) <= bound, i3 = in1 && boxd(g3) <= bound;
+        const int nxt = i0 ? 2 * c : (i1 ? 2 * c + 1 : (i2 ? 2 * c + 2 : (i3 ? 2 * c + 3 : 0)));
+        // every lane stores the same values
+        if (i3 && nxt != 2 * c + 3) stk[sp++] = (uint32_t)(2 * c + 3);
+        if (i2 && nxt != 2 * c + 2) stk[sp++] = (uint32_t)(2 * c + 2);
+        if (i1 && nxt != 2 * c + 1) stk[sp++] = (uint32_t)(2 * c + 1);
+        if (nxt) { node = nxt; continue; }
+      } else {
+        reads += 2;
+        bool in0 = boxd(c0) <= bound, in1 = boxd(c1) <= bound;
+        if (in0 && in1) {
+          stk[sp] = (uint32_t)(c + 1);  // every lane stores the same value
+          sp++;
+        }
+        if (in0) { node = c; continue; }
+        if (in1) { node = c + 1; continue; }
       }
-      if (in0) { node = 2 * node; continue; }
-      if (in1) { node = 2 * node + 1; continue; }
     } else if (leaf(node - L)) {
       return reads;
     }
@@ -300,13 +326,24 @@ __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, b
   if (N > 0 && K > 0) {
     int node = 1;
     while (node < L) {
-      KdNode nd = ld_node(a.map.nodes, node);
+      // (WALK2) the node's children are read with it: two levels per round trip
+      KdNode nd = ld_node(a.map.nodes, node), k0, k1;
+      const bool two = WALK2 && 2 * node < L;
+      if (two) { k0 = ld_node(a.map.nodes, 2 * node); k1 = ld_node(a.map.nodes, 2 * node + 1); }
       const int ax = __float_as_int(nd.hi.w);
       if (lane == depth) { path_split = nd.lo.w; path_axis = ax; }
       float qa = kd_axis_q(ax, cx, cy, cz);
       node = 2 * node + ((qa - nd.lo.w >= 0.0f) ? 1 : 0);
       depth++;
       if (P.on) P.c[5]++;
+      if (two) {
+        const KdNode &kn = (node & 1) ? k1 : k0;
+        const int kax = __float_as_int(kn.hi.w);
+        if (lane == depth) { path_split = kn.lo.w; path_axis = kax; }
+        float ka = kd_axis_q(kax, cx, cy, cz);
+        node = 2 * node + ((ka - kn.lo.w >= 0.0f) ? 1 : 0);
+        depth++;
+      }
     }
     cleaf = node;
     int leaf = node - L;

@@ -3,17 +3,24 @@
 photons (BASELINE.json configs[1] = SURVEY.md C2).
 
 A step = one full frame (RenderImage, render.cpp:155-259) over the resident scene and photon
-maps. With N ranks (torchrun, one process per GPU) the frame's 16x16-pixel tiles are dealt
-round-robin (tile % N, the reference's column interleave render.cpp:90 re-cut as tiles); each
-rank renders its tiles and sends only its own packed pixels to rank 0 in one RCCL gather over
-xGMI (gi_dist.py). Total work per step is fixed -> "scaling": "strong".
-The photon maps are built once per rank from the same seed (identical, no communication) and
+maps. The frame's 16x16-pixel output tiles are dealt round-robin over the GPUs (tile % N, the
+reference's column interleave render.cpp:90 re-cut as tiles); total work per step is fixed ->
+"scaling": "strong". Two ways to run N GPUs:
+- torchrun (WORLD_SIZE set; the driver's N>1 launch): one process per GPU. Each rank renders its
+  tiles into a packed device buffer (gi_render_tiles_packed) and rank 0 gathers the packed
+  buffers over RCCL/xGMI (one gather, 1/N of the frame per rank) and composes the frame on its
+  GPU (gi_dist.py).
+- `--gpus N` without WORLD_SIZE: the drop-in's own device set in one process (gi_create_devices,
+  render.cpp:188-199's thread fork re-cut as devices): one host thread per device, ncclSend /
+  ncclRecv tile gather onto device 0. GI_DEVICES="0,0" names the devices explicitly (tests).
+The photon maps are built once (per rank, from the same seed: identical, no communication) and
 their build time is reported separately (photon_map_s), as SURVEY.md §8(d) prescribes.
 
 Extra JSON fields: roofline (k-NN radiance kernel, algorithmic bytes = 16 B per photon
 returned), cpu_baseline (the oracle/ C++ restatement on this host's cores).
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -45,7 +52,8 @@ def parse():
     ap.add_argument("--scene", default="cornell.scn", help="scene under tests/scenes (C2: cornell)")
     ap.add_argument("--extra", default="", help="extra reference flags, e.g. '-dof 4 12.2 0.025'")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-res", type=int, default=16, help="CPU baseline sample: res x res px")
+    ap.add_argument("--cpu-res", type=int, default=32,
+                    help="CPU baseline sample: res x res px at the same aa (BASELINE.md section 3)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     return ap.parse_args()
 
@@ -93,22 +101,56 @@ def load_traffic(a, qpl):
     return bpq * qpl  # the PMC pass's bytes per query, at this run's launch size
 
 
+def host_threads():
+    """CPU threads this process may use: its affinity set, capped by a cgroup CPU quota and by
+    the host's declared CPU share (OMP_NUM_THREADS, set on the GPU boxes) when those are set (a
+    container can see more CPUs than it may run)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return n
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(a):
     """Oracle restatement (port) of the reference path timed on this host: same scene, flags
     and photon counts, on a res x res pixel sample of the same image plane (uniform sub-grid,
     identical per-sample workload)."""
     import oracle_lib
-    threads = a.cpu_threads or min(16, os.cpu_count() or 1)
+    threads = a.cpu_threads or host_threads()
     args = [os.path.join(SCENES, a.scene), "/tmp/cpu.png", "-resolution", str(a.cpu_res),
             str(a.cpu_res), "-aa", str(a.aa), "-global", str(a.global_photons), "-caustic",
             str(a.caustic_photons), "-threads", str(threads), "-seed", str(a.seed)] + a.extra.split()
     _, st = oracle_lib.render(args, a.cpu_res, a.cpu_res)
-    samples = a.cpu_res * a.cpu_res * 4 ** a.aa
+    dof = 1
+    ex = a.extra.split()
+    if "-dof" in ex:
+        dof = max(1, int(ex[ex.index("-dof") + 1]))
+    samples = a.cpu_res * a.cpu_res * 4 ** a.aa * dof
     value = samples / st["render_s"] / 1e6
-    full = a.res * a.res * 4 ** a.aa
+    full = a.res * a.res * 4 ** a.aa * dof
     ratio = CPU_CALIBRATION["ratio"] if a.scene == "cornell.scn" else None
     return {"value": value, "unit": "Mpixel-samples/s",
-            "cores": threads, "kind": "port",
+            "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+            "host_cpus_visible": os.cpu_count(),
             "sample": f"{a.scene} {a.cpu_res}x{a.cpu_res} aa={a.aa} ({samples} pixel-samples), "
                       f"{a.global_photons}+{a.caustic_photons} photons; render {st['render_s']:.2f} s, "
                       f"photon map {st['trace_s'] + st['kd_s']:.2f} s on {threads} threads",
@@ -118,39 +160,69 @@ def cpu_baseline(a):
             "calibration": CPU_CALIBRATION if ratio else None}
 
 
+def device_list(n):
+    """Devices of the single-process device set: GI_DEVICES (e.g. "0,0") or 0..n-1."""
+    env = os.environ.get("GI_DEVICES")
+    if env:
+        return [int(x) for x in env.split(",") if x.strip()]
+    return list(range(n))
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    devices = None
     if world > 1:
         import torch
         import torch.distributed as dist
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
+        # GI_BENCH_SAME_GPU=1 maps every rank onto GPU 0 and GI_BENCH_BACKEND=gloo carries the
+        # gather through host memory (tests on a one-GPU box; RCCL needs distinct GPUs)
+        if os.environ.get("GI_BENCH_SAME_GPU") == "1":
+            local = 0
+        backend = os.environ.get("GI_BENCH_BACKEND") or (
+            "nccl" if torch.cuda.is_available() else "gloo")
+        if torch.cuda.is_available():
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
+        n_gpus = world
+        mode = "torchrun"
+    elif a.gpus > 1 or os.environ.get("GI_DEVICES"):
+        devices = device_list(a.gpus)
+        n_gpus = len(devices)
+        mode = "device-set"
+    else:
+        n_gpus = 1
+        mode = "single"
     import gi_amd
 
     args = [os.path.join(SCENES, a.scene), "/tmp/bench.png", "-resolution", str(a.res),
             str(a.res), "-aa", str(a.aa), "-global", str(a.global_photons), "-caustic",
             str(a.caustic_photons), "-seed", str(a.seed)] + a.extra.split()
     p, sc, _o, w, h, aa, real = gi_amd.ParseArgs(args)
-    r = gi_amd.Renderer(local, p)
+    r = gi_amd.Renderer(local, p, devices=devices)
     r.ReadScene(sc, real)
     t0 = time.perf_counter()
     pst = r.MapPhotons()
     photon_s = time.perf_counter() - t0
 
+    dev = None
+    if world > 1:
+        import torch
+        dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+    last = {}
+
     def step():
         if world == 1:
             rgb, st = r.RenderImage(aa, w, h)
+            last["rgb"] = rgb
             return st
-        import torch
         import gi_dist
-        dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
-        _img, st = gi_dist.render_sharded(r, aa, w, h, a.tile, rank, world, dist, dev)
+        img, st = gi_dist.render_sharded(r, aa, w, h, a.tile, rank, world, dist, dev)
+        if img is not None:
+            last["rgb"] = img[0] if isinstance(img, tuple) else None
         return st
 
     def barrier():
@@ -168,7 +240,7 @@ def main():
     barrier()
     t0 = time.perf_counter()
     keys = ("q0", "q1", "ph0", "ph1", "vis0", "vis1", "ms0", "ms1", "n0", "n1", "fb0", "fb1",
-            "fbq0", "fbq1")
+            "fbq0", "fbq1", "p2ms0", "p2ms1", "p2q0", "p2q1", "devmax", "devmin", "gather")
     agg = dict.fromkeys(keys, 0.0)
     kind = [-1, -1]
     for _ in range(a.steps):
@@ -182,15 +254,20 @@ def main():
             agg[f"n{m}"] += st["knn_map_launches"][m]
             agg[f"fb{m}"] += st["knn_map_fallback_ms"][m]
             agg[f"fbq{m}"] += st["knn_map_fallback_queries"][m]
+            agg[f"p2ms{m}"] += st["knn_map_pass2_ms"][m]
+            agg[f"p2q{m}"] += st["knn_map_pass2_queries"][m]
+        agg["devmax"] += st["device_render_s_max"]
+        agg["devmin"] += st["device_render_s_min"]
+        agg["gather"] += st["gather_s"]
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
         import torch
-        dev = "cuda" if torch.cuda.is_available() else "cpu"
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dv = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dv)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-        ag = torch.tensor([agg[k] for k in keys], dtype=torch.float64, device=dev)
+        ag = torch.tensor([agg[k] for k in keys], dtype=torch.float64, device=dv)
         dist.all_reduce(ag)  # sums over ranks (kernel ms summed over GPUs)
         agg = dict(zip(keys, [float(x) for x in ag.tolist()]))
     samples_per_frame = w * h * 4 ** aa * p.dof_test
@@ -213,9 +290,11 @@ def main():
                     "queries_per_launch": agg[f"q{m}"] / launches,
                     "photons_per_query": photons / max(1.0, agg[f"q{m}"]),
                     "visited_per_query": agg[f"vis{m}"] / max(1.0, agg[f"q{m}"]),
+                    "second_pass_avg_ms": round(agg[f"p2ms{m}"] / launches, 3),
+                    "second_pass_query_frac": round(agg[f"p2q{m}"] / max(1.0, agg[f"q{m}"]), 4),
                     "fallback_avg_ms": round(agg[f"fb{m}"] / launches, 3),
                     "fallback_query_frac": round(agg[f"fbq{m}"] / max(1.0, agg[f"q{m}"]), 4),
-                    "ms_per_frame": ms / a.steps / max(1, world)}
+                    "ms_per_frame": ms / a.steps / max(1, n_gpus)}
         g, c = kstats(0), kstats(1)
         traffic = load_traffic(a, g["queries_per_launch"])
         roofline = {"bound": "hbm", "achieved": g["achieved_GBps"], "peak": HBM_PEAK_GBPS,
@@ -226,11 +305,17 @@ def main():
                     "bytes_per_unit": "16 B per photon returned (SURVEY.md 8(d))",
                     "global": g, "caustic_kernel": dict(c, kernel=KNN_KINDS.get(kind[1], str(kind[1])))}
         cpu = None
-        if not a.no_cpu_baseline and world == 1:
+        if not a.no_cpu_baseline and n_gpus == 1:
             cpu = cpu_baseline(a)
+        rgb = last.get("rgb")
+        par = {"single": "1 GPU",
+               "device-set": f"one process, device set {devices}: tiles{a.tile}x{a.tile} % {n_gpus}, "
+                             "ncclSend/ncclRecv tile gather onto device 0",
+               "torchrun": f"one process per GPU: tiles{a.tile}x{a.tile} % {n_gpus}, packed shards "
+                           "gathered to rank 0 over RCCL"}[mode]
         line = {
             "metric": "Mpixel-samples/sec (and ms/frame) at 1024^2 aa=2, 1M+1M photons",
-            "value": round(value, 4), "unit": "Mpixel-samples/s", "n_gpus": world,
+            "value": round(value, 4), "unit": "Mpixel-samples/s", "n_gpus": n_gpus,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_per_step, 2),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": "f64 (shading/geometry), f32 (photon positions)",
@@ -239,12 +324,21 @@ def main():
             "config": {"workload": f"{a.scene} {w}x{h} aa={aa} "
                                    f"{a.global_photons}+{a.caustic_photons} photons {a.extra}".strip(),
                        "pixel_samples_per_frame": samples_per_frame,
-                       "parallelism": f"tiles{a.tile}x{a.tile} % {world}",
+                       "parallelism": par,
                        "photon_map_s": round(photon_s, 3),
                        "global_stored": pst["global_stored"],
                        "caustic_stored": pst["caustic_stored"]},
+            "image_sha16": (hashlib.sha256(rgb.tobytes()).hexdigest()[:16]
+                            if rgb is not None else None),
             "roofline": roofline, "cpu_baseline": cpu,
         }
+        if mode == "device-set":
+            line["device_set"] = {"devices": devices,
+                                  "device_render_ms_max": round(agg["devmax"] / a.steps * 1e3, 2),
+                                  "device_render_ms_min": round(agg["devmin"] / a.steps * 1e3, 2),
+                                  "gather_ms": round(agg["gather"] / a.steps * 1e3, 3),
+                                  "knn_kernel_ms_per_device_per_frame":
+                                      round((agg["ms0"] + agg["ms1"]) / a.steps / n_gpus, 2)}
         print(json.dumps(line), flush=True)
     r.close()
     if dist is not None:

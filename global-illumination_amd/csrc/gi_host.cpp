@@ -237,7 +237,8 @@ Rccl g_rccl;
 // map, so the two maps' estimates can run concurrently on two streams during a render.
 struct MapExec {
   hipStream_t st = nullptr;        // the ctx stream, or the side stream while maps overlap
-  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;  // launch / fallback split timing
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;  // chunk pass | second
+                                   // chunk pass | fallback split timing (ev0 ev2 ev3 ev1)
   SortScratch sorter;              // Morton order of the query list
   DBuf list_idx, list_d2, list_n;  // K-best lists of the query-per-wave k-NN path
   DBuf gheap_d2, gheap_idx;        // global-memory heaps (K > 64 per-lane kernel)
@@ -287,8 +288,10 @@ struct gi_ctx {
   int chunk_cap_big = 512;        // large-K chunk kernel: the same (384 or 512)
   int chunk_minsub_big = 64;      // large-K chunk kernel: overflowing chunks retried down to this (64: none, measured best)
   int chunk_minsub = 32;          // chunk kernel: overflowing chunks retried as halves (measured best with the dk bound)
-  double fb_ms[2] = {0, 0};       // fallback time and queries per map (since the last reset)
-  uint64_t fb_q[2] = {0, 0};
+  double fb_ms[2] = {0, 0};       // final fallback kernel's time and queries per map (since the
+  uint64_t fb_q[2] = {0, 0};      // last reset)
+  double p2_ms[2] = {0, 0};       // second chunk pass's time and queries per map
+  uint64_t p2_q[2] = {0, 0};
   int last_kind[2] = {-1, -1};
   bool knn_log = false;            // GI_KNN_LOG: one stderr line per chunk k-NN launch
   int elem_pretest = -1;           // GI_ELEM_PRETEST: -1 auto (make_view), 0 off, 1 on
@@ -579,30 +582,30 @@ int trace_batch_dev(gi_ctx *c, int caustic, int light, int64_t e0, int64_t n,
   return GI_OK;
 }
 
-// Run fn(k, ctx_k) for every device of the set on its own host thread (k = 0 is this context);
-// returns the first failure, with that device's message copied into c->err.
+// Run fn(k, ctx_k) for every device of the set (k = 0 is this context, run on the calling
+// thread, so its progress callbacks arrive where gi.h promises; each peer on a host thread of
+// its own); returns the first failure, with that device's message copied into c->err.
 template <typename Fn>
 int on_devices(gi_ctx *c, Fn fn) {
   const int nd = 1 + (int)c->peers.size();
   if (nd == 1) return fn(0, c);
   std::vector<int> rc(nd, GI_OK);
+  auto run = [&](int k, gi_ctx *d) {
+    if (hipSetDevice(d->device) != hipSuccess) {
+      rc[k] = fail(d, GI_ERR_HIP, "hipSetDevice failed");
+      return;
+    }
+    try {
+      rc[k] = fn(k, d);
+    } catch (const std::bad_alloc &) {
+      rc[k] = fail(d, GI_ERR_ALLOC, "host allocation failed");
+    } catch (...) {
+      rc[k] = fail(d, GI_ERR_HIP, "unexpected exception");
+    }
+  };
   std::vector<std::thread> th;
-  for (int k = 0; k < nd; k++) {
-    gi_ctx *d = k ? c->peers[k - 1] : c;
-    th.emplace_back([&, k, d]() {
-      if (hipSetDevice(d->device) != hipSuccess) {
-        rc[k] = fail(d, GI_ERR_HIP, "hipSetDevice failed");
-        return;
-      }
-      try {
-        rc[k] = fn(k, d);
-      } catch (const std::bad_alloc &) {
-        rc[k] = fail(d, GI_ERR_ALLOC, "host allocation failed");
-      } catch (...) {
-        rc[k] = fail(d, GI_ERR_HIP, "unexpected exception");
-      }
-    });
-  }
+  for (int k = 1; k < nd; k++) th.emplace_back(run, k, c->peers[k - 1]);
+  run(0, c);
   for (auto &t : th) t.join();
   hipSetDevice(c->device);
   for (int k = 0; k < nd; k++)
@@ -787,7 +790,9 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
     HIPCHK(c, hipStreamSynchronize(X.st));
     X.fb_total += nfb;
     uint32_t nfb2 = nfb;
+    bool ran2 = false;
     if (nfb && c->chunk_big2) {
+      ran2 = true;
       // second chunk pass with 1024 LDS candidates over the overflowing chunks' queries (the
       // compacted list keeps each chunk's queries together, in Morton order); what overflows
       // again goes to the query-per-wave kernel
@@ -816,6 +821,7 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
       HIPCHK(c, hipMemcpyAsync(&nfb2, dense + nfb, 4, hipMemcpyDeviceToHost, X.st));
       HIPCHK(c, hipStreamSynchronize(X.st));
     }
+    HIPCHK(c, hipEventRecord(X.ev3, X.st));
     if (nfb2) {
       KnnArgs f = k;
       f.perm = dense;
@@ -828,16 +834,19 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
     HIPCHK(c, hipEventRecord(X.ev1, X.st));
     if (ms) {
       HIPCHK(c, hipEventSynchronize(X.ev1));
-      float t = 0, tf = 0;
+      float t = 0, tf = 0, t2 = 0;
       HIPCHK(c, hipEventElapsedTime(&t, X.ev0, X.ev1));
-      HIPCHK(c, hipEventElapsedTime(&tf, X.ev2, X.ev1));
+      HIPCHK(c, hipEventElapsedTime(&tf, X.ev3, X.ev1));
+      HIPCHK(c, hipEventElapsedTime(&t2, X.ev2, X.ev3));
       *ms += t;
       int mi = k.stat_off ? 1 : 0;
       c->fb_ms[mi] += tf;
-      c->fb_q[mi] += nfb;
+      c->fb_q[mi] += nfb2;
+      c->p2_ms[mi] += t2;
+      c->p2_q[mi] += ran2 ? nfb : 0;
       if (c->knn_log)
-        fprintf(stderr, "[gi] knn map %d kind 8: nq %lld chunk pass %.2f ms, second pass %u, wave %u, fallback %.2f ms\n",
-                mi, (long long)nq, t - tf, nfb, nfb2, tf);
+        fprintf(stderr, "[gi] knn map %d kind 8: nq %lld chunk pass %.2f ms, second pass %u (%.2f ms), wave %u (%.2f ms)\n",
+                mi, (long long)nq, t - tf - t2, nfb, t2, nfb2, tf);
     }
     return GI_OK;
   }
@@ -881,7 +890,9 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
     HIPCHK(c, hipStreamSynchronize(X.st));
     X.fb_total += nfb;
     uint32_t nfb2 = nfb;
+    bool ran2 = false;
     if (nfb && c->chunk_lane2 && !c->chunk_fb_all) {
+      ran2 = true;
       // second chunk pass, 480 LDS candidates, over the overflowing chunks' queries (the
       // compacted list keeps each chunk's queries together, in Morton order)
       int64_t chunks2 = ((int64_t)nfb + 63) / 64;
@@ -907,6 +918,7 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
       HIPCHK(c, hipMemcpyAsync(&nfb2, dense + nfb, 4, hipMemcpyDeviceToHost, X.st));
       HIPCHK(c, hipStreamSynchronize(X.st));
     }
+    HIPCHK(c, hipEventRecord(X.ev3, X.st));
     if (nfb2) {
       KnnArgs f = k;
       f.perm = dense;
@@ -919,16 +931,19 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
     HIPCHK(c, hipEventRecord(X.ev1, X.st));
     if (ms) {
       HIPCHK(c, hipEventSynchronize(X.ev1));
-      float t = 0, tf = 0;
+      float t = 0, tf = 0, t2 = 0;
       HIPCHK(c, hipEventElapsedTime(&t, X.ev0, X.ev1));
-      HIPCHK(c, hipEventElapsedTime(&tf, X.ev2, X.ev1));
+      HIPCHK(c, hipEventElapsedTime(&tf, X.ev3, X.ev1));
+      HIPCHK(c, hipEventElapsedTime(&t2, X.ev2, X.ev3));
       *ms += t;
       int mi = k.stat_off ? 1 : 0;
       c->fb_ms[mi] += tf;
-      c->fb_q[mi] += nfb;
+      c->fb_q[mi] += nfb2;
+      c->p2_ms[mi] += t2;
+      c->p2_q[mi] += ran2 ? nfb : 0;
       if (c->knn_log)
-        fprintf(stderr, "[gi] knn map %d kind 7: nq %lld chunk %.2f ms, second pass %u, per-lane %u, fallback %.2f ms\n",
-                mi, (long long)nq, t - tf, nfb, nfb2, tf);
+        fprintf(stderr, "[gi] knn map %d kind 7: nq %lld chunk %.2f ms, second pass %u (%.2f ms), per-lane %u (%.2f ms)\n",
+                mi, (long long)nq, t - tf - t2, nfb, t2, nfb2, tf);
     }
     return GI_OK;
   }
@@ -1369,6 +1384,7 @@ int gi_create(gi_ctx **out, int dev) {
     hipEventCreate(&c->mx[m].ev0);
     hipEventCreate(&c->mx[m].ev1);
     hipEventCreate(&c->mx[m].ev2);
+    hipEventCreate(&c->mx[m].ev3);
   }
   std::vector<double> lut;
   build_lut(lut);
@@ -1470,6 +1486,7 @@ void gi_destroy(gi_ctx *c) {
     if (X.ev0) hipEventDestroy(X.ev0);
     if (X.ev1) hipEventDestroy(X.ev1);
     if (X.ev2) hipEventDestroy(X.ev2);
+    if (X.ev3) hipEventDestroy(X.ev3);
   }
   for (int l = 0; l < 2; l++) {
     c->qpos[l].release(); c->qshade[l].release(); c->qkey[l].release(); c->qout[l].release();
@@ -1639,15 +1656,31 @@ int gi_map_photons(gi_ctx *c, gi_photon_stats *st) {
   rc = replicate_maps(c);
   if (rc) return rc;
   auto t3 = std::chrono::steady_clock::now();
+  // the k-NN kernels' per-photon K-th distance bounds (ensure_dk), for the estimate sizes and
+  // distances the render will use: part of building the maps, so timed here and not inside
+  // the first RenderImage
+  rc = on_devices(c, [&](int, gi_ctx *d) -> int {
+    for (int m = 0; m < 2; m++) {
+      if (!d->map_valid[m] || d->dmap[m].n == 0) continue;
+      KnnArgs k = knn_args(d, m);
+      if (k.K <= 0 || k.K + 64 > 1024) continue;  // only the per-lane global-heap kernel
+      int r = ensure_dk(d, k);
+      if (r) return r;
+    }
+    return (int)GI_OK;
+  });
+  if (rc) return rc;
+  auto t4 = std::chrono::steady_clock::now();
   if (st) {
     st->global_stored = (int64_t)c->hmap[0].storage.size();
     st->caustic_stored = (int64_t)c->hmap[1].storage.size();
     st->global_emitted = gem;
     st->caustic_emitted = cem;
     st->trace_s = std::chrono::duration<double>(t1 - t0).count();
-    st->kd_s = std::chrono::duration<double>(t2 - t1).count();
+    // kd_s: the tree builds, their replication and the k-NN bound pass
+    st->kd_s = std::chrono::duration<double>((t2 - t1) + (t4 - t3)).count();
     st->irradiance_s = std::chrono::duration<double>(t3 - t2).count();
-    st->total_s = std::chrono::duration<double>(t3 - t0).count();
+    st->total_s = std::chrono::duration<double>(t4 - t0).count();
   }
   return GI_OK;
 }
@@ -1715,6 +1748,8 @@ static int render_common(gi_ctx *c, int aa, int w, int h, const std::vector<int3
   HIPCHK(c, hipMemsetAsync(c->d_stats.p, 0, ST_BYTES, c->stream));
   c->fb_ms[0] = c->fb_ms[1] = 0;
   c->fb_q[0] = c->fb_q[1] = 0;
+  c->p2_ms[0] = c->p2_ms[1] = 0;
+  c->p2_q[0] = c->p2_q[1] = 0;
   c->last_kind[0] = c->last_kind[1] = -1;
   gi_render_stats local;
   memset(&local, 0, sizeof local);
@@ -1745,6 +1780,8 @@ static int render_common(gi_ctx *c, int aa, int w, int h, const std::vector<int3
       st->knn_map_launches[m] = local.knn_map_launches[m];
       st->knn_map_fallback_ms[m] = c->fb_ms[m];
       st->knn_map_fallback_queries[m] = c->fb_q[m];
+      st->knn_map_pass2_ms[m] = c->p2_ms[m];
+      st->knn_map_pass2_queries[m] = c->p2_q[m];
       st->knn_map_kind[m] = c->last_kind[m];
     }
     st->knn_queries = st->knn_map_queries[0] + st->knn_map_queries[1];
@@ -1801,8 +1838,9 @@ static int render_multi(gi_ctx *c, int aa, int w, int h, uint8_t *rgb8, float *r
     return (int)GI_OK;
   });
   if (rc) return rc;
-  c->recv.resize(nd);
-  c->peer_pix.resize(nd);
+  auto tg = std::chrono::steady_clock::now();
+  if ((int)c->recv.size() < nd) c->recv.resize(nd);
+  if ((int)c->peer_pix.size() < nd) c->peer_pix.resize(nd);
   for (int k = 1; k < nd; k++) {
     const int64_t n = (int64_t)pix[k].size() / 2;
     HIPCHK(c, c->recv[k].ensure((size_t)n * 16));
@@ -1853,10 +1891,16 @@ static int render_multi(gi_ctx *c, int aa, int w, int h, uint8_t *rgb8, float *r
         st->knn_map_launches[m] += a.knn_map_launches[m];
         st->knn_map_fallback_ms[m] += a.knn_map_fallback_ms[m];
         st->knn_map_fallback_queries[m] += a.knn_map_fallback_queries[m];
+        st->knn_map_pass2_ms[m] += a.knn_map_pass2_ms[m];
+        st->knn_map_pass2_queries[m] += a.knn_map_pass2_queries[m];
         if (k == 0) st->knn_map_kind[m] = a.knn_map_kind[m];
       }
+      st->device_render_s_max = k ? std::max(st->device_render_s_max, a.render_s) : a.render_s;
+      st->device_render_s_min = k ? std::min(st->device_render_s_min, a.render_s) : a.render_s;
     }
-    st->render_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    const auto t1 = std::chrono::steady_clock::now();
+    st->gather_s = std::chrono::duration<double>(t1 - tg).count();
+    st->render_s = std::chrono::duration<double>(t1 - t0).count();
   }
   return GI_OK;
 }
@@ -1887,6 +1931,52 @@ int gi_render_tiles(gi_ctx *c, int aa, int w, int h, int tile, int shard, int ns
   hipSetDevice(c->device);
   std::vector<int32_t> pix = shard_pixels(w, h, tile, shard, nshards);
   return render_common(c, aa, w, h, pix, nullptr, rgbf, st, true);
+}
+
+// One rank's shard, left on the device and packed (torchrun: each rank gathers these buffers to
+// rank 0 over RCCL and rank 0 composes them with gi_compose_tiles; nothing else crosses).
+int gi_render_tiles_packed(gi_ctx *c, int aa, int w, int h, int tile, int shard, int nshards,
+                           void *packed, int64_t cap, int64_t *npix, gi_render_stats *st) {
+  if (!c || !npix || tile <= 0 || nshards <= 0 || shard < 0 || shard >= nshards || w <= 0 || h <= 0)
+    return GI_ERR_ARG;
+  hipSetDevice(c->device);
+  std::vector<int32_t> pix = shard_pixels(w, h, tile, shard, nshards);
+  const int64_t n = (int64_t)pix.size() / 2;
+  *npix = n;
+  if (!packed) return GI_OK;
+  if (cap < n) return fail(c, GI_ERR_ARG, "packed buffer holds fewer pixels than the shard");
+  if (!c->peers.empty()) return fail(c, GI_ERR_STATE, "packed shards are for one-device contexts");
+  int rc = render_common(c, aa, w, h, pix, nullptr, nullptr, st, false);
+  if (rc) return rc;
+  launch_pack_pixels(c->pixels.as<int32_t>(), n, w, c->rgbf.as<float>(), c->rgb8.as<uint8_t>(),
+                     packed, c->stream);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GI_OK;
+}
+
+int gi_compose_tiles(gi_ctx *c, int w, int h, int tile, int nshards, const void *packed,
+                     int64_t stride, uint8_t *rgb8, float *rgbf) {
+  if (!c || !packed || tile <= 0 || nshards <= 0 || w <= 0 || h <= 0) return GI_ERR_ARG;
+  hipSetDevice(c->device);
+  const size_t npx = (size_t)w * h * 3;
+  HIPCHK(c, c->rgbf.ensure(npx * 4));
+  HIPCHK(c, c->rgb8.ensure(npx));
+  if ((int)c->peer_pix.size() < nshards) c->peer_pix.resize(nshards);
+  for (int s = 0; s < nshards; s++) {
+    std::vector<int32_t> pix = shard_pixels(w, h, tile, s, nshards);
+    const int64_t n = (int64_t)pix.size() / 2;
+    if (n > stride) return fail(c, GI_ERR_ARG, "packed stride smaller than a shard");
+    HIPCHK(c, upload(c->peer_pix[s], pix.data(), pix.size() * 4, c->stream));
+    launch_unpack_pixels(c->peer_pix[s].as<int32_t>(), n, w,
+                         (const uint8_t *)packed + (size_t)s * stride * 16, c->rgbf.as<float>(),
+                         c->rgb8.as<uint8_t>(), c->stream);
+    HIPCHK(c, hipGetLastError());
+  }
+  if (rgbf) HIPCHK(c, hipMemcpyAsync(rgbf, c->rgbf.p, npx * 4, hipMemcpyDeviceToHost, c->stream));
+  if (rgb8) HIPCHK(c, hipMemcpyAsync(rgb8, c->rgb8.p, npx, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GI_OK;
 }
 
 int gi_quantize(int w, int h, const float *rgbf, uint8_t *rgb8) {

@@ -932,8 +932,10 @@ void knn_chunk_lane_kernel(KnnArgs a) {
   __shared__ uint32_t stk[64];  // kd walk stack (walk_within)
   // kept LDS slots [s][lane] (K <= 64, u8) during the collect and the estimate; during the
   // counting passes the lanes' bin counters [w][lane] (u32, four u8 bins each), and during the
-  // bound phase the centre select's 256-bin histogram
-  __shared__ uint32_t selh[16 * SB * 64];
+  // bound phase the centre select's 256-bin histogram. One spare slot row (row 64): a lane that
+  // keeps exactly K = 64 photons without a bracket stores its later, unkept candidates there
+  // (the collect's branch-free store always writes entry n).
+  __shared__ uint32_t selh[16 * SB * 64 + 16 * SB];
   SlotT *sel = reinterpret_cast<SlotT *>(selh);
   uint32_t *hist = selh;
   const int lane = threadIdx.x;

@@ -28,7 +28,8 @@ EXPORTED = [
     "gi_params_default", "gi_parse_args", "gi_create", "gi_create_devices", "gi_destroy",
     "gi_last_error",
     "gi_set_params", "gi_read_scene", "gi_scene_info", "gi_map_photons", "gi_set_photon_map",
-    "gi_get_photon_map", "gi_get_kd_tree", "gi_set_progress", "gi_render_image", "gi_render_tiles", "gi_quantize",
+    "gi_get_photon_map", "gi_get_kd_tree", "gi_set_progress", "gi_render_image", "gi_render_tiles",
+    "gi_render_tiles_packed", "gi_compose_tiles", "gi_quantize",
     "gi_estimate_radiance_batch", "gi_knn_batch", "gi_knn_bench", "gi_intersect_batch",
     "gi_write_image",
 ]
@@ -81,7 +82,10 @@ class RenderStats(C.Structure):
         ("knn_map_queries", C.c_uint64 * 2), ("knn_map_photons", C.c_uint64 * 2),
         ("knn_map_visited", C.c_uint64 * 2), ("knn_map_kernel_ms", C.c_double * 2),
         ("knn_map_launches", C.c_double * 2), ("knn_map_fallback_ms", C.c_double * 2),
-        ("knn_map_fallback_queries", C.c_uint64 * 2), ("knn_map_kind", C.c_int32 * 2)]
+        ("knn_map_fallback_queries", C.c_uint64 * 2), ("knn_map_kind", C.c_int32 * 2),
+        ("knn_map_pass2_ms", C.c_double * 2), ("knn_map_pass2_queries", C.c_uint64 * 2),
+        ("device_render_s_max", C.c_double), ("device_render_s_min", C.c_double),
+        ("gather_s", C.c_double)]
 
 
 def _stats_dict(st):
@@ -127,6 +131,11 @@ def lib():
                                       C.c_void_p, P(RenderStats)]
         L.gi_render_tiles.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                       C.c_int, C.c_void_p, P(RenderStats)]
+        L.gi_render_tiles_packed.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                             C.c_int, C.c_int, C.c_void_p, C.c_int64,
+                                             P(C.c_int64), P(RenderStats)]
+        L.gi_compose_tiles.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                       C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
         L.gi_quantize.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         L.gi_estimate_radiance_batch.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_void_p,
                                                  C.c_void_p, C.c_void_p, C.c_void_p]
@@ -261,6 +270,33 @@ class Renderer:
         self._check(lib().gi_render_tiles(self._ctx, aa, width, height, tile, shard, nshards,
                                           rgbf.ctypes.data, C.byref(st)))
         return rgbf, _stats_dict(st)
+
+    def shard_pixels(self, width, height, tile, shard, nshards):
+        """Pixels of one tile shard (gi_render_tiles_packed with a null buffer)."""
+        n = C.c_int64(0)
+        self._check(lib().gi_render_tiles_packed(self._ctx, 0, width, height, tile, shard,
+                                                 nshards, None, 0, C.byref(n), None))
+        return n.value
+
+    def render_tiles_packed(self, aa, width, height, tile, shard, nshards, dev_ptr, capacity):
+        """Render a tile shard into a device buffer (`dev_ptr`, 16 B per pixel, e.g. the
+        data_ptr() of a CUDA tensor on this context's device). Returns (pixels, stats)."""
+        n = C.c_int64(0)
+        st = RenderStats()
+        self._check(lib().gi_render_tiles_packed(self._ctx, aa, width, height, tile, shard,
+                                                 nshards, C.c_void_p(dev_ptr), capacity,
+                                                 C.byref(n), C.byref(st)))
+        return n.value, _stats_dict(st)
+
+    def compose_tiles(self, width, height, tile, nshards, dev_ptr, stride, want_float=False):
+        """Full frame from nshards packed shard buffers at dev_ptr (device, stride pixels
+        apart). Returns rgb8 [, rgbf]."""
+        rgb = np.zeros((height, width, 3), dtype=np.uint8)
+        rgbf = np.zeros((height, width, 3), dtype=np.float32) if want_float else None
+        self._check(lib().gi_compose_tiles(self._ctx, width, height, tile, nshards,
+                                           C.c_void_p(dev_ptr), stride, rgb.ctypes.data,
+                                           rgbf.ctypes.data if want_float else None))
+        return (rgb, rgbf) if want_float else rgb
 
     def EstimateRadiance(self, which, queries):
         q = np.ascontiguousarray(queries, dtype=QUERY_DTYPE)

@@ -124,6 +124,8 @@ typedef struct gi_radiance_query {
 typedef struct gi_photon_stats {
   int64_t global_stored, caustic_stored;
   int64_t global_emitted, caustic_emitted;
+  /* trace_s: emission rounds + power rescale; kd_s: kd builds and the k-NN kernels' per-photon
+   * K-th distance bound pass; irradiance_s: the -cache pass and replication over a device set */
   double total_s, trace_s, kd_s, irradiance_s;
 } gi_photon_stats;
 
@@ -139,13 +141,21 @@ typedef struct gi_render_stats {
   /* the same split per photon map (0 = global, 1 = caustic) */
   uint64_t knn_map_queries[2], knn_map_photons[2], knn_map_visited[2];
   double knn_map_kernel_ms[2], knn_map_launches[2];
-  /* chunk k-NN path: time and queries of the per-lane fallback within knn_map_kernel_ms */
+  /* chunk k-NN path, within knn_map_kernel_ms: time and queries of the final fallback kernel
+   * (per-lane for K <= 64, query-per-wave for K > 64): the queries neither chunk pass resolved */
   double knn_map_fallback_ms[2];
   uint64_t knn_map_fallback_queries[2];
   /* k-NN launch sequence the last batch ran per map (-1 none): 7 lane-select chunk kernel +
    * per-lane fallback, 8 large-K chunk kernel (+ second chunk pass) + query-per-wave fallback,
    * 3 per-lane, 1 query-per-wave, 0 per-lane with global heaps, 9 irradiance-cache lookup */
   int32_t knn_map_kind[2];
+  /* chunk k-NN path: time of the second chunk pass (larger LDS candidate set) and the queries
+   * the first pass handed to it (those it did not resolve are in knn_map_fallback_queries) */
+  double knn_map_pass2_ms[2];
+  uint64_t knn_map_pass2_queries[2];
+  /* device sets (gi_create_devices): the slowest and fastest device's render phase and the
+   * tile gather onto the first device after the last one finished (0 on one device) */
+  double device_render_s_max, device_render_s_min, gather_s;
 } gi_render_stats;
 
 typedef struct gi_ctx gi_ctx;
@@ -206,6 +216,21 @@ int gi_render_image(gi_ctx *ctx, int aa, int width, int height, uint8_t *rgb8, f
  * t % nshards == shard; rgbf is the full W*H*3 image, untouched outside the shard. */
 int gi_render_tiles(gi_ctx *ctx, int aa, int width, int height, int tile_px, int shard,
                     int nshards, float *rgbf, gi_render_stats *stats);
+/* Shard left on the device (one-process-per-GPU ranks, e.g. torchrun): renders the same tiles
+ * as gi_render_tiles and writes them packed into `packed`, a DEVICE pointer on the context's
+ * device holding `capacity` pixels: 16 B per pixel of the shard, in the shard's tile order
+ * (f32 r, g, b; the u8 r, g, b in the low 24 bits of the fourth word). *npix receives the
+ * shard's pixel count (packed == NULL only reports it). Synchronous: the buffer is complete on
+ * return. */
+int gi_render_tiles_packed(gi_ctx *ctx, int aa, int width, int height, int tile_px, int shard,
+                           int nshards, void *packed, int64_t capacity, int64_t *npix,
+                           gi_render_stats *stats);
+/* Compose the frame from every shard's packed pixels: `packed` is a DEVICE pointer on the
+ * context's device to nshards buffers of `stride` pixels (16 B each), shard s at s * stride
+ * (the layout of a gather of gi_render_tiles_packed outputs). rgb8 / rgbf (host, optional)
+ * receive the full image as gi_render_image returns it. */
+int gi_compose_tiles(gi_ctx *ctx, int width, int height, int tile_px, int nshards,
+                     const void *packed, int64_t stride, uint8_t *rgb8, float *rgbf);
 /* Quantise a full float image like RenderImage's SetPixelRGB (truncate 255*c). */
 int gi_quantize(int width, int height, const float *rgbf, uint8_t *rgb8);
 

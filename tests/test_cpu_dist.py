@@ -32,7 +32,33 @@ class FakeTiles:
             {"pixels": int(own.sum())}
 
 
-def _worker(rank, world, port, w, h, tile, q):
+class FakePacked:
+    """gi_render_tiles_packed / gi_compose_tiles contract on host memory: the shard's pixels in
+    packed order, 16 B each (f32 RGB + u8 RGB bits), written through a raw pointer."""
+    @staticmethod
+    def _view(ptr, n):
+        import ctypes as C
+        return np.ctypeslib.as_array((C.c_float * (4 * n)).from_address(ptr)).reshape(n, 4)
+
+    def render_tiles_packed(self, aa, w, h, tile, rank, world, ptr, cap):
+        pix = gi_dist.shard_pixel_list(w, h, tile, rank, world)
+        assert len(pix) <= cap
+        ref = reference_image(w, h)
+        v = self._view(ptr, cap)
+        for i, (x, y) in enumerate(pix):
+            v[i, :3] = ref[y, x]
+        return len(pix), {"pixels": len(pix)}
+
+    def compose_tiles(self, w, h, tile, world, ptr, stride, want_float=True):
+        full = np.zeros((h, w, 3), dtype=np.float32)
+        v = self._view(ptr, stride * world).reshape(world, stride, 4)
+        for s in range(world):
+            for i, (x, y) in enumerate(gi_dist.shard_pixel_list(w, h, tile, s, world)):
+                full[y, x] = v[s, i, :3]
+        return (full * 255).astype(np.uint8), full
+
+
+def _worker(rank, world, port, w, h, tile, q, packed=False):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -45,18 +71,26 @@ def _worker(rank, world, port, w, h, tile, q):
             sent.append(t.numel())
             return real_gather(t, parts, dst=dst)
         dist.gather = spy
-        img, st = gi_dist.render_sharded(FakeTiles(), 0, w, h, tile, rank, world, dist)
+        if packed:
+            import torch
+            img, st = gi_dist.render_sharded(FakePacked(), 0, w, h, tile, rank, world, dist,
+                                             torch.device("cpu"))
+            img = None if img is None else img[1]
+        else:
+            img, st = gi_dist.render_sharded(FakeTiles(), 0, w, h, tile, rank, world, dist)
         q.put((rank, st["pixels"], None if img is None else img, sent))
     finally:
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("packed", [False, True], ids=["host", "packed"])
 @pytest.mark.parametrize("world,w,h,tile", [(2, 70, 45, 16), (3, 64, 64, 16)])
-def test_sharded_gather_equals_full_frame(world, w, h, tile):
+def test_sharded_gather_equals_full_frame(world, w, h, tile, packed):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, w, h, tile, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, w, h, tile, q, packed))
+             for r in range(world)]
     for p in procs:
         p.start()
     out = [q.get(timeout=120) for _ in range(world)]
@@ -70,8 +104,21 @@ def test_sharded_gather_equals_full_frame(world, w, h, tile):
     # one gather per rank of at most the largest shard (not the whole frame)
     biggest = int(np.bincount(gi_dist.tile_owner_map(w, h, tile, world).ravel()).max())
     for o in out:
-        assert o[3] == [biggest * 3]
+        assert o[3] == [biggest * (4 if packed else 3)]
         assert biggest * world < w * h + tile * tile * world
+
+
+def test_shard_pixel_list_matches_owner_map():
+    w, h, tile, world = 70, 45, 16, 3
+    own = gi_dist.tile_owner_map(w, h, tile, world)
+    seen = np.zeros((h, w), dtype=int)
+    for s in range(world):
+        pix = gi_dist.shard_pixel_list(w, h, tile, s, world)
+        assert len(pix) == gi_dist.shard_sizes(w, h, tile, world)[s]
+        for x, y in pix:
+            assert own[y, x] == s
+            seen[y, x] += 1
+    assert np.all(seen == 1)
 
 
 def test_tile_owner_map_round_robin():

@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("n,k,r", [(20000, 50, 2.5), (50000, 225, 0.225), (3000, 50, 0.05),
-                                   (1, 50, 2.5), (100, 1, 0.3)])
+                                   (1, 50, 2.5), (100, 1, 0.3), (20000, 64, 2.5), (20000, 65, 0.5)])
 def test_knn_sets_match_oracle(renderer, n, k, r):
     ph = synth.photon_map(n, seed=n)
     q = synth.queries(512, seed=k)["point"]
@@ -44,7 +44,8 @@ def test_knn_empty_map(renderer):
 
 @pytest.mark.parametrize("filt,k,r,spec", [(DISK, 50, 2.5, False), (DISK, 225, 0.225, True),
                                            (CONE, 50, 0.3, False), (GAUSS, 64, 0.3, True),
-                                           (DISK, 10, 0.02, True)])
+                                           (DISK, 10, 0.02, True), (DISK, 64, 2.5, False),
+                                           (DISK, 64, 0.05, True)])
 def test_estimate_radiance_matches_oracle(renderer, filt, k, r, spec):
     ph = synth.photon_map(30000, seed=7)
     q = synth.queries(1000, seed=3, k=k, r=r, filt=filt, spec=spec)

@@ -111,7 +111,8 @@ def clustered_queries(n, seed, k, r, filt):
 
 
 @pytest.mark.parametrize("env", VARIANTS, ids=lambda e: "-".join(f"{k[3:]}{v}" for k, v in e.items()))
-@pytest.mark.parametrize("filt,k,r", [(DISK, 50, 2.5), (CONE, 32, 0.05), (DISK, 225, 0.225)])
+@pytest.mark.parametrize("filt,k,r", [(DISK, 50, 2.5), (CONE, 32, 0.05), (DISK, 225, 0.225),
+                                      (DISK, 64, 0.05), (DISK, 64, 2.5)])
 def test_variant_dense_queries(env, filt, k, r):
     r_ = make_renderer(env)
     try:

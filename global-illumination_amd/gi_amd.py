@@ -105,6 +105,14 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} missing: run `make -C global-illumination_amd`")
+        # One HIP runtime per process: torch ships its own libamdhip64 (soname libamdhip64.so.7,
+        # but its libraries NEED it under the unversioned name), so a process that loads this
+        # library first and torch later ends up with two runtimes, and torch then sees no GPU.
+        # When torch is importable it is loaded first and the library binds to its runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         P = C.POINTER
         L.gi_params_default.argtypes = [P(GiParams)]

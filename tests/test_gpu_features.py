@@ -238,15 +238,17 @@ def _off_triangles(path):
     return v, np.array(tris)
 
 
+@pytest.mark.parametrize("scn,off", [("teapot.scn", "teapot.off"), ("violin.scn", "violinBody.off"),
+                                     ("violin.scn", "strings.off")])
 @pytest.mark.parametrize("kind", ["surface", "edges", "outside"])
-def test_mesh_bvh_matches_linear_loop(renderer, kind):
+def test_mesh_bvh_matches_linear_loop(renderer, kind, scn, off):
     """The device walks each mesh of >= 16 triangles through its BVH (gi_device.h ray_mesh_bvh);
     the result must be R3Intersects(ray, R3TriangleArray)'s linear loop exactly: Q2 self-hits
     from rays leaving the surface (whole mesh missed), rays through shared edges and vertices
     (equal-t ties go to the lowest triangle index), and rays from outside."""
     rng = np.random.default_rng({"surface": 1, "edges": 2, "outside": 3}[kind])
-    v, f = _off_triangles(scene("teapot.off"))
-    renderer.ReadScene(scene("teapot.scn"))
+    v, f = _off_triangles(scene(off))
+    renderer.ReadScene(scene(scn))
     n = 6000
     tri = f[rng.integers(0, len(f), n)]
     a, b, c = v[tri[:, 0]], v[tri[:, 1]], v[tri[:, 2]]
@@ -267,10 +269,10 @@ def test_mesh_bvh_matches_linear_loop(renderer, kind):
         d = tgt - org
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     gh, gt, gp, gn, gm = renderer.Intersects(org, d)
-    oh, ot, op, on, om = oracle_lib.intersect(scene("teapot.scn"), org, d)
+    oh, ot, op, on, om = oracle_lib.intersect(scene(scn), org, d)
     np.testing.assert_array_equal(gh, oh)
     both = gh == 1
-    assert both.sum() > (0.05 if kind == "surface" else 0.5) * n
+    assert both.sum() > (0.05 if kind == "surface" else 0.3) * n
     np.testing.assert_array_equal(gt[both], ot[both])
     np.testing.assert_array_equal(gn[both], on[both])
     np.testing.assert_array_equal(gp[both], op[both])

@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--cpu-res", type=int, default=32,
                     help="CPU baseline sample: res x res px at the same aa (BASELINE.md section 3)")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--shard", default="",
+                    help="S/N: render only tile shard S of N on this GPU (one GPU's share of an "
+                         "N-GPU frame, e.g. C5's 0/8); value = that shard's pixel-samples/s")
     return ap.parse_args()
 
 
@@ -214,7 +217,21 @@ def main():
         dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
     last = {}
 
+    shard = None
+    if a.shard:
+        if world > 1 or n_gpus > 1:
+            raise SystemExit("--shard measures one GPU's share: run it on one GPU")
+        shard = tuple(int(x) for x in a.shard.split("/"))
+        import torch
+        npix_shard = r.shard_pixels(w, h, a.tile, shard[0], shard[1])
+        shard_buf = torch.zeros((npix_shard, 4), dtype=torch.float32, device="cuda:0")
+        torch.cuda.synchronize()
+
     def step():
+        if shard is not None:
+            _n, st = r.render_tiles_packed(aa, w, h, a.tile, shard[0], shard[1],
+                                           shard_buf.data_ptr(), npix_shard)
+            return st
         if world == 1:
             rgb, st = r.RenderImage(aa, w, h)
             last["rgb"] = rgb
@@ -271,7 +288,10 @@ def main():
         dist.all_reduce(ag)  # sums over ranks (kernel ms summed over GPUs)
         agg = dict(zip(keys, [float(x) for x in ag.tolist()]))
     samples_per_frame = w * h * 4 ** aa * p.dof_test
-    value = samples_per_frame * a.steps / elapsed / 1e6
+    samples_per_step = samples_per_frame
+    if shard is not None:
+        samples_per_step = npix_shard * 4 ** aa * p.dof_test
+    value = samples_per_step * a.steps / elapsed / 1e6
     ms_per_step = elapsed / a.steps * 1000.0
 
     if rank == 0:
@@ -332,6 +352,12 @@ def main():
                             if rgb is not None else None),
             "roofline": roofline, "cpu_baseline": cpu,
         }
+        if shard is not None:
+            line["shard"] = {"shard": shard[0], "nshards": shard[1], "pixels": npix_shard,
+                             "pixel_samples_per_step": samples_per_step,
+                             "ms_per_shard": round(ms_per_step, 1),
+                             "note": f"one GPU rendering tile shard {shard[0]} of {shard[1]}: an "
+                                     f"{shard[1]}-GPU frame takes about the slowest shard's time"}
         if mode == "device-set":
             line["device_set"] = {"devices": devices,
                                   "device_render_ms_max": round(agg["devmax"] / a.steps * 1e3, 2),

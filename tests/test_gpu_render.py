@@ -212,3 +212,16 @@ def test_element_pretest_is_exact(scene, monkeypatch):
             r.close()
         out.append(f)
     np.testing.assert_array_equal(out[0], out[1])
+
+
+def test_c5_settings_match_oracle(renderer):
+    """C5's sampling settings at an oracle-sized resolution: teapot.scn, aa 3 (64 subsamples per
+    pixel, render.cpp:174-178), depth of field with 4 aperture samples at the C5 focus and
+    aperture (-dof 4 12.2282 0.025, render.cpp:104-117, Q7), global map only."""
+    args = [scene("teapot.scn"), "/tmp/x.png", "-resolution", "10", "8", "-aa", "3", "-global",
+            "20000", "-no_caustic", "-it", "4", "-dof", "4", "12.2282", "0.025", "-seed", "6"]
+    g, gst, gp = run_gpu(renderer, args)
+    o, ost = oracle_lib.render(args, 10, 8)
+    assert gp["global_stored"] == ost["global_stored"]
+    assert gst["screen_rays"] == ost["screen_rays"] > 0  # primary hits (render.cpp:119-121)
+    compare(g, o, 0.99, 0.99, 0.5)

@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/photon_figs/oracle_blocks.npz: the oracle restatement's block means of
+every photon-map figure pin (tests/photon_figs.py FIGS) at the seeds photon_figs.SEEDS, plus the
+figures' own block means and the diffuse-block masks.
+
+The renders are the slow part of the pin (the oracle follows the reference's child-0-first kd
+search; fig_25b traces 10 M caustic photons per seed), so they are made once here, in the build
+container, and committed (figures with FIGS[...][4] = False are left to the GPU twin).
+tests/test_cpu_photon_figs.py re-renders seed 1 of the cheap figures to check the file still
+matches the oracle, and the GPU twin (tests/test_gpu_photon_figs.py) must reproduce every
+seed's blocks on the device.
+
+usage: python3 tools/photon_figs_oracle.py [fig ...]   (default: all; merges into the file)
+(the .png figures are only read here and by the CPU tests; the GPU twin reads this file)
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "global-illumination_amd"))
+
+import oracle_lib  # noqa: E402
+import photon_figs as pf  # noqa: E402
+
+
+def main():
+    names = sys.argv[1:] or list(pf.FIGS)
+    old = dict(np.load(pf.STATS)) if os.path.exists(pf.STATS) else {}
+    threads = len(os.sched_getaffinity(0))
+    for name in names:
+        t0 = time.time()
+        old[name + "/figure"] = pf.figure_blocks(name).astype(np.float32)
+        old[name + "/mask"] = pf.block_mask(name, oracle_lib.intersect)
+        if not pf.FIGS[name][4]:  # GPU twin only: the figure's blocks and mask
+            np.savez_compressed(pf.STATS, **old)
+            print(f"{name}: figure blocks and mask only", flush=True)
+            continue
+        blocks = []
+        for s in pf.SEEDS:
+            args, w, h = pf.render_args(name, s, threads=threads)
+            rgb, _st = oracle_lib.render(args, w, h)
+            blocks.append(pf.render_blocks(rgb, name))
+        old[name + "/seeds"] = np.stack(blocks).astype(np.float32)
+        r = pf.pin(old[name + "/figure"].astype(float), old[name + "/seeds"].astype(float),
+                   old[name + "/mask"])
+        print(f"{name}: {time.time() - t0:.0f} s  z_frac {r['z_frac']:.3f}  median|z| "
+              f"{r['median_abs_z']:.2f}  ratio {r['ratio']:.4f}  blocks {r['blocks']}  "
+              f"{'PASS' if r['ok'] else 'FAIL'}", flush=True)
+        np.savez_compressed(pf.STATS, **old)
+
+
+if __name__ == "__main__":
+    main()

@@ -119,6 +119,8 @@ struct SceneView {
   uint32_t kinds;  // bit k set: the scene holds shapes of ShapeKind k
   int32_t hard_lights;  // every light is a point, spot or directional light
   int32_t elem_pretest; // scene_intersect runs elem_maybe_hit before each element's box test
+  int32_t rigid;        // every node transform is rigid: a hit's world t is its distance
+  int32_t pad;
   double radius;
   double centroid[3];
   double ambient[3];
@@ -500,9 +502,20 @@ struct Hit {
 // Ray direction is renormalised per graph level (R3Line::InverseTransform, R3Line.cpp:140).
 // Inlined at every call site: node/element/shape records are wave-uniform (scalar loads) and
 // the root-first transform chain is precomputed per node, so nothing lives in scratch.
+//
+// Elements of triangles / spheres / circles (DElement::shapes_first_ok) test their shapes
+// first and the element box only when a shape would improve on closest: the box test gates the
+// element's hits, so running it last gives the same result, and most rays miss most elements
+// (the plane test of a triangle is cheaper than the box's slab divisions).
+//
+// Bounded form for shadow rays (illum_test): t_init < kInf starts the search at that world t
+// (hits beyond it are not looked for), and the walk returns 2 as soon as an element is taken
+// with t < t_exit (closest only decreases, so the final hit is nearer still). 0 = no hit below
+// t_init, 1 = hit in h.
 template <uint32_t KINDS = KINDS_ALL>
-__device__ __forceinline__ bool scene_intersect(const SceneView &S, V org, V dir, Hit &h) {
-  double closest = kInf;  // world-frame t (rigid transforms keep t; scale handled below)
+__device__ __forceinline__ int scene_intersect_b(const SceneView &S, V org, V dir, Hit &h,
+                                                 double t_init, double t_exit) {
+  double closest = t_init;  // world-frame t (rigid transforms keep t; scale handled below)
   bool found = false;
   V hp = mk(0, 0, 0), hn = mk(0, 0, 0);
   int hnode = 0, hmat = -1;
@@ -533,11 +546,14 @@ __device__ __forceinline__ bool scene_intersect(const SceneView &S, V org, V dir
       const DElement &el = S.elems[nd.elem_first + ei];
       double maxt = closest / scale;
       if (S.elem_pretest && !elem_maybe_hit(el, lo, linv, maxt)) continue;
-      if (!box_contains(el.bmin, el.bmax, lo)) {
+      auto box_pass = [&]() -> bool {
+        if (box_contains(el.bmin, el.bmax, lo)) return true;
         double bt;
-        if (!ray_box(lo, ldir, el.bmin, el.bmax, &bt, nullptr)) continue;
-        if (isPos(bt - maxt)) continue;
-      }
+        if (!ray_box(lo, ldir, el.bmin, el.bmax, &bt, nullptr)) return false;
+        return !isPos(bt - maxt);
+      };
+      const bool shapes_first = el.shapes_first_ok != 0;
+      if (!shapes_first && !box_pass()) continue;
       double ec = maxt;
       V ep = mk(0, 0, 0), en = mk(0, 0, 0);
       for (int si = 0; si < el.shape_count; si++) {
@@ -552,15 +568,17 @@ __device__ __forceinline__ bool scene_intersect(const SceneView &S, V org, V dir
         }
       }
       if (ec == maxt) continue;
+      if (shapes_first && !box_pass()) continue;
       found = true;
       closest = ec * scale;
       hp = ep;
       hn = en;
       hnode = ni;
       hmat = el.material;
+      if (closest < t_exit) return 2;
     }
   }
-  if (!found) return false;
+  if (!found) return 0;
   // transform hit point / normal back to world (Q11: normal by the forward affine)
   for (int c = hnode; c >= 0; c = S.nodes[c].parent) {
     const DNode &a = S.nodes[c];
@@ -574,7 +592,12 @@ __device__ __forceinline__ bool scene_intersect(const SceneView &S, V org, V dir
   h.n = hn;
   h.t = closest;
   h.mat = hmat;
-  return true;
+  return 1;
+}
+
+template <uint32_t KINDS = KINDS_ALL>
+__device__ __forceinline__ bool scene_intersect(const SceneView &S, V org, V dir, Hit &h) {
+  return scene_intersect_b<KINDS>(S, org, dir, h, kInf, -1.0) == 1;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -655,14 +678,26 @@ struct Counts {  // per-thread -v counters (render.cpp:26-32)
   uint32_t shadow, monte, trans, spec, indirect, caustic;
 };
 
-// RayIlluminationTest, illumination_utils.cpp:16-31 (Q13 distance equality)
+// RayIlluminationTest, illumination_utils.cpp:16-31 (Q13 distance equality).
+// The verdict only needs the closest hit near unocc: a hit farther than unocc + 1e-6 leaves the
+// point unlit whatever lies beyond it (so the search starts at that bound), and once any hit is
+// taken below unocc - 1e-6 the final one is nearer still (so the walk stops there). The margins
+// (1e-8 relative) cover the rounding between the walk's t and the distance of the transformed
+// hit point. The no-hit case keeps the reference's l = RN_INFINITY.
 template <uint32_t KINDS = KINDS_ALL>
 __device__ __forceinline__ bool illum_test_inl(const SceneView &S, V p_scene, V p_light, Counts &cnt) {
   double unocc = dist(p_light, p_scene);
   V d = normalize(p_scene - p_light);
   Hit h;
-  double l = scene_intersect<KINDS>(S, p_light, d, h) ? dist(p_light, h.p) : kInf;
+  // (only in scenes of rigid transforms: under a scaling node R3SceneNode's t rescale,
+  // R3SceneNode.cpp:449-458, is not the hit's distance, so no bound is derived from it)
+  const double mg = 1e-8 * fmax(1.0, unocc);
+  const int r = S.rigid ? scene_intersect_b<KINDS>(S, p_light, d, h, fmin(kInf, unocc + kEps + mg),
+                                                   unocc - kEps - mg)
+                        : scene_intersect_b<KINDS>(S, p_light, d, h, kInf, -1.0);
   cnt.shadow++;
+  if (r == 2) return false;
+  double l = (r == 1) ? dist(p_light, h.p) : kInf;
   return fabs(l - unocc) < kEps;
 }
 template <uint32_t KINDS = KINDS_ALL>

@@ -397,6 +397,18 @@ SceneView make_view(gi_ctx *c) {
   // the division-free element pre-test pays where soft lights cast many shadow rays (C3 jensen
   // +3 %) and costs where every light is hard (C2 cornell -2 %, r02 A/B); GI_ELEM_PRETEST=0/1
   S.elem_pretest = c->elem_pretest >= 0 ? c->elem_pretest : (S.hard_lights ? 0 : 1);
+  // rigid scene graph: every node's 3x3 part orthonormal (then R3SceneNode's t rescale stays 1
+  // and a hit's t is its world distance, which the bounded shadow walk relies on)
+  S.rigid = 1;
+  for (const DNode &nd : H.nodes) {
+    if (nd.identity) continue;
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) {
+        double g = nd.T[4 * 0 + i] * nd.T[4 * 0 + j] + nd.T[4 * 1 + i] * nd.T[4 * 1 + j] +
+                   nd.T[4 * 2 + i] * nd.T[4 * 2 + j];
+        if (std::fabs(g - (i == j ? 1.0 : 0.0)) > 1e-12) S.rigid = 0;
+      }
+  }
   S.radius = H.radius;
   for (int i = 0; i < 3; i++) {
     S.centroid[i] = H.centroid[i];

@@ -68,6 +68,11 @@ struct DElement {
   // only elements R3Intersects(ray, box) + the t <= closest rule would reject too (gi_device.h
   // elem_maybe_hit)
   double pmin[3], pmax[3];
+  // 1 when every shape is a triangle, sphere or circle: tests as cheap as the element's box
+  // test, so scene_intersect tests the shapes first and the box only for an element that would
+  // take a hit (same result: a box test that fails discards the element's hits either way)
+  int32_t shapes_first_ok;
+  int32_t pad;
 };
 
 constexpr int GI_MAX_DEPTH = 16;  // scene-graph depth supported on the device

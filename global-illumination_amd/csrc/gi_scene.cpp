@@ -590,7 +590,10 @@ static Bx flatten(Graph &G, int gi_idx, int parent, HostScene &S) {
     de.shape_first = (int)S.shapes.size();
     de.shape_count = (int)e.shapes.size();
     Bx eb;
+    de.shapes_first_ok = 1;
     for (auto &s : e.shapes) {
+      if (s.s.kind != SK_TRI && s.s.kind != SK_SPHERE && s.s.kind != SK_CIRCLE)
+        de.shapes_first_ok = 0;
       shape_box(s);
       DShape ds = s.s;
       ds.bvh_first = -1;

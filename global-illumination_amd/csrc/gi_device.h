@@ -372,19 +372,40 @@ __device__ __forceinline__ bool bvh_box(const DBvhNode &b, V o, V inv, double bo
 // minimum t over every triangle ray_tri accepts (t >= -1e-6, Q2), the same tie rule as the
 // file-order loop (equal t: lowest triangle index), visiting only boxes the ray meets below the
 // current minimum. Stackless pre-order walk with skip links.
+// hint: a triangle (global index into S.tris) tested before the walk -- the one the ray leaves
+// from. A ray leaving a mesh meets its own triangle at t ~ -1e-6 (Q2), and with that as the
+// current minimum the walk prunes to the boxes around the origin instead of every box the ray
+// crosses. The minimum over all triangles and its (t, index) tie rule do not depend on the order
+// the triangles are tested in, so the result is unchanged. Returns the winner's global index in
+// otri.
 __device__ __noinline__ bool ray_mesh_bvh(const SceneView &S, const DShape &sh, V o, V d, double &t,
-                                          V &p, V &n, double tmax) {
+                                          V &p, V &n, double tmax, int hint, int &otri) {
   const DBvhNode *B = S.bvh + sh.bvh_first;
   const DTri *T = S.tris + sh.tri_first;
   const V inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
   bool found = false;
   double mt = 3.40282346638528859811704183484516925440e+38;  // FLT_MAX, as the linear loop
   int32_t midx = 0x7fffffff;
+  int mpos = -1;
+  if (hint >= sh.tri_first && hint < sh.tri_first + sh.tri_count) {
+    const DTri &tr = S.tris[hint];
+    double tt;
+    V pp;
+    if (ray_tri(o, d, tr, tt, pp, tmax)) {
+      found = true;
+      p = pp;
+      n = ld3(tr.n);
+      mt = tt;
+      midx = tr.idx;
+      mpos = hint - sh.tri_first;
+    }
+  }
   const int end = B[0].skip;
   int i = 0;
   while (i < end) {
     const DBvhNode &nd = B[i];
-    if (!bvh_box(nd, o, inv, fmin(mt, tmax))) {
+    const double bound = fmin(mt, tmax);
+    if (!bvh_box(nd, o, inv, bound)) {
       i = nd.skip;
       continue;
     }
@@ -392,17 +413,20 @@ __device__ __noinline__ bool ray_mesh_bvh(const SceneView &S, const DShape &sh, 
       const DTri &tr = T[nd.tri_first + k];
       double tt;
       V pp;
-      if (ray_tri(o, d, tr, tt, pp, tmax) && (tt < mt || (tt == mt && tr.idx < midx))) {
+      // (a triangle beyond the current minimum cannot win: ray_tri stops after its plane test)
+      if (ray_tri(o, d, tr, tt, pp, fmin(mt, tmax)) && (tt < mt || (tt == mt && tr.idx < midx))) {
         found = true;
         p = pp;
         n = ld3(tr.n);
         mt = tt;
         midx = tr.idx;
+        mpos = nd.tri_first + k;
       }
     }
     i++;
   }
   t = mt;
+  otri = mpos >= 0 ? sh.tri_first + mpos : -1;
   return found;
 }
 
@@ -416,14 +440,19 @@ constexpr uint32_t KINDS_POLY = (1u << SK_TRI) | (1u << SK_SPHERE) | (1u << SK_M
 
 // R3Shape::Intersects dispatch (R3Shape.cpp:328-329); SK_MESH is R3Intersects(ray,
 // R3TriangleArray) (R3Isect.cpp:800-833): min t over ALL triangles, t >= -1e-6 allowed (Q2).
+// hint / otri: the triangle a ray leaves from (ray_mesh_bvh) and the triangle hit (global index
+// into S.tris, -1 for other shapes), passed on to the next bounce's walk
 template <uint32_t KINDS = KINDS_ALL>
 __device__ __forceinline__ bool shape_intersect(const SceneView &S, const DShape &sh, V o, V d,
-                                             double &t, V &p, V &n, double tmax = INFINITY) {
+                                             double &t, V &p, V &n, double tmax, int hint,
+                                             int &otri) {
+  otri = -1;
   if (KINDS == KINDS_TRI_SPHERE) {
     if (sh.kind == SK_TRI) {
       const DTri &tr = S.tris[sh.tri_first];
       if (!ray_tri(o, d, tr, t, p, tmax)) return false;
       n = ld3(tr.n);
+      otri = sh.tri_first;
       return true;
     }
     if (sh.kind == SK_SPHERE) return ray_sphere(o, d, ld3(sh.c), sh.r, t, p, n, tmax);
@@ -435,11 +464,12 @@ __device__ __forceinline__ bool shape_intersect(const SceneView &S, const DShape
       const DTri &tr = S.tris[sh.tri_first];
       if (!ray_tri(o, d, tr, t, p, tmax)) return false;
       n = ld3(tr.n);
+      otri = sh.tri_first;
       return true;
     }
     case SK_MESH: {
       if (!ray_box(o, d, sh.bmin, sh.bmax, nullptr, nullptr)) return false;
-      if (sh.bvh_first >= 0) return ray_mesh_bvh(S, sh, o, d, t, p, n, tmax);
+      if (sh.bvh_first >= 0) return ray_mesh_bvh(S, sh, o, d, t, p, n, tmax, hint, otri);
       bool found = false;
       double mt = 3.40282346638528859811704183484516925440e+38;  // FLT_MAX
       for (int i = 0; i < sh.tri_count; i++) {
@@ -452,6 +482,7 @@ __device__ __forceinline__ bool shape_intersect(const SceneView &S, const DShape
             p = pp;
             n = ld3(tr.n);
             mt = tt;
+            otri = sh.tri_first + i;
           }
         }
       }
@@ -493,6 +524,7 @@ struct Hit {
   V p, n;
   double t;
   int mat;
+  int tri;  // triangle hit (global index into SceneView::tris), -1 for other shapes
 };
 
 // R3Scene::Intersects (R3Scene.cpp:471-479) -> R3SceneNode::Intersects (R3SceneNode.cpp:
@@ -514,11 +546,11 @@ struct Hit {
 // t_init, 1 = hit in h.
 template <uint32_t KINDS = KINDS_ALL>
 __device__ __forceinline__ int scene_intersect_b(const SceneView &S, V org, V dir, Hit &h,
-                                                 double t_init, double t_exit) {
+                                                 double t_init, double t_exit, int hint = -1) {
   double closest = t_init;  // world-frame t (rigid transforms keep t; scale handled below)
   bool found = false;
   V hp = mk(0, 0, 0), hn = mk(0, 0, 0);
-  int hnode = 0, hmat = -1;
+  int hnode = 0, hmat = -1, htri = -1;
   for (int ni = 0; ni < S.nnodes; ni++) {
     const DNode &nd = S.nodes[ni];
     if (nd.elem_count == 0) continue;
@@ -556,14 +588,18 @@ __device__ __forceinline__ int scene_intersect_b(const SceneView &S, V org, V di
       if (!shapes_first && !box_pass()) continue;
       double ec = maxt;
       V ep = mk(0, 0, 0), en = mk(0, 0, 0);
+      int etri = -1;
       for (int si = 0; si < el.shape_count; si++) {
         double t;
         V p, n;
-        if (shape_intersect<KINDS>(S, S.shapes[el.shape_first + si], lo, ldir, t, p, n, ec)) {
+        int st;
+        if (shape_intersect<KINDS>(S, S.shapes[el.shape_first + si], lo, ldir, t, p, n, ec, hint,
+                                   st)) {
           if ((t >= 0.0) && (t <= ec)) {
             ep = p;
             en = n;
             ec = t;
+            etri = st;
           }
         }
       }
@@ -575,6 +611,7 @@ __device__ __forceinline__ int scene_intersect_b(const SceneView &S, V org, V di
       hn = en;
       hnode = ni;
       hmat = el.material;
+      htri = etri;
       if (closest < t_exit) return 2;
     }
   }
@@ -592,12 +629,15 @@ __device__ __forceinline__ int scene_intersect_b(const SceneView &S, V org, V di
   h.n = hn;
   h.t = closest;
   h.mat = hmat;
+  h.tri = htri;
   return 1;
 }
 
+// hint: the triangle the ray leaves from (the previous hit's Hit::tri), -1 for none
 template <uint32_t KINDS = KINDS_ALL>
-__device__ __forceinline__ bool scene_intersect(const SceneView &S, V org, V dir, Hit &h) {
-  return scene_intersect_b<KINDS>(S, org, dir, h, kInf, -1.0) == 1;
+__device__ __forceinline__ bool scene_intersect(const SceneView &S, V org, V dir, Hit &h,
+                                                int hint = -1) {
+  return scene_intersect_b<KINDS>(S, org, dir, h, kInf, -1.0, hint) == 1;
 }
 
 // ---------------------------------------------------------------------------------------

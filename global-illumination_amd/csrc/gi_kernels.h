@@ -23,7 +23,7 @@ struct Spawn {
   int32_t mat, hit;
   int32_t n_t, n_s, n_i;  // transmissive / specular / indirect sample counts
   int32_t q_glob, q_caus; // primary-hit photon-map queries (photon_viz / caustic)
-  int32_t pad;
+  int32_t tri;            // triangle hit (gi_device.h Hit::tri): the sample paths leave from it
 };
 
 // shading half of a photon-map query (search half is float4 {x, y, z, meta})
@@ -44,6 +44,8 @@ struct IndCont {
   uint32_t pslot, qslot;  // slot within the primary, global-query slot (~0: append)
   int32_t mat;
   uint32_t j;             // queries already issued by the path (mat == -1)
+  int32_t tri;            // triangle the continued ray leaves from (-1: none), Hit::tri
+  int32_t pad;
 };
 
 // continuation queue stripes: wave w appends to stripe w % IND_QS (one atomic per wave on a

@@ -103,6 +103,7 @@ __global__ __launch_bounds__(256) void primary_kernel(RenderArgs a) {
     V dir = normalize(far_point - org);
     Spawn sp;
     sp.hit = 0;
+    sp.tri = -1;
     sp.n_t = sp.n_s = sp.n_i = 0;
     sp.q_glob = sp.q_caus = 0;
     Hit h;
@@ -146,6 +147,7 @@ __global__ __launch_bounds__(256) void primary_kernel(RenderArgs a) {
       sp.ct = ct;
       sp.R = R;
       sp.mat = h.mat;
+      sp.tri = h.tri;
       sp.base[0] = color.r; sp.base[1] = color.g; sp.base[2] = color.b;
     }
     a.spawn[b] = sp;
@@ -204,6 +206,7 @@ struct PathCtx {
   C3 base;
   Counts cnt;
   int64_t fixed[2]; // deterministic query slot per list (>= 0), -1 append, -2 used
+  int hint;         // triangle the path's current ray leaves from (ray_mesh_bvh), -1 none
 };
 
 __device__ __forceinline__ void put_none(const RenderArgs &a, int list, int64_t slot) {
@@ -309,11 +312,12 @@ __device__ __forceinline__ bool diffuse_only(const DMaterial &m) {
 template <uint32_t KINDS = KINDS_ALL>
 __device__ __forceinline__ bool ind_bounce(PathCtx &P, V &org, V &dir, Rng &rng, C3 W, C3 &tw) {
   Hit h;
-  if (!scene_intersect<KINDS>(*P.S, org, dir, h)) {
+  if (!scene_intersect<KINDS>(*P.S, org, dir, h, P.hint)) {
     P.base += W * (tw * ldc(P.S->background));
     return false;
   }
   P.cnt.monte++;
+  P.hint = h.tri;
   return ind_shade<false>(P, h, org, dir, rng, W, tw);
 }
 
@@ -340,11 +344,12 @@ __device__ __forceinline__ void mc_path(PathCtx &P, V org, V dir, Rng &rng, C3 W
   V ray_start = org;
   for (int iter = 0; iter < F.max_monte_depth; iter++) {
     Hit h;
-    if (!scene_intersect<KINDS>(S, org, dir, h)) {
+    if (!scene_intersect<KINDS>(S, org, dir, h, P.hint)) {
       P.base += W * (tw * ldc(S.background));
       break;
     }
     P.cnt.monte++;
+    P.hint = h.tri;
     const DMaterial &m = S.mats[h.mat];
     C3 cb = rgb(0, 0, 0);
     if (F.ambient) cb += ldc(S.ambient);
@@ -401,6 +406,7 @@ __device__ __forceinline__ void mc_path(PathCtx &P, V org, V dir, Rng &rng, C3 W
           q.qslot = P.fixed[0] >= 0 ? (uint32_t)P.fixed[0] : 0xffffffffu;
           q.mat = -1;
           q.j = P.j;
+          q.tri = h.tri;
           P.fixed[0] = -2;  // the sub-path owns the global slot now
         } else {
           mc_indirect<KINDS>(P, h.p + s2 * kEps, s2, rng, w2);
@@ -479,6 +485,7 @@ __device__ __forceinline__ void path_init(PathCtx &P, const RenderArgs &a, int64
   Counts z = {0, 0, 0, 0, 0, 0};
   P.cnt = z;
   P.fixed[0] = P.fixed[1] = -1;
+  P.hint = -1;
 }
 
 __device__ __forceinline__ void path_stats(const RenderArgs &a, const Counts &cnt) {
@@ -549,6 +556,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void i
     PathCtx P;
     path_init(P, a, g, pb, pslot);
     P.fixed[0] = a.qind_base + t;  // at most one (global) query per indirect path
+    P.hint = sp.tri;
     Rng rng;
     rng.init(a.F.seed, KIND_IND, psample, (uint64_t)s);
     V p = ld3(sp.p), n = ld3(sp.n);
@@ -562,7 +570,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void i
       V org = p + sb * kEps, dir = sb;
       C3 tw = rgb(1, 1, 1);
       Hit h;
-      if (!scene_intersect<KINDS>(a.S, org, dir, h)) {
+      if (!scene_intersect<KINDS>(a.S, org, dir, h, sp.tri)) {
         P.base += Wt * (tw * ldc(a.S.background));
       } else {
         P.cnt.monte++;
@@ -593,6 +601,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void i
           q.pslot = (uint32_t)pslot;
           q.qslot = (uint32_t)P.fixed[0];
           q.mat = h.mat;
+          q.tri = h.tri;
           }
         }
       }
@@ -628,6 +637,7 @@ void ind_cont_kernel(RenderArgs a, const IndCont *queue, const uint32_t *fill, u
     PathCtx P;
     path_init(P, a, q.g, q.prim, (int)q.pslot);
     P.fixed[0] = (q.qslot == 0xffffffffu) ? -1 : (int64_t)q.qslot;
+    P.hint = q.tri;
     Rng rng;
     rng.key = q.rkey;
     rng.ctr = q.rctr;
@@ -641,6 +651,7 @@ void ind_cont_kernel(RenderArgs a, const IndCont *queue, const uint32_t *fill, u
       h.n = ld3(q.hn);
       h.t = 0.0;
       h.mat = q.mat;
+      h.tri = q.tri;
       go = ind_shade<false>(P, h, org, dir, rng, W, tw);
       iter0 = 1;
     } else {
@@ -692,6 +703,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(MC_WPE))) v
     double ct = sp.ct, R = sp.R;
     PathCtx P;
     path_init(P, a, g, pb, 1 + s);
+    P.hint = sp.tri;
     Rng rng;
     if (s < sp.n_t) {
       rng.init(F.seed, KIND_TRANS, psample, (uint64_t)s);
@@ -1260,9 +1272,11 @@ __device__ __noinline__ void photon_trace(const SceneView &S, const Flags &F, V 
                                           PhotonOut &o) {
   bool store = (!caustic && !F.fast_global);
   V ray_start = org;
+  int hint = -1;  // the triangle each bounce leaves from (ray_mesh_bvh)
   for (int iter = 0; iter < F.max_photon_depth; iter++) {
     Hit h;
-    if (!scene_intersect(S, org, dir, h)) break;
+    if (!scene_intersect(S, org, dir, h, hint)) break;
+    hint = h.tri;
     const DMaterial &m = S.mats[h.mat];
     V view = normalize(h.p - ray_start);
     double ct = dot(h.n, -view);

@@ -326,7 +326,13 @@ __device__ __forceinline__ void wave_estimate(const KnnArgs &a, int64_t qi, floa
 #ifndef WAVE_WPE
 #define WAVE_WPE 6  // fused query-per-wave kernel: occupancy target (80 VGPRs)
 #endif
-template <int CAP, int LB, bool PROF, bool FUSE>
+// Leaf sweep height (SWEEP instances): a subtree of at most 2^SWEEP_H leaves is not walked node
+// by node; its leaf boxes are read at once, one per lane, and the leaves within the bound are
+// scanned nearest first.
+#ifndef SWEEP_H
+#define SWEEP_H 6
+#endif
+template <int CAP, int LB, bool PROF, bool FUSE, bool SWEEP>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FUSE ? WAVE_WPE : 1)))
 void knn_wave_kernel(KnnArgs a) {
   __shared__ uint64_t buf[CAP];
@@ -366,141 +372,290 @@ void knn_wave_kernel(KnnArgs a) {
     uint32_t visited = 0;
     bool tight = false;
     if (prof) { pt = clock64(); pq = pt; }
-    if (a.map.dk && N > 0 && K > 0) {
-      // Start from a bound instead of r: for any photon p, d_K(q) <= |q - p| + d_K(p)
-      // (triangle inequality; the map's per-photon dk holds d_K(p)). The photons of the leaf
-      // containing q give a bound within a few percent of d_K(q), so the walk prunes to the
-      // K-neighbourhood from the first leaf on and the buffer rarely needs a select before
-      // the final one.
-      int node = 1;
-      while (node < L) {
-        KdNode nd = ld_node(a.map.nodes, node);
-        float qa = kd_axis_q(__float_as_int(nd.hi.w), qx, qy, qz);
-        node = 2 * node + ((qa - nd.lo.w >= 0.0f) ? 1 : 0);
-      }
-      int leaf = node - L;
-      int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
-      double best = INFINITY;
-      for (int64_t b = s0; b < s1; b += 64) {
-        int64_t ii = b + lane;
-        if (ii < s1) {
-          float4 p = pos[ii];
-          float dkp = a.map.dk[ii];
-          float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
-          float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
-          // fp32 metric -> true distance: 1e-5 relative margin
-          if (dkp < INFINITY) best = fmin(best, sqrt((double)d2 * (1.0 + 1e-5)) + (double)dkp);
-        }
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) best = fmin(best, __shfl_xor(best, o, 64));
-      if (best < INFINITY) {
-        double U = best * (1.0 + 1e-6) + 1e-12;
-        float U2 = __double2float_ru(U * U * (1.0 + 1e-5));
-        if (U2 < a.r2f) thr = ((uint64_t)__float_as_uint(U2) << 32) + 0x100000000ull;
-        tight = true;
-      }
-    }
-    // Traversal with a per-wave LDS stack: expanding a node loads both children's tight boxes
-    // (adjacent 32-B records, one scalar load) and pushes the far child with its box distance,
-    // so backtracking re-reads nothing from memory (the stackless walk re-read one parent per
-    // level climbed, each a dependent round trip). Near child = the smaller box distance; the
-    // visiting order does not change the result set.
-    if (N > 0) {
-      int sp = 0;
-      int node = 0;
-      {
-        KdNode r = ld_node(a.map.nodes, 1);
-        if (prof) pc[4]++;
-        if (kd_box_d2(r.lo, r.hi, qx, qy, qz) <= __uint_as_float((uint32_t)((thr - 1ull) >> 32)))
-          node = 1;
-      }
-      while (node) {
-        node = __builtin_amdgcn_readfirstlane(node);  // wave-uniform: scalar node loads
-        if (node < L) {
-          KdNode c0 = ld_node(a.map.nodes, 2 * node), c1 = ld_node(a.map.nodes, 2 * node + 1);
+    if (SWEEP) {
+      // Walk with leaf sweeps: nodes above sweep height are expanded near child first (both
+      // children's boxes in one scalar load, the far one pushed with its box distance); a node
+      // at sweep height has its <= 2^SWEEP_H leaf boxes read in one vector load (lane i: leaf
+      // i), and the leaves within the bound are scanned nearest first. The first leaf scanned
+      // (the nearest to q) also gives the start bound from the per-photon K-th distances (for
+      // any photon p: d_K(q) <= |q - p| + d_K(p)), computed from the same loads.
+      // The walk replaces the bottom SWEEP_H levels' dependent node loads (most of a query's
+      // node visits) by one round trip per subtree. The result set is order independent.
+      if (N > 0) {
+        const int levels = a.map.levels;
+        const KdNode *nodesv = reinterpret_cast<const KdNode *>(a.map.nodes);
+        bool need_dk = (a.map.dk != nullptr) && K > 0;
+        int sp = 0;
+        int node = 0;
+        {
+          KdNode r = ld_node(a.map.nodes, 1);
           if (prof) pc[4]++;
+          if (kd_box_d2(r.lo, r.hi, qx, qy, qz) <= __uint_as_float((uint32_t)((thr - 1ull) >> 32)))
+            node = 1;
+        }
+        while (true) {
           float pr = __uint_as_float((uint32_t)((thr - 1ull) >> 32));
-          float d0 = kd_box_d2(c0.lo, c0.hi, qx, qy, qz), d1 = kd_box_d2(c1.lo, c1.hi, qx, qy, qz);
-          int nn = 2 * node, fn = nn + 1;
-          if (d1 < d0) {
-            float t = d0; d0 = d1; d1 = t;
-            nn = fn; fn = 2 * node;
+          if (!node) {
+            while (sp > 0) {
+              sp--;
+              if (ffirst(sdist[sp]) <= pr) {
+                node = (int)ufirst(stk[sp]);
+                break;
+              }
+            }
+            if (!node) break;
           }
-          if (d1 <= pr) {
-            stk[sp] = (uint32_t)fn;  // every lane stores the same value: no cross-lane LDS hazard
-            sdist[sp] = d1;
-            sp++;
-          }
-          if (d0 <= pr) {
-            node = nn;
+          node = __builtin_amdgcn_readfirstlane(node);
+          const int h = levels - (31 - __clz(node));
+          if (h > SWEEP_H) {
+            KdNode c0 = ld_node(a.map.nodes, 2 * node), c1 = ld_node(a.map.nodes, 2 * node + 1);
+            if (prof) pc[4]++;
+            float d0 = kd_box_d2(c0.lo, c0.hi, qx, qy, qz), d1 = kd_box_d2(c1.lo, c1.hi, qx, qy, qz);
+            int nn = 2 * node, fn = nn + 1;
+            if (d1 < d0) {
+              float t = d0; d0 = d1; d1 = t;
+              nn = fn; fn = 2 * node;
+            }
+            if (d1 <= pr) {
+              stk[sp] = (uint32_t)fn;  // every lane stores the same value
+              sdist[sp] = d1;
+              sp++;
+            }
+            node = (d0 <= pr) ? nn : 0;
             continue;
           }
-        } else {
-          int leaf = node - L;
-          int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
-          visited += (uint32_t)(s1 - s0);
-          if (prof) { uint64_t n = clock64(); pc[0] += n - pt; pt = n; }
-          // the leaf's photons, LB batches of 64 loaded before any is used: one memory round
-          // trip per leaf instead of one per batch (a wave's traversal is a dependent chain,
-          // and ~7 waves per SIMD cannot hide a round trip per 64 photons)
-          for (int64_t base0 = s0; base0 < s1; base0 += 64 * LB) {
-            float4 pf[LB];
+          // sweep: leaf boxes of the 2^h leaves under node, lane i holding leaf i
+          const int nl = 1 << h;
+          const int lf0 = node << h;  // node index of the first leaf
+          float ldist = INFINITY;
+          if (lane < nl) {
+            KdNode b = nodesv[lf0 + lane];
+            ldist = kd_box_d2(b.lo, b.hi, qx, qy, qz);
+          }
+          if (prof) pc[4]++;
+          uint64_t lm = __ballot(ldist <= pr);
+          while (lm) {
+            pr = __uint_as_float((uint32_t)((thr - 1ull) >> 32));
+            const uint32_t cb = ((lm >> lane) & 1ull) ? __float_as_uint(ldist) : 0xffffffffu;
+            const uint32_t mn = wave_min_u32(cb);
+            if (__uint_as_float(mn) > pr) break;  // the rest are farther than the bound
+            const int li = __ffsll((long long)__ballot(cb == mn)) - 1;
+            lm &= ~(1ull << li);
+            const int leaf = lf0 + li - L;
+            int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
+            if (need_dk) {
+              need_dk = false;
+              double best = INFINITY;
+              for (int64_t b = s0; b < s1; b += 64) {
+                int64_t ii = b + lane;
+                if (ii < s1) {
+                  float4 p = pos[ii];
+                  float dkp = a.map.dk[ii];
+                  float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
+                  float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
+                  if (dkp < INFINITY) best = fmin(best, sqrt((double)d2 * (1.0 + 1e-5)) + (double)dkp);
+                }
+              }
 #pragma unroll
-            for (int u = 0; u < LB; u++) {
-              int64_t ii = base0 + u * 64 + lane;
-              pf[u] = pos[ii < s1 ? ii : s0];
+              for (int o = 32; o > 0; o >>= 1) best = fmin(best, __shfl_xor(best, o, 64));
+              if (best < INFINITY) {
+                double U = best * (1.0 + 1e-6) + 1e-12;
+                float U2 = __double2float_ru(U * U * (1.0 + 1e-5));
+                if (U2 < a.r2f) thr = ((uint64_t)__float_as_uint(U2) << 32) + 0x100000000ull;
+                tight = true;
+              }
             }
+            visited += (uint32_t)(s1 - s0);
+            if (prof) { uint64_t n = clock64(); pc[0] += n - pt; pt = n; }
+            for (int64_t base0 = s0; base0 < s1; base0 += 64 * LB) {
+              float4 pf[LB];
 #pragma unroll
-            for (int u = 0; u < LB; u++) {
-            const int64_t base = base0 + u * 64;
-            if (base >= s1) break;
-            int64_t ii = base + lane;
-            uint64_t key = ~0ull;
-            if (ii < s1) {
-              float4 p = pf[u];
-              float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
-              float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
-              key = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)(uint32_t)ii;
-            }
-            bool pass = key < thr;
-            uint64_t m = __ballot(pass);
-            uint32_t nnew = (uint32_t)__popcll(m);
-            if (nnew == 0) continue;
-            if (count + nnew > (uint32_t)CAP) {
-              if (prof) { uint64_t n = clock64(); pc[1] += n - pt; pt = n; pc[3]++; }
-              select_k<CAP>(buf, hist, lane, count, K, thr);
-              if (prof) { uint64_t n = clock64(); pc[2] += n - pt; pt = n; }
-              pass = key < thr;
-              m = __ballot(pass);
-              nnew = (uint32_t)__popcll(m);
+              for (int u = 0; u < LB; u++) {
+                int64_t ii = base0 + u * 64 + lane;
+                pf[u] = pos[ii < s1 ? ii : s0];
+              }
+#pragma unroll
+              for (int u = 0; u < LB; u++) {
+              const int64_t base = base0 + u * 64;
+              if (base >= s1) break;
+              int64_t ii = base + lane;
+              uint64_t key = ~0ull;
+              if (ii < s1) {
+                float4 p = pf[u];
+                float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
+                float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
+                key = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)(uint32_t)ii;
+              }
+              bool pass = key < thr;
+              uint64_t m = __ballot(pass);
+              uint32_t nnew = (uint32_t)__popcll(m);
               if (nnew == 0) continue;
+              if (count + nnew > (uint32_t)CAP) {
+                if (prof) { uint64_t n = clock64(); pc[1] += n - pt; pt = n; pc[3]++; }
+                select_k<CAP>(buf, hist, lane, count, K, thr);
+                if (prof) { uint64_t n = clock64(); pc[2] += n - pt; pt = n; }
+                pass = key < thr;
+                m = __ballot(pass);
+                nnew = (uint32_t)__popcll(m);
+                if (nnew == 0) continue;
+              }
+              if (pass) {
+                uint32_t off = count + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                buf[off] = key;
+              }
+              count += nnew;
+              __syncthreads();
+              }
             }
-            if (pass) {
-              uint32_t off = count + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-              buf[off] = key;
-            }
-            count += nnew;
-            __syncthreads();
+            // first time K candidates are held: select now so the prune bound tightens from
+            // r^2 to the K-th distance early (otherwise it stays r^2 until the buffer fills)
+            if (prof) { uint64_t n = clock64(); pc[1] += n - pt; pt = n; }
+            if (K > 0 && count >= (uint32_t)K + (tight ? (uint32_t)a.sel_slack : 0u)) {
+              select_k<CAP>(buf, hist, lane, count, K, thr);
+              tight = true;
+              if (prof) { uint64_t n = clock64(); pc[2] += n - pt; pt = n; pc[3]++; }
             }
           }
-          // first time K candidates are held: select now so the prune bound tightens from
-          // r^2 to the K-th distance early (otherwise it stays r^2 until the buffer fills)
-          if (prof) { uint64_t n = clock64(); pc[1] += n - pt; pt = n; }
-          if (K > 0 && count >= (uint32_t)K + (tight ? (uint32_t)a.sel_slack : 0u)) {
-            select_k<CAP>(buf, hist, lane, count, K, thr);
-            tight = true;
-            if (prof) { uint64_t n = clock64(); pc[2] += n - pt; pt = n; pc[3]++; }
+          node = 0;
+        }
+      }
+    } else {
+    if (a.map.dk && N > 0 && K > 0) {
+        // Start from a bound instead of r: for any photon p, d_K(q) <= |q - p| + d_K(p)
+        // (triangle inequality; the map's per-photon dk holds d_K(p)). The photons of the leaf
+        // containing q give a bound within a few percent of d_K(q), so the walk prunes to the
+        // K-neighbourhood from the first leaf on and the buffer rarely needs a select before
+        // the final one.
+        int node = 1;
+        while (node < L) {
+          KdNode nd = ld_node(a.map.nodes, node);
+          float qa = kd_axis_q(__float_as_int(nd.hi.w), qx, qy, qz);
+          node = 2 * node + ((qa - nd.lo.w >= 0.0f) ? 1 : 0);
+        }
+        int leaf = node - L;
+        int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
+        double best = INFINITY;
+        for (int64_t b = s0; b < s1; b += 64) {
+          int64_t ii = b + lane;
+          if (ii < s1) {
+            float4 p = pos[ii];
+            float dkp = a.map.dk[ii];
+            float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
+            float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
+            // fp32 metric -> true distance: 1e-5 relative margin
+            if (dkp < INFINITY) best = fmin(best, sqrt((double)d2 * (1.0 + 1e-5)) + (double)dkp);
           }
         }
-        // pop the nearest pending subtree still within the (possibly tightened) bound
-        node = 0;
-        float pr = __uint_as_float((uint32_t)((thr - 1ull) >> 32));
-        while (sp > 0) {
-          sp--;
-          if (ffirst(sdist[sp]) <= pr) {  // uniform: keeps the walk in scalar registers
-            node = (int)ufirst(stk[sp]);
-            break;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) best = fmin(best, __shfl_xor(best, o, 64));
+        if (best < INFINITY) {
+          double U = best * (1.0 + 1e-6) + 1e-12;
+          float U2 = __double2float_ru(U * U * (1.0 + 1e-5));
+          if (U2 < a.r2f) thr = ((uint64_t)__float_as_uint(U2) << 32) + 0x100000000ull;
+          tight = true;
+        }
+      }
+      // Traversal with a per-wave LDS stack: expanding a node loads both children's tight boxes
+      // (adjacent 32-B records, one scalar load) and pushes the far child with its box distance,
+      // so backtracking re-reads nothing from memory (the stackless walk re-read one parent per
+      // level climbed, each a dependent round trip). Near child = the smaller box distance; the
+      // visiting order does not change the result set.
+      if (N > 0) {
+        int sp = 0;
+        int node = 0;
+        {
+          KdNode r = ld_node(a.map.nodes, 1);
+          if (prof) pc[4]++;
+          if (kd_box_d2(r.lo, r.hi, qx, qy, qz) <= __uint_as_float((uint32_t)((thr - 1ull) >> 32)))
+            node = 1;
+        }
+        while (node) {
+          node = __builtin_amdgcn_readfirstlane(node);  // wave-uniform: scalar node loads
+          if (node < L) {
+            KdNode c0 = ld_node(a.map.nodes, 2 * node), c1 = ld_node(a.map.nodes, 2 * node + 1);
+            if (prof) pc[4]++;
+            float pr = __uint_as_float((uint32_t)((thr - 1ull) >> 32));
+            float d0 = kd_box_d2(c0.lo, c0.hi, qx, qy, qz), d1 = kd_box_d2(c1.lo, c1.hi, qx, qy, qz);
+            int nn = 2 * node, fn = nn + 1;
+            if (d1 < d0) {
+              float t = d0; d0 = d1; d1 = t;
+              nn = fn; fn = 2 * node;
+            }
+            if (d1 <= pr) {
+              stk[sp] = (uint32_t)fn;  // every lane stores the same value: no cross-lane LDS hazard
+              sdist[sp] = d1;
+              sp++;
+            }
+            if (d0 <= pr) {
+              node = nn;
+              continue;
+            }
+          } else {
+            int leaf = node - L;
+            int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
+            visited += (uint32_t)(s1 - s0);
+            if (prof) { uint64_t n = clock64(); pc[0] += n - pt; pt = n; }
+            // the leaf's photons, LB batches of 64 loaded before any is used: one memory round
+            // trip per leaf instead of one per batch (a wave's traversal is a dependent chain,
+            // and ~7 waves per SIMD cannot hide a round trip per 64 photons)
+            for (int64_t base0 = s0; base0 < s1; base0 += 64 * LB) {
+              float4 pf[LB];
+#pragma unroll
+              for (int u = 0; u < LB; u++) {
+                int64_t ii = base0 + u * 64 + lane;
+                pf[u] = pos[ii < s1 ? ii : s0];
+              }
+#pragma unroll
+              for (int u = 0; u < LB; u++) {
+              const int64_t base = base0 + u * 64;
+              if (base >= s1) break;
+              int64_t ii = base + lane;
+              uint64_t key = ~0ull;
+              if (ii < s1) {
+                float4 p = pf[u];
+                float dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
+                float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
+                key = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)(uint32_t)ii;
+              }
+              bool pass = key < thr;
+              uint64_t m = __ballot(pass);
+              uint32_t nnew = (uint32_t)__popcll(m);
+              if (nnew == 0) continue;
+              if (count + nnew > (uint32_t)CAP) {
+                if (prof) { uint64_t n = clock64(); pc[1] += n - pt; pt = n; pc[3]++; }
+                select_k<CAP>(buf, hist, lane, count, K, thr);
+                if (prof) { uint64_t n = clock64(); pc[2] += n - pt; pt = n; }
+                pass = key < thr;
+                m = __ballot(pass);
+                nnew = (uint32_t)__popcll(m);
+                if (nnew == 0) continue;
+              }
+              if (pass) {
+                uint32_t off = count + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                buf[off] = key;
+              }
+              count += nnew;
+              __syncthreads();
+              }
+            }
+            // first time K candidates are held: select now so the prune bound tightens from
+            // r^2 to the K-th distance early (otherwise it stays r^2 until the buffer fills)
+            if (prof) { uint64_t n = clock64(); pc[1] += n - pt; pt = n; }
+            if (K > 0 && count >= (uint32_t)K + (tight ? (uint32_t)a.sel_slack : 0u)) {
+              select_k<CAP>(buf, hist, lane, count, K, thr);
+              tight = true;
+              if (prof) { uint64_t n = clock64(); pc[2] += n - pt; pt = n; pc[3]++; }
+            }
+          }
+          // pop the nearest pending subtree still within the (possibly tightened) bound
+          node = 0;
+          float pr = __uint_as_float((uint32_t)((thr - 1ull) >> 32));
+          while (sp > 0) {
+            sp--;
+            if (ffirst(sdist[sp]) <= pr) {  // uniform: keeps the walk in scalar registers
+              node = (int)ufirst(stk[sp]);
+              break;
+            }
           }
         }
       }
@@ -879,14 +1034,20 @@ void launch_list_estimate(const KnnArgs &a, hipStream_t st) {
 #ifndef WAVE_LB
 #define WAVE_LB 1  // leaf batches of 64 photons loaded together by the 512/1024 instances
 #endif
-template <bool PROF, bool FUSE>
+template <bool PROF, bool FUSE, bool SWEEP>
 bool wave_launch(const KnnArgs &a, int need, unsigned grid, hipStream_t st) {
-  if (need <= 128) knn_wave_kernel<128, 1, PROF, FUSE><<<grid, 64, 0, st>>>(a);
-  else if (need <= 256) knn_wave_kernel<256, 1, PROF, FUSE><<<grid, 64, 0, st>>>(a);
-  else if (need <= 512) knn_wave_kernel<512, WAVE_LB, PROF, FUSE><<<grid, 64, 0, st>>>(a);
-  else if (need <= 1024) knn_wave_kernel<1024, WAVE_LB, PROF, FUSE><<<grid, 64, 0, st>>>(a);
+  if (need <= 128) knn_wave_kernel<128, 1, PROF, FUSE, SWEEP><<<grid, 64, 0, st>>>(a);
+  else if (need <= 256) knn_wave_kernel<256, 1, PROF, FUSE, SWEEP><<<grid, 64, 0, st>>>(a);
+  else if (need <= 512) knn_wave_kernel<512, WAVE_LB, PROF, FUSE, SWEEP><<<grid, 64, 0, st>>>(a);
+  else if (need <= 1024) knn_wave_kernel<1024, WAVE_LB, PROF, FUSE, SWEEP><<<grid, 64, 0, st>>>(a);
   else return false;
   return true;
+}
+template <bool PROF, bool FUSE>
+bool wave_launch(const KnnArgs &a, int need, unsigned grid, hipStream_t st) {
+  // GI_KNN_DBG & 1024: the node-by-node walk (A/B measurements)
+  return (a.dbg & 1024) ? wave_launch<PROF, FUSE, false>(a, need, grid, st)
+                        : wave_launch<PROF, FUSE, true>(a, need, grid, st);
 }
 
 bool launch_knn_wave(const KnnArgs &a, int cap_mul, hipStream_t st) {

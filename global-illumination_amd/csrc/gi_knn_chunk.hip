@@ -236,8 +236,7 @@ struct ChunkProf {
 // Wave-uniform walk over every kd leaf whose node box passes boxd(node) <= bound, with a
 // per-wave LDS stack (stk, >= tree depth entries): an expansion reads both children's boxes
 // (scalar loads, ld_node) and pushes one, so backtracking reads nothing from memory. leaf(l)
-// returns true to stop the walk. The visiting order does not matter to the callers (they
-// collect every photon within a fixed bound). Returns the number of node records read.
+// returns true to stop the walk. Returns the number of node records read.
 //
 // WALK2: an expansion whose children are internal also reads the four grandchildren (128
 // contiguous bytes, issued with the children's 64): two levels per dependent round trip. A
@@ -245,21 +244,46 @@ struct ChunkProf {
 // would take it, and the in-grandchildren are pushed right to left, so leaves are still visited
 // left to right: the callers' LDS candidate order, and so every estimate sum, is unchanged.
 // Stack: at most three entries per two levels.
+//
+// Leaf sweep: a node with at most 2^CHUNK_SWEEP_H leaves below it is not expanded further; its
+// leaf boxes are read in one vector load (lane i: leaf i) and the passing leaves are visited in
+// index order. A leaf's tight box lies inside every ancestor's and boxd is monotone under
+// containment (the same fp operation sequence, every rounding monotone), so the leaves that
+// pass are exactly those the node-by-node walk reaches, in the same left-to-right order: the
+// candidate order, and every result, are unchanged; the bottom levels' dependent node loads
+// become one round trip per subtree.
 #ifndef WALK2
 #define WALK2 1
+#endif
+#ifndef CHUNK_SWEEP_H
+#define CHUNK_SWEEP_H 6
 #endif
 template <typename BoxD, typename Leaf>
 __device__ __forceinline__ uint32_t walk_within(const float *nodes, int L, float bound, uint32_t *stk,
                                                 BoxD boxd, Leaf leaf, int root = 1) {
+  const int levels = 31 - __clz(L);
+  const int lane = threadIdx.x & 63;
   uint32_t reads = 1;
   int sp = 0;
   int node = (boxd(ld_node(nodes, root)) <= bound) ? root : 0;
   while (node) {
     node = __builtin_amdgcn_readfirstlane(node);
-    if (node < L) {
+    const int h = levels - (31 - __clz(node));
+    if (h <= CHUNK_SWEEP_H) {
+      const int lf0 = node << h;
+      bool in = false;
+      if (lane < (1 << h)) in = boxd(reinterpret_cast<const KdNode *>(nodes)[lf0 + lane]) <= bound;
+      reads += 1u << h;
+      uint64_t m = __ballot(in);
+      while (m) {
+        const int li = __ffsll((long long)m) - 1;
+        m &= m - 1ull;
+        if (leaf(lf0 + li - L)) return reads;
+      }
+    } else {
       const int c = 2 * node;
       KdNode c0 = ld_node(nodes, c), c1 = ld_node(nodes, c + 1);
-      if (WALK2 && c < L) {
+      if (WALK2 && h > CHUNK_SWEEP_H + 1) {
         KdNode g0 = ld_node(nodes, 2 * c), g1 = ld_node(nodes, 2 * c + 1);
         KdNode g2 = ld_node(nodes, 2 * c + 2), g3 = ld_node(nodes, 2 * c + 3);
         reads += 6;
@@ -282,8 +306,6 @@ __device__ __forceinline__ uint32_t walk_within(const float *nodes, int L, float
         if (in0) { node = c; continue; }
         if (in1) { node = c + 1; continue; }
       }
-    } else if (leaf(node - L)) {
-      return reads;
     }
     node = 0;
     if (sp > 0) {

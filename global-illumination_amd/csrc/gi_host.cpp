@@ -261,13 +261,6 @@ struct gi_ctx {
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;     // side stream: Monte Carlo paths beside the indirect paths
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;  // caustic k-NN on the side stream
-  bool overlap_mc = true;
-  bool overlap_maps = false;        // caustic k-NN on the side stream beside the global k-NN
-                                    // (GI_OVERLAP_MAPS=1; r02: equal frame time either way, and
-                                    // alone each map's kernels are timed without the other's)
-  bool fork_after_sort = true;      // ... forked after the global queries' Morton sort (a radix
-                                    // sort pass co-running with the caustic kernels stalled)
   MapExec mx[2];
   std::string err;
   gi_params P;
@@ -285,7 +278,7 @@ struct gi_ctx {
   KdBuildScratch kdb;            // its scratch
   DBuf kd_ph;                    // emission-ordered photons uploaded for the device build
   int wave_cap_mul = 1;
-  int chunk_cap_big = 512;        // large-K chunk kernel: the same (384 or 512)
+  int chunk_cap_big = 512;        // large-K chunk kernel: LDS candidates of the first pass
   int chunk_minsub_big = 64;      // large-K chunk kernel: overflowing chunks retried down to this (64: none, measured best)
   int chunk_minsub = 32;          // chunk kernel: overflowing chunks retried as halves (measured best with the dk bound)
   double fb_ms[2] = {0, 0};       // final fallback kernel's time and queries per map (since the
@@ -330,7 +323,6 @@ struct gi_ctx {
   int64_t prim_per_batch = 1 << 21;
   int64_t query_budget = 400000000;  // photon-map queries per batch (~120 B each: ~48 GB)
   double q_per_prim = 0.0;           // largest queries per primary sample seen so far
-  bool sort_queries = true;
   float sbmin[3] = {0, 0, 0}, sbmax[3] = {1, 1, 1};
 };
 
@@ -1036,18 +1028,15 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
 }
 
 // run the k-NN estimate of one query list into out[slot] (Morton-ordered launch)
-// (perm: the Morton order when the caller already sorted this list, else null)
 int knn_list(gi_ctx *c, int mi, const float4 *qpos, const QShade *qshade, int64_t nq,
-             double *out, double *ms, uint32_t *perm_in = nullptr) {
+             double *out, double *ms) {
   MapExec &X = c->mx[mi];
   KnnArgs k = knn_args(c, mi);
   k.qpos = qpos;
   k.qshade = qshade;
   k.out = out;
   k.nq = nq;
-  if (perm_in) {
-    k.perm = perm_in;
-  } else if (c->sort_queries) {
+  {
     uint32_t *perm = nullptr;
     HIPCHK(c, morton_order(qpos, nq, c->sbmin, c->sbmax, X.sorter, &perm, X.st));
     k.perm = perm;
@@ -1187,7 +1176,7 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
       }
       a.qcount = c->qcount.as<uint32_t>();
       HIPCHK(c, hipMemcpyAsync(c->qcount.p, qbase, 8, hipMemcpyHostToDevice, c->stream));
-      launch_path(a, c->stream, c->overlap_mc ? c->stream2 : nullptr, c->ev_fork, c->ev_join);
+      launch_path(a, c->stream, c->stream2, c->ev_fork, c->ev_join);
       HIPCHK(c, hipGetLastError());
       HIPCHK(c, hipMemcpyAsync(nq, c->qcount.p, 8, hipMemcpyDeviceToHost, c->stream));
       uint32_t fills[IND_QS * 32];
@@ -1227,56 +1216,14 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
           run[l] = true;
       }
     }
-    // The two maps' estimates are independent (own query lists, maps and outputs): the caustic
-    // one runs in a worker thread on the side stream while this thread drives the global one,
-    // so each map's low-occupancy phases (fallbacks, second chunk pass) overlap the other's
-    // kernels. Each map has its own stream, events and scratch (MapExec).
-    const bool side = c->overlap_maps && c->stream2 && run[0] && run[1];
+    // the two maps' estimates, one after the other on the render stream (running the caustic
+    // one in a worker thread on a second stream measured no faster: r02)
     int rcm[2] = {GI_OK, GI_OK};
-    std::thread worker;
-    // The global list's Morton sort runs before the fork: onesweep radix passes wait on their
-    // predecessor blocks (decoupled look-back), and beside the caustic k-NN kernels one pass
-    // took ~150 ms instead of ~4 ms (profiles/r02 kernel trace).
-    // The caustic list is sorted there too (its kernels then start beside the global chunk
-    // kernel, not beside a sort).
-    uint32_t *mperm[2] = {nullptr, nullptr};
-    if (side && c->fork_after_sort && c->sort_queries) {
-      if (!c->P.irradiance_cache)
-        HIPCHK(c, morton_order(a.qpos[0], nq[0], c->sbmin, c->sbmax, c->mx[0].sorter, &mperm[0], c->stream));
-      HIPCHK(c, morton_order(a.qpos[1], nq[1], c->sbmin, c->sbmax, c->mx[1].sorter, &mperm[1], c->stream));
-    }
-    if (side) {
-      HIPCHK(c, hipEventRecord(c->ev_fork2, c->stream));
-      HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork2, 0));
-      c->mx[1].st = c->stream2;
-      worker = std::thread([&]() {
-        if (hipSetDevice(c->device) != hipSuccess) {  // the current device is per host thread
-          rcm[1] = fail(c, GI_ERR_HIP, "k-NN worker: hipSetDevice failed");
-          return;
-        }
-        try {
-          rcm[1] = knn_list(c, 1, a.qpos[1], a.qshade[1], nq[1], c->qout[1].as<double>(),
-                            rs ? &knn_ms[1] : nullptr, mperm[1]);
-        } catch (const std::bad_alloc &) {
-          rcm[1] = fail(c, GI_ERR_ALLOC, "k-NN worker: host allocation failed");
-        } catch (...) {
-          rcm[1] = fail(c, GI_ERR_HIP, "k-NN worker: unexpected exception");
-        }
-      });
-    }
     for (int l = 0; l < 2; l++) {
-      if (!run[l] || (side && l == 1)) continue;
+      if (!run[l]) continue;
       rcm[l] = knn_list(c, l, a.qpos[l], a.qshade[l], nq[l], c->qout[l].as<double>(),
-                        rs ? &knn_ms[l] : nullptr, mperm[l]);
+                        rs ? &knn_ms[l] : nullptr);
       if (rcm[l]) break;
-    }
-    if (side) {
-      worker.join();
-      c->mx[1].st = c->stream;
-      if (rcm[1] == GI_OK) {
-        HIPCHK(c, hipEventRecord(c->ev_join2, c->stream2));
-        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join2, 0));
-      }
     }
     for (int l = 0; l < 2; l++) {
       if (rcm[l]) return rcm[l];
@@ -1389,8 +1336,6 @@ int gi_create(gi_ctx **out, int dev) {
   if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) c->stream2 = nullptr;
   hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
   hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
-  hipEventCreateWithFlags(&c->ev_fork2, hipEventDisableTiming);
-  hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming);
   for (int m = 0; m < 2; m++) {
     c->mx[m].st = c->stream;
     hipEventCreate(&c->mx[m].ev0);
@@ -1410,28 +1355,16 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_QUERY_BUDGET")) c->query_budget = std::max(1LL, atoll(s));
   // tuning knobs (measurement only; defaults are the measured best)
   if (const char *s = getenv("GI_LEAF_SIZE")) c->leaf_size[0] = c->leaf_size[1] = std::max(1, atoi(s));
-  if (const char *s = getenv("GI_LEAF_SIZE_C")) c->leaf_size[1] = std::max(1, atoi(s));
   if (const char *s = getenv("GI_KD_BUILD")) c->gpu_kd = strcmp(s, "host") != 0;
-  if (const char *s = getenv("GI_WAVE_CAP_MUL")) c->wave_cap_mul = std::max(1, atoi(s));
-  if (const char *s = getenv("GI_SEL_SLACK")) c->sel_slack = std::max(1, atoi(s));
-  if (const char *s = getenv("GI_CHUNK_CAP_BIG")) c->chunk_cap_big = atoi(s) <= 384 ? 384 : 512;
   if (const char *s = getenv("GI_CHUNK_MINSUB_BIG")) c->chunk_minsub_big = std::min(64, std::max(1, atoi(s)));
   if (const char *s = getenv("GI_CHUNK_MINSUB")) c->chunk_minsub = std::min(64, std::max(1, atoi(s)));
-  if (const char *s = getenv("GI_IND_WAVES")) c->ind_waves = std::max(1, atoi(s));
   if (const char *s = getenv("GI_SPLIT_IND")) c->split_ind = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_DK")) c->use_dk = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_DK")) c->chunk_dk = atoi(s) != 0;
-  if (const char *s = getenv("GI_CHUNK_BIG2")) c->chunk_big2 = atoi(s) != 0;
-  if (const char *s = getenv("GI_CHUNK_LANE2")) c->chunk_lane2 = atoi(s) != 0;
-  if (const char *s = getenv("GI_CHUNK_MINSUB_BIG2")) c->chunk_minsub_big2 = std::min(64, std::max(1, atoi(s)));
-  if (const char *s = getenv("GI_OVERLAP_MC")) c->overlap_mc = atoi(s) != 0;
-  if (const char *s = getenv("GI_OVERLAP_MAPS")) c->overlap_maps = atoi(s) != 0;
-  if (const char *s = getenv("GI_FORK_AFTER_SORT")) c->fork_after_sort = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_LOG")) c->knn_log = atoi(s) != 0;
   if (const char *s = getenv("GI_ELEM_PRETEST")) c->elem_pretest = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_FB_ALL")) c->chunk_fb_all = atoi(s) != 0;
   if (const char *s = getenv("GI_IND_FRAC")) c->ind_frac = std::min(1.0, std::max(1e-6, atof(s)));
-  if (const char *s = getenv("GI_SORT_QUERIES")) c->sort_queries = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_KERNEL")) c->knn_kernel_kind = atoi(s);
   *out = c;
   return GI_OK;
@@ -1514,8 +1447,6 @@ void gi_destroy(gi_ctx *c) {
   c->kdb.release();
   c->kd_ph.release();
   if (c->ev_fork) hipEventDestroy(c->ev_fork);
-  if (c->ev_fork2) hipEventDestroy(c->ev_fork2);
-  if (c->ev_join2) hipEventDestroy(c->ev_join2);
   if (c->ev_join) hipEventDestroy(c->ev_join);
   if (c->stream2) hipStreamDestroy(c->stream2);
   if (c->stream) hipStreamDestroy(c->stream);

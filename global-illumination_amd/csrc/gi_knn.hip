@@ -704,7 +704,7 @@ void knn_wave_kernel(KnnArgs a) {
 }
 
 // the estimate over the K-best lists written by knn_wave_kernel in list mode (kept for
-// GI_WAVE_FUSE=0 and the group kernel); split from the search so the search kernel keeps a
+// the group kernel); split from the search so the search kernel keeps a
 // small register footprint
 __global__ __launch_bounds__(64) void knn_list_estimate_kernel(KnnArgs a) {
   const int K = a.K;
@@ -1055,11 +1055,10 @@ bool launch_knn_wave(const KnnArgs &a, int cap_mul, hipStream_t st) {
   int need = (a.K + 64) * cap_mul;
   int64_t grid = a.nq < (1 << 16) ? a.nq : (1 << 16);
   // GI_KNN_DBG & 16 selects the instance with phase cycle counters
-  // the estimate fused into the search (GI_WAVE_FUSE=0: lists + knn_list_estimate_kernel)
-  static const bool fuse = getenv("GI_WAVE_FUSE") ? atoi(getenv("GI_WAVE_FUSE")) != 0 : true;
+  // the estimate fused into the search (list and dk modes write lists / bounds instead)
   const bool est = a.mode != KNN_MODE_LIST && a.mode != KNN_MODE_DK;
   bool ok;
-  if (est && fuse) {
+  if (est) {
     ok = (a.dbg & 16) ? wave_launch<true, true>(a, need, (unsigned)grid, st)
                       : wave_launch<false, true>(a, need, (unsigned)grid, st);
   } else {
@@ -1067,7 +1066,6 @@ bool launch_knn_wave(const KnnArgs &a, int cap_mul, hipStream_t st) {
                       : wave_launch<false, false>(a, need, (unsigned)grid, st);
   }
   if (!ok) return false;
-  if (est && !fuse) knn_list_estimate_kernel<<<(unsigned)grid, 64, 0, st>>>(a);
   return true;
 }
 

@@ -53,8 +53,8 @@ hipError_t morton_order(const float4 *q, int64_t n, const float bmin[3], const f
   if ((e = grow(s.k1, s.k1_cap, b4)) != hipSuccess) return e;
   if ((e = grow(s.v0, s.v0_cap, b4)) != hipSuccess) return e;
   if ((e = grow(s.v1, s.v1_cap, b4)) != hipSuccess) return e;
-  // cells per axis 2^bits (GI_MORTON_BITS, 8..10): the radix sort runs ceil(3 bits / 8) passes
-  static const int bits = getenv("GI_MORTON_BITS") ? std::min(10, std::max(8, atoi(getenv("GI_MORTON_BITS")))) : 10;
+  // 2^10 cells per axis: a 30-bit code, four 8-bit radix passes
+  constexpr int bits = 10;
   const float cmax = (float)((1 << bits) - 1);
   float sc[3];
   for (int i = 0; i < 3; i++) {

@@ -34,7 +34,7 @@ VARIANTS = [
     {"GI_KNN_KERNEL": "7", "GI_CHUNK_DK": "0"},
     {"GI_KNN_KERNEL": "7", "GI_CHUNK_FB_ALL": "1", "GI_KNN_DK": "0"},
     {"GI_KNN_KERNEL": "8"},
-    {"GI_KNN_KERNEL": "8", "GI_CHUNK_CAP_BIG": "384", "GI_LEAF_SIZE": "128"},
+    {"GI_KNN_KERNEL": "8", "GI_LEAF_SIZE": "128"},
     {"GI_KNN_KERNEL": "8", "GI_CHUNK_MINSUB_BIG": "1"},
 ]
 

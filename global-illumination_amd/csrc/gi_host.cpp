@@ -297,7 +297,9 @@ struct gi_ctx {
   DBuf ind_cont, ind_ncont;       // indirect paths that continue past their first bounce
   DBuf mc_cont, mc_ncont;         // Monte Carlo paths' indirect sub-paths
   DBuf prim_rgb;                  // per-primary sums of the reduction
-  DBuf ind_tab, mc_tab;           // path owner tables (owner of path 64k)
+  DBuf ind_tab, mc_tab;           // row -> tile of the tiled indirect entries; owner of MC path 64k
+  DBuf ind_trows, ind_rows;       // indirect paths' tiled slots: rows per tile, their scan
+  DBuf ind_masks;                 // their rows' query and base masks
   bool split_ind = true;          // continuation queue for indirect paths (else one loop per lane)
   double ind_frac = 0.25;         // continuation queue size, as a fraction of its worst case
   // render scratch
@@ -1122,22 +1124,39 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     a.total_mc = totals[1];
     a.total_ind = totals[2];
     // owner tables: the path kernels find their waves' primary sample in one load
-    if (a.total_ind > 0) {
-      HIPCHK(c, c->ind_tab.ensure(((size_t)a.total_ind / 64 + 2) * 4));
-      launch_owner_table(c->ind_off.as<uint32_t>(), nprim, c->ind_tab.as<uint32_t>(), c->stream);
-      a.ind_tab = c->ind_tab.as<uint32_t>();
-    }
     if (a.total_mc > 0) {
       HIPCHK(c, c->mc_tab.ensure(((size_t)a.total_mc / 64 + 2) * 4));
       launch_owner_table(c->mc_off.as<uint32_t>(), nprim, c->mc_tab.as<uint32_t>(), c->stream);
       a.mc_tab = c->mc_tab.as<uint32_t>();
     }
-    HIPCHK(c, c->base.ensure((size_t)total_paths * 24));
+    // the indirect paths' tiled slots (RenderArgs::ind_rows): rows per 64-primary tile, scanned
+    const int64_t ntiles = (nprim + 63) / 64;
+    HIPCHK(c, c->ind_trows.ensure((size_t)(ntiles + 1) * 4));
+    HIPCHK(c, c->ind_rows.ensure((size_t)(ntiles + 1) * 4));
+    launch_ind_tiles(a.nind, nprim, c->ind_trows.as<uint32_t>(), c->stream);
+    HIPCHK(c, launch_scan(c->ind_trows.as<uint32_t>(), c->ind_rows.as<uint32_t>(), ntiles, t, c->stream));
+    uint32_t trows = 0;
+    HIPCHK(c, hipMemcpyAsync(&trows, c->ind_rows.as<uint32_t>() + ntiles, 4, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const uint64_t tind = 64ull * trows;  // tiled entries (>= total_ind)
+    if ((uint64_t)total_paths + tind + (uint64_t)nprim > 0xFFFFFFF0ull)
+      return fail(c, GI_ERR_ALLOC, "batch too large for 32-bit path slots");
+    a.ind_rows = c->ind_rows.as<uint32_t>();
+    a.ind_g0 = total_paths;
+    a.tind = (int64_t)tind;
+    HIPCHK(c, c->ind_tab.ensure(((size_t)trows + 1) * 4));
+    launch_ind_row_tile(a.ind_rows, ntiles, c->ind_tab.as<uint32_t>(), c->stream);
+    a.ind_row_tile = c->ind_tab.as<uint32_t>();
+    HIPCHK(c, c->ind_masks.ensure(((size_t)trows + 1) * 16));
+    a.ind_qmask = c->ind_masks.as<uint64_t>();
+    a.ind_bmask = a.ind_qmask + trows + 1;
+    HIPCHK(c, c->base.ensure(((size_t)total_paths + tind) * 24));
     a.base = c->base.as<double>();
     // continuation queue: stripe s takes the appends of waves w with w % IND_QS == s (<= 64
     // paths per wave, so `full` entries per stripe can never overflow); sized from the fill
     // seen so far (c->ind_frac of full), re-run with more room when a stripe overflows
-    const uint64_t ind_full = 64 * ((((uint64_t)a.total_ind + 63) / 64 + IND_QS - 1) / IND_QS);
+    const uint64_t ind_full = 64 * ((((uint64_t)a.tind + 63) / 64 + IND_QS - 1) / IND_QS);
     if (a.split_ind && a.total_ind > 0) HIPCHK(c, c->ind_ncont.ensure(IND_QS * 32 * 4));
     // Monte Carlo paths' indirect sub-paths: at most one per path, so the worst case is sized
     if (a.split_ind && a.total_mc > 0 && a.F.indirect) {
@@ -1152,9 +1171,9 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     uint32_t nq[2] = {0, 0};
     HIPCHK(c, hipMemcpyAsync(c->stats_bak.p, c->d_stats.p, ST_BYTES,
                              hipMemcpyDeviceToDevice, c->stream));
-    // deterministic slots: [0, nprim) per primary sample, then (global list) one per
-    // indirect path; Monte Carlo paths append after qbase[l]
-    uint32_t qbase[2] = {(uint32_t)(nprim + a.total_ind), (uint32_t)nprim};
+    // deterministic slots: [0, nprim) per primary sample, then (global list) the indirect
+    // paths' tiled slots; Monte Carlo paths append after qbase[l]
+    uint32_t qbase[2] = {(uint32_t)(nprim + tind), (uint32_t)nprim};
     a.qind_base = nprim;
     for (int attempt = 0; attempt < 3; attempt++) {
       for (int l = 0; l < 2; l++) {
@@ -1176,6 +1195,7 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
       }
       a.qcount = c->qcount.as<uint32_t>();
       HIPCHK(c, hipMemcpyAsync(c->qcount.p, qbase, 8, hipMemcpyHostToDevice, c->stream));
+      if (tind > (uint64_t)a.total_ind) launch_ind_pad(a, c->stream);  // (never when tind = 0)
       launch_path(a, c->stream, c->stream2, c->ev_fork, c->ev_join);
       HIPCHK(c, hipGetLastError());
       HIPCHK(c, hipMemcpyAsync(nq, c->qcount.p, 8, hipMemcpyDeviceToHost, c->stream));
@@ -1199,8 +1219,8 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
                                hipMemcpyDeviceToDevice, c->stream));
     }
     // photon-map estimates, then a deterministic order of each list for the reduction. The
-    // deterministic slots (a primary's own query at slot b; indirect path t's at qind_base + t)
-    // are already in (primary, slot-in-primary) order; only the Monte Carlo appends after
+    // deterministic slots (a primary's own query at slot b; its indirect paths' at tiled slots)
+    // are located by (primary, slot-in-primary); only the Monte Carlo appends after
     // qbase[l] are key-sorted and indexed per primary (CSR over the sorted keys).
     bool run[2] = {false, false};
     for (int l = 0; l < 2; l++) {
@@ -1417,7 +1437,7 @@ void gi_destroy(gi_ctx *c) {
   DBuf *bufs[] = {&c->d_nodes, &c->d_elems, &c->d_shapes, &c->d_tris, &c->d_bvh, &c->d_mats, &c->d_lights,
                   &c->d_lut, &c->d_stats, &c->spawn, &c->npaths, &c->path_off, &c->base,
                   &c->pixels, &c->rgbf, &c->rgb8, &c->qcount,
-                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont, &c->mc_cont, &c->mc_ncont, &c->prim_rgb, &c->ind_tab, &c->mc_tab};
+                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont, &c->mc_cont, &c->mc_ncont, &c->prim_rgb, &c->ind_tab, &c->mc_tab, &c->ind_trows, &c->ind_rows, &c->ind_masks};
   for (DBuf *b : bufs) b->release();
   c->pack.release();
   for (auto &b : c->recv) b.release();

@@ -82,15 +82,17 @@ struct RenderArgs {
   int64_t nprim;        // npix * af^2 * dof_test
   int64_t total_paths;
   Spawn *spawn;
-  uint32_t *npaths;     // [nprim] 1 + transmissive + specular + indirect paths
+  uint32_t *npaths;     // [nprim] 1 + transmissive + specular paths (CSR base slots; the
+                        // indirect paths' are tiled, ind_rows)
   uint32_t *nmc;        // [nprim] transmissive + specular (Monte Carlo path) samples
   uint32_t *nind;       // [nprim] indirect samples
   const uint32_t *path_off;  // [nprim + 1] exclusive scans of the three counts
   const uint32_t *mc_off;
   const uint32_t *ind_off;
-  const uint32_t *ind_tab;   // [total_ind / 64 + 1] owner of path 64k (owner_table_kernel)
+  const uint32_t *ind_row_tile;  // [rows] tile of each 64-entry row of the tiled indirect slots
   const uint32_t *mc_tab;    // same for the Monte Carlo paths
   int64_t total_mc, total_ind;
+  int64_t tind;               // tiled indirect entries (64 per row, >= total_ind; RenderArgs::ind_rows)
   int32_t ind_waves;    // occupancy target of the indirect-path kernel (waves per SIMD)
   int32_t dbg;          // diagnostics: 1 = skip the indirect trace, 2 = skip diffuse sampling too
   int32_t split_ind;    // 1: indirect paths trace their first bounce, continuations are queued
@@ -100,7 +102,17 @@ struct RenderArgs {
   IndCont *mc_cont;     // Monte Carlo paths' indirect sub-paths, striped the same way
   uint32_t *mc_ncont;
   uint32_t mc_cap_s;
-  int64_t qind_base;    // global list: indirect path t owns slot qind_base + t
+  // Indirect paths' slots, tiled: primaries b in tiles of 64 (T = b / 64); tile T holds
+  // ind_rows[T+1] - ind_rows[T] = max n_i over its primaries rows of 64 entries, and indirect
+  // path s of primary b is entry tau(b, s) = 64 * (ind_rows[T] + s) + b % 64 (ind_tau). Its
+  // base is base slot ind_g0 + tau, its query (global list) slot qind_base + tau. The indirect
+  // path kernel runs one thread per entry (a wave = one row: sample s of 64 primaries) and the
+  // reduction one per primary, so both read and write rows as 64 contiguous entries.
+  int64_t qind_base;
+  const uint32_t *ind_rows;  // [ntiles + 1] exclusive scan of the tiles' row counts
+  int64_t ind_g0;            // first base slot of the tiled region (= the CSR paths' total)
+  uint64_t *ind_qmask;       // [rows] bit l of row r: entry 64 r + l holds a query
+  uint64_t *ind_bmask;       // [rows] ... holds a stored base (not +0; unstored bases are +0)
   // query lists (0 = global map, 1 = caustic map). Deterministic slots first: list l slot p
   // = primary sample p's own query (slot-0 path), then (global list only) slot
   // qind_base + t = indirect path t's single query; unused ones hold QMETA_NONE. Monte Carlo
@@ -320,6 +332,9 @@ void launch_fb_compact(const uint32_t *list, const uint32_t *count, uint32_t cap
                        uint32_t *total, hipStream_t st);  // slot0 + indirect + Monte Carlo
 void launch_reduce(const RenderArgs &a, hipStream_t st);
 void launch_owner_table(const uint32_t *off, int64_t n, uint32_t *tab, hipStream_t st);
+void launch_ind_tiles(const uint32_t *nind, int64_t nprim, uint32_t *rows, hipStream_t st);
+void launch_ind_row_tile(const uint32_t *rows, int64_t ntiles, uint32_t *tab, hipStream_t st);
+void launch_ind_pad(const RenderArgs &a, hipStream_t st);
 // device-set gather: pixels (x, y int32 pairs) packed 16 B each / scattered back
 void launch_pack_pixels(const int32_t *pix_xy, int64_t n, int w, const float *rgbf,
                         const uint8_t *rgb8, void *out, hipStream_t st);

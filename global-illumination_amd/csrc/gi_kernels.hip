@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) void primary_kernel(RenderArgs a) {
       sp.base[0] = color.r; sp.base[1] = color.g; sp.base[2] = color.b;
     }
     a.spawn[b] = sp;
-    a.npaths[b] = 1u + (uint32_t)(sp.n_t + sp.n_s + sp.n_i);
+    a.npaths[b] = 1u + (uint32_t)(sp.n_t + sp.n_s);
     a.nmc[b] = (uint32_t)(sp.n_t + sp.n_s);
     a.nind[b] = (uint32_t)sp.n_i;
     c_shadow = cnt.shadow;
@@ -472,6 +472,42 @@ __global__ void owner_table_kernel(const uint32_t *off, int64_t n, uint32_t *tab
   for (uint32_t k = (lo + 63) >> 6; (k << 6) < hi; k++) tab[k] = (uint32_t)p;
 }
 
+// a path base that is +0 in every channel adds nothing to a sum that starts at +0 (such a sum is
+// never -0: x + (+0) == x for every x other than -0), so it need not be stored or read
+__device__ __forceinline__ bool base_is_pzero(const C3 &c) {
+  return __double_as_longlong(c.r) == 0 && __double_as_longlong(c.g) == 0 &&
+         __double_as_longlong(c.b) == 0;
+}
+
+// tiled entry of indirect path s of primary b (RenderArgs::ind_rows)
+__device__ __forceinline__ int64_t ind_tau(const RenderArgs &a, int64_t b, int s) {
+  return 64 * ((int64_t)a.ind_rows[b >> 6] + s) + (b & 63);
+}
+
+// rows[T] = max n_i over tile T's primaries (one wave per tile); scanned into ind_rows after
+__global__ __launch_bounds__(64) void ind_tile_rows_kernel(const uint32_t *nind, int64_t nprim,
+                                                          uint32_t *rows) {
+  const int64_t b = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  uint32_t v = b < nprim ? nind[b] : 0u;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  if (threadIdx.x == 0) rows[blockIdx.x] = v;
+}
+
+// the tiled entries past a primary's own n_i (its tile's other primaries have more), and every
+// entry of the last tile's lanes past nprim: empty global-list query slots (the k-NN skips them;
+// the reduction never reads them). One thread per lane of every tile.
+__global__ __launch_bounds__(256) void ind_pad_kernel(RenderArgs a) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= ((a.nprim + 63) & ~(int64_t)63)) return;
+  const int rows = (int)(a.ind_rows[(b >> 6) + 1] - a.ind_rows[b >> 6]);
+  for (int s = b < a.nprim ? (int)a.nind[b] : 0; s < rows; s++) {
+    const int64_t sl = a.qind_base + ind_tau(a, b, s);
+    a.qpos[0][sl] = make_float4(0.f, 0.f, 0.f, __uint_as_float(QMETA_NONE));
+    a.qkey[0][sl] = ~0ull;
+  }
+}
+
 __device__ __forceinline__ void path_init(PathCtx &P, const RenderArgs &a, int64_t g, int64_t prim,
                                           int pslot) {
   P.S = &a.S;
@@ -540,22 +576,25 @@ __global__ __launch_bounds__(256) void slot0_kernel(RenderArgs a) {
 // append) and finish compacted in ind_cont_kernel; the arithmetic and RNG stream are unchanged.
 template <int W, bool SPLIT, uint32_t KINDS>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void ind_kernel(RenderArgs a) {
-  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // thread t = tiled entry t (RenderArgs::ind_rows): row t / 64 of tile T, lane = primary
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   Counts cnt = {0, 0, 0, 0, 0, 0};
-  bool queue = false;
-  if (t < a.total_ind) {
-    int64_t pb = wave_owner(a.ind_off, a.nprim, t, a.total_ind, a.ind_tab);
-    int s = (int)(t - a.ind_off[pb]);
+  bool queue = false, hasq = false, hasb = false;
+  const uint32_t T = t < a.tind ? a.ind_row_tile[t >> 6] : 0u;
+  const int64_t pb = 64 * (int64_t)T + (t & 63);
+  const int s = t < a.tind ? (int)((t >> 6) - (int64_t)a.ind_rows[T]) : 0;
+  if (t < a.tind && pb < a.nprim && s < (int)a.nind[pb]) {
     const Spawn &sp = a.spawn[pb];
     int pslot = 1 + sp.n_t + sp.n_s + s;
-    int64_t g = (int64_t)a.path_off[pb] + pslot;
+    const int64_t tau = t;
+    int64_t g = a.ind_g0 + tau;
     int pix, i, j, k;
     uint64_t psample;
     decode_primary(a, pb, pix, i, j, k, psample);
     const DMaterial &m = a.S.mats[sp.mat];
     PathCtx P;
     path_init(P, a, g, pb, pslot);
-    P.fixed[0] = a.qind_base + t;  // at most one (global) query per indirect path
+    P.fixed[0] = a.qind_base + tau;  // at most one (global) query per indirect path
     P.hint = sp.tri;
     Rng rng;
     rng.init(a.F.seed, KIND_IND, psample, (uint64_t)s);
@@ -608,12 +647,24 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void i
     }
     P.cnt.indirect++;
     if (!queue) {
+      hasq = P.fixed[0] == -2;
       if (P.fixed[0] >= 0) put_none(a, 0, P.fixed[0]);
-      a.base[3 * g] = P.base.r;
-      a.base[3 * g + 1] = P.base.g;
-      a.base[3 * g + 2] = P.base.b;
+      hasb = !base_is_pzero(P.base);
+      if (hasb) {
+        a.base[3 * g] = P.base.r;
+        a.base[3 * g + 1] = P.base.g;
+        a.base[3 * g + 2] = P.base.b;
+      }
     }
     cnt = P.cnt;
+  }
+  // the row's masks (a wave is one row; tind is a multiple of 64): which entries hold a query,
+  // which a base other than +0 (only those bases are stored). Queued paths set theirs in
+  // ind_cont_kernel.
+  const uint64_t qm = __ballot(hasq), bm = __ballot(hasb);
+  if (t < a.tind && (threadIdx.x & 63) == 0) {
+    a.ind_qmask[t >> 6] = qm;
+    a.ind_bmask[t >> 6] = bm;
   }
   path_stats(a, cnt);
 }
@@ -663,12 +714,20 @@ void ind_cont_kernel(RenderArgs a, const IndCont *queue, const uint32_t *fill, u
     if (go)
       for (int iter = iter0; iter < a.F.max_monte_depth; iter++)
         if (!ind_bounce<KINDS>(P, org, dir, rng, W, tw)) break;
+    const bool used = P.fixed[0] == -2;
     if (P.fixed[0] >= 0) put_none(a, 0, P.fixed[0]);
     double *bp = a.base + 3 * (int64_t)q.g;
     if (q.mat >= 0) {
-      bp[0] = P.base.r;
-      bp[1] = P.base.g;
-      bp[2] = P.base.b;
+      // an indirect path's tiled entry (q.qslot = qind_base + tau): its mask bits
+      const int64_t tau = (int64_t)q.qslot - a.qind_base;
+      const unsigned long long bit = 1ull << (tau & 63);
+      if (used) atomicOr((unsigned long long *)&a.ind_qmask[tau >> 6], bit);
+      if (!base_is_pzero(P.base)) {
+        bp[0] = P.base.r;
+        bp[1] = P.base.g;
+        bp[2] = P.base.b;
+        atomicOr((unsigned long long *)&a.ind_bmask[tau >> 6], bit);
+      }
     } else {  // the sub-path's background term is the last addition to the path's sum
       bp[0] = bp[0] + P.base.r;
       bp[1] = bp[1] + P.base.g;
@@ -1118,37 +1177,73 @@ void launch_segments(const uint64_t *skeys, uint32_t n, uint32_t nprim, uint32_t
 // Per-pixel reduction: RenderImage's DOF average + ClampColor + box filter + SetPixelRGB
 // (render.cpp:130-135, 205-221; R2Image.cpp:205-208)
 // ---------------------------------------------------------------------------------------
-// Pass 1, one thread per primary sample b: c(b) = sum of b's path bases, then of its queries,
-// in the oracle's order (a sequential fp64 sum; the loads of each run are issued four at a
-// time so a lane has several lines in flight, the additions stay in order).
-__global__ __launch_bounds__(256) void reduce_prim_kernel(RenderArgs a) {
-  int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= a.nprim) return;
-  double c0 = 0, c1 = 0, c2 = 0;
-  {
-    uint32_t g = a.path_off[b];
-    const uint32_t p1 = a.path_off[b + 1];
-    const double *bs = a.base;
-    for (; g + 4 <= p1; g += 4) {
+// lane i's value of a wave-uniform index i (two readlanes)
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int i) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, i);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), i);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// the sum over the tiled rows [r0, r0 + M) of one mask array: lane l (primary 64 T + l) adds
+// entry 64 r + l of vals where bit l of mask[r] is set, rows in order. The masks of 64 rows come
+// in with one load (lane i: row r0 + s0 + i) and are read back with readlane; four rows' entries
+// are loaded before they are added.
+__device__ __forceinline__ void tiled_row_sum(const uint64_t *mask, const double *vals, int64_t r0, int M,
+                                              int lane, double &c0, double &c1, double &c2) {
+  for (int s0 = 0; s0 < M; s0 += 64) {
+    const int n = M - s0 < 64 ? M - s0 : 64;
+    const uint64_t mk = lane < n ? mask[r0 + s0 + lane] : 0ull;
+    for (int j = 0; j < n; j += 4) {
+      bool on[4];
       double v[12];
 #pragma unroll
-      for (int u = 0; u < 12; u++) v[u] = bs[3 * (int64_t)g + u];
-#pragma unroll
       for (int u = 0; u < 4; u++) {
-        c0 += v[3 * u];
-        c1 += v[3 * u + 1];
-        c2 += v[3 * u + 2];
+        on[u] = j + u < n && ((readlane64(mk, j + u < n ? j + u : 0) >> lane) & 1ull);
+        v[3 * u] = v[3 * u + 1] = v[3 * u + 2] = 0.0;
+        if (on[u]) {  // unflagged entries are not read
+          const double *e = vals + 3 * (64 * (r0 + s0 + j + u) + lane);
+          v[3 * u] = e[0];
+          v[3 * u + 1] = e[1];
+          v[3 * u + 2] = e[2];
+        }
       }
+#pragma unroll
+      for (int u = 0; u < 4; u++)
+        if (on[u]) {
+          c0 += v[3 * u];
+          c1 += v[3 * u + 1];
+          c2 += v[3 * u + 2];
+        }
     }
-    for (; g < p1; g++) {
+  }
+}
+
+// Pass 1, one thread per primary sample b: c(b) = sum of b's path bases, then of its queries,
+// in the oracle's order (a sequential fp64 sum). The CSR runs (slot-0 and Monte Carlo path bases)
+// are short. The indirect paths are tiled (RenderArgs::ind_rows): a wave is one tile, its lanes
+// its 64 primaries, and row s's masks say which lanes have a stored base (the others are +0,
+// which adds nothing) and which a query; only those entries are read, 64 contiguous per row
+// (a lane's entries past its own n_i are padding, never flagged).
+__global__ __launch_bounds__(256) void reduce_prim_kernel(RenderArgs a) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t T = b >> 6;  // wave-uniform: blocks of whole waves
+  if (T * 64 >= a.nprim) return;
+  const bool own = b < a.nprim;
+  const int lane = (int)(b & 63);
+  const int64_t r0 = (int64_t)a.ind_rows[T];
+  const int M = (int)((int64_t)a.ind_rows[T + 1] - r0);
+  double c0 = 0, c1 = 0, c2 = 0;
+  const double *bs = a.base;
+  if (own)
+    for (uint32_t g = a.path_off[b], p1 = a.path_off[b + 1]; g < p1; g++) {
       c0 += bs[3 * (int64_t)g];
       c1 += bs[3 * (int64_t)g + 1];
       c2 += bs[3 * (int64_t)g + 2];
     }
-  }
+  tiled_row_sum(a.ind_bmask, bs + 3 * a.ind_g0, r0, M, lane, c0, c1, c2);
   // each list in (primary, slot in primary, query in path) order: the primary's own query
   // (slot b), its Monte Carlo paths' appends (sorted), then (global list) its indirect paths'
-  // queries (slots qind_base + t, in path order); empty slots skipped
+  // queries (tiled slots, in path order); empty slots skipped
   for (int l = 0; l < 2; l++) {
     if (!a.qout[l]) continue;
     const uint64_t *qk = a.qkey[l];
@@ -1159,34 +1254,18 @@ __global__ __launch_bounds__(256) void reduce_prim_kernel(RenderArgs a) {
       c1 += qo[3 * sl + 1];
       c2 += qo[3 * sl + 2];
     };
-    add(b);
-    uint32_t q0 = a.qseg[l][b], q1 = a.qseg[l][b + 1];
-    for (uint32_t q = q0; q < q1; q++) add((int64_t)a.qapp[l] + a.sslot[l][q]);
-    if (l == 0) {
-      uint32_t t = a.ind_off[b];
-      const uint32_t t1 = a.ind_off[b + 1];
-      for (; t + 4 <= t1; t += 4) {
-        const int64_t s0 = a.qind_base + t;
-        uint64_t k[4];
-        double v[12];
-#pragma unroll
-        for (int u = 0; u < 4; u++) k[u] = qk[s0 + u];
-#pragma unroll
-        for (int u = 0; u < 12; u++) v[u] = qo[3 * s0 + u];
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-          if (k[u] != ~0ull) {
-            c0 += v[3 * u];
-            c1 += v[3 * u + 1];
-            c2 += v[3 * u + 2];
-          }
-      }
-      for (; t < t1; t++) add(a.qind_base + t);
+    if (own) {
+      add(b);
+      uint32_t q0 = a.qseg[l][b], q1 = a.qseg[l][b + 1];
+      for (uint32_t q = q0; q < q1; q++) add((int64_t)a.qapp[l] + a.sslot[l][q]);
     }
+    if (l == 0) tiled_row_sum(a.ind_qmask, qo + 3 * a.qind_base, r0, M, lane, c0, c1, c2);
   }
-  a.prim_rgb[3 * b] = c0;
-  a.prim_rgb[3 * b + 1] = c1;
-  a.prim_rgb[3 * b + 2] = c2;
+  if (own) {
+    a.prim_rgb[3 * b] = c0;
+    a.prim_rgb[3 * b + 1] = c1;
+    a.prim_rgb[3 * b + 2] = c2;
+  }
 }
 
 // Pass 2, one thread per output pixel
@@ -1483,7 +1562,7 @@ void launch_path(const RenderArgs &a, hipStream_t st, hipStream_t st2, hipEvent_
   }
   if (a.nprim > 0) slot0_kernel<<<nblk(a.nprim, 256), 256, 0, st>>>(a);
   if (a.total_ind > 0) {
-    unsigned g = nblk(a.total_ind, 128);
+    unsigned g = nblk(a.tind, 128);
     if (a.split_ind) (void)hipMemsetAsync(a.ind_ncont, 0, IND_QS * 32 * sizeof(uint32_t), st);
     if (!a.split_ind) ind_kernel<2, false, KINDS_ALL><<<g, 128, 0, st>>>(a);
     else if ((a.S.kinds & ~KINDS_TRI_SPHERE) == 0) launch_ind<KINDS_TRI_SPHERE>(a, g, st);
@@ -1536,11 +1615,30 @@ void launch_unpack_pixels(const int32_t *pix_xy, int64_t n, int w, const void *i
                                                      reinterpret_cast<const uint4 *>(in), rgbf,
                                                      rgb8);
 }
+void launch_ind_tiles(const uint32_t *nind, int64_t nprim, uint32_t *rows, hipStream_t st) {
+  ind_tile_rows_kernel<<<(unsigned)((nprim + 63) / 64), 64, 0, st>>>(nind, nprim, rows);
+}
+
+// tab[r] = the tile of row r of the tiled indirect entries (thread per tile)
+__global__ void ind_row_tile_kernel(const uint32_t *rows, int64_t ntiles, uint32_t *tab) {
+  const int64_t T = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (T >= ntiles) return;
+  for (uint32_t r = rows[T]; r < rows[T + 1]; r++) tab[r] = (uint32_t)T;
+}
+
+void launch_ind_row_tile(const uint32_t *rows, int64_t ntiles, uint32_t *tab, hipStream_t st) {
+  if (ntiles > 0) ind_row_tile_kernel<<<nblk(ntiles, 256), 256, 0, st>>>(rows, ntiles, tab);
+}
+
+void launch_ind_pad(const RenderArgs &a, hipStream_t st) {
+  ind_pad_kernel<<<nblk((a.nprim + 63) & ~(int64_t)63, 256), 256, 0, st>>>(a);
+}
+
 void launch_owner_table(const uint32_t *off, int64_t n, uint32_t *tab, hipStream_t st) {
   if (n > 0) owner_table_kernel<<<nblk(n, 256), 256, 0, st>>>(off, n, tab);
 }
 void launch_reduce(const RenderArgs &a, hipStream_t st) {
-  reduce_prim_kernel<<<nblk(a.nprim, 256), 256, 0, st>>>(a);
+  reduce_prim_kernel<<<nblk((a.nprim + 63) & ~(int64_t)63, 256), 256, 0, st>>>(a);
   reduce_kernel<<<nblk(a.npix, 64), 64, 0, st>>>(a);
 }
 void launch_knn(const KnnArgs &a, hipStream_t st) {

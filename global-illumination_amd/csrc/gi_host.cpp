@@ -293,7 +293,7 @@ struct gi_ctx {
   int64_t progress_done = 0, progress_total = 0;  // output pixels of the current RenderImage     // k-NN kind run_knn chose last, per map (gi_render_stats)
   int sel_slack = 64;
   int knn_qpl = 1;
-  int ind_waves = 3;              // indirect-path kernel occupancy target (waves per SIMD)
+  int ind_waves = 4;              // indirect-path kernel occupancy target (launch_ind)
   DBuf ind_cont, ind_ncont;       // indirect paths that continue past their first bounce
   DBuf mc_cont, mc_ncont;         // Monte Carlo paths' indirect sub-paths
   DBuf prim_rgb;                  // per-primary sums of the reduction
@@ -1145,9 +1145,9 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     a.ind_rows = c->ind_rows.as<uint32_t>();
     a.ind_g0 = total_paths;
     a.tind = (int64_t)tind;
-    HIPCHK(c, c->ind_tab.ensure(((size_t)trows + 1) * 4));
-    launch_ind_row_tile(a.ind_rows, ntiles, c->ind_tab.as<uint32_t>(), c->stream);
-    a.ind_row_tile = c->ind_tab.as<uint32_t>();
+    HIPCHK(c, c->ind_tab.ensure(((size_t)trows + 1) * 8));
+    launch_ind_row_tile(a.ind_rows, ntiles, c->ind_tab.as<uint64_t>(), c->stream);
+    a.ind_row_info = c->ind_tab.as<uint64_t>();
     HIPCHK(c, c->ind_masks.ensure(((size_t)trows + 1) * 16));
     a.ind_qmask = c->ind_masks.as<uint64_t>();
     a.ind_bmask = a.ind_qmask + trows + 1;

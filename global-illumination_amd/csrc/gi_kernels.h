@@ -24,6 +24,7 @@ struct Spawn {
   int32_t n_t, n_s, n_i;  // transmissive / specular / indirect sample counts
   int32_t q_glob, q_caus; // primary-hit photon-map queries (photon_viz / caustic)
   int32_t tri;            // triangle hit (gi_device.h Hit::tri): the sample paths leave from it
+  double wt[3];           // indirect paths' outer weight kd / n_i (raytracer.cpp:112-135)
 };
 
 // shading half of a photon-map query (search half is float4 {x, y, z, meta})
@@ -89,7 +90,8 @@ struct RenderArgs {
   const uint32_t *path_off;  // [nprim + 1] exclusive scans of the three counts
   const uint32_t *mc_off;
   const uint32_t *ind_off;
-  const uint32_t *ind_row_tile;  // [rows] tile of each 64-entry row of the tiled indirect slots
+  const uint64_t *ind_row_info;  // [rows] tile << 32 | sample index of each 64-entry row of
+                                 // the tiled indirect slots
   const uint32_t *mc_tab;    // same for the Monte Carlo paths
   int64_t total_mc, total_ind;
   int64_t tind;               // tiled indirect entries (64 per row, >= total_ind; RenderArgs::ind_rows)
@@ -333,7 +335,7 @@ void launch_fb_compact(const uint32_t *list, const uint32_t *count, uint32_t cap
 void launch_reduce(const RenderArgs &a, hipStream_t st);
 void launch_owner_table(const uint32_t *off, int64_t n, uint32_t *tab, hipStream_t st);
 void launch_ind_tiles(const uint32_t *nind, int64_t nprim, uint32_t *rows, hipStream_t st);
-void launch_ind_row_tile(const uint32_t *rows, int64_t ntiles, uint32_t *tab, hipStream_t st);
+void launch_ind_row_tile(const uint32_t *rows, int64_t ntiles, uint64_t *tab, hipStream_t st);
 void launch_ind_pad(const RenderArgs &a, hipStream_t st);
 // device-set gather: pixels (x, y int32 pairs) packed 16 B each / scattered back
 void launch_pack_pixels(const int32_t *pix_xy, int64_t n, int w, const float *rgbf,

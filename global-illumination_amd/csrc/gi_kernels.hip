@@ -133,8 +133,11 @@ __global__ __launch_bounds__(256) void primary_kernel(RenderArgs a) {
         C3 tw = ldc(m.kt) * R + ldc(m.ks);
         sp.n_s = (int)ceil((F.spec_test * maxch(tw) + F.spec_test) / 2.0);
       }
-      if (F.indirect && (m.flags & MF_DIFFUSE))
+      if (F.indirect && (m.flags & MF_DIFFUSE)) {
         sp.n_i = (int)ceil((F.indirect_test * m.max_kd + F.indirect_test) / 2.0);
+        const C3 wt = ldc(m.kd) / (double)sp.n_i;
+        sp.wt[0] = wt.r; sp.wt[1] = wt.g; sp.wt[2] = wt.b;
+      }
       if (F.caustic && (m.flags & MF_DIFFUSE)) sp.q_caus = 1;
       if (F.photon_viz && (m.flags & MF_DIFFUSE)) {
         sp.q_glob = 1;
@@ -209,9 +212,15 @@ struct PathCtx {
   int hint;         // triangle the path's current ray leaves from (ray_mesh_bvh), -1 none
 };
 
+// the indirect paths' tiled global-list slots carry no key: the reduction reads their row
+// masks (RenderArgs::ind_qmask) instead
+__device__ __forceinline__ bool keyed_slot(const RenderArgs &a, int list, int64_t slot) {
+  return list != 0 || slot < a.qind_base || slot >= a.qind_base + a.tind;
+}
+
 __device__ __forceinline__ void put_none(const RenderArgs &a, int list, int64_t slot) {
   a.qpos[list][slot] = make_float4(0.f, 0.f, 0.f, __uint_as_float(QMETA_NONE));
-  a.qkey[list][slot] = ~0ull;
+  if (keyed_slot(a, list, slot)) a.qkey[list][slot] = ~0ull;
 }
 
 // append one photon-map query (list 0 = global, 1 = caustic): search half (point as f32 +
@@ -248,7 +257,7 @@ __device__ __forceinline__ void put_query(PathCtx &P, int list, V p, V n, V ex, 
   q.ex[0] = ex.x; q.ex[1] = ex.y; q.ex[2] = ex.z;
   q.w[0] = w.r; q.w[1] = w.g; q.w[2] = w.b;
   a.qshade[list][slot] = q;
-  a.qkey[list][slot] = key;
+  if (keyed_slot(a, list, slot)) a.qkey[list][slot] = key;
 }
 
 // global-map lookup at a diffuse hit: EstimateRadiance or (with -cache) the cached radiance
@@ -504,7 +513,6 @@ __global__ __launch_bounds__(256) void ind_pad_kernel(RenderArgs a) {
   for (int s = b < a.nprim ? (int)a.nind[b] : 0; s < rows; s++) {
     const int64_t sl = a.qind_base + ind_tau(a, b, s);
     a.qpos[0][sl] = make_float4(0.f, 0.f, 0.f, __uint_as_float(QMETA_NONE));
-    a.qkey[0][sl] = ~0ull;
   }
 }
 
@@ -580,18 +588,19 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void i
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   Counts cnt = {0, 0, 0, 0, 0, 0};
   bool queue = false, hasq = false, hasb = false;
-  const uint32_t T = t < a.tind ? a.ind_row_tile[t >> 6] : 0u;
-  const int64_t pb = 64 * (int64_t)T + (t & 63);
-  const int s = t < a.tind ? (int)((t >> 6) - (int64_t)a.ind_rows[T]) : 0;
-  if (t < a.tind && pb < a.nprim && s < (int)a.nind[pb]) {
-    const Spawn &sp = a.spawn[pb];
+  // one row-table load gives the tile and the sample index; the spawn record (n_i, the weight)
+  // and the pixel come next, side by side: two dependent loads before the path's arithmetic
+  const uint64_t ri = t < a.tind ? a.ind_row_info[t >> 6] : 0ull;
+  const int64_t pb = 64 * (int64_t)(ri >> 32) + (t & 63);
+  const int s = (int)(uint32_t)ri;
+  const Spawn &sp = a.spawn[pb < a.nprim ? pb : 0];
+  if (t < a.tind && pb < a.nprim && s < sp.n_i) {
     int pslot = 1 + sp.n_t + sp.n_s + s;
     const int64_t tau = t;
     int64_t g = a.ind_g0 + tau;
     int pix, i, j, k;
     uint64_t psample;
     decode_primary(a, pb, pix, i, j, k, psample);
-    const DMaterial &m = a.S.mats[sp.mat];
     PathCtx P;
     path_init(P, a, g, pb, pslot);
     P.fixed[0] = a.qind_base + tau;  // at most one (global) query per indirect path
@@ -600,7 +609,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void i
     rng.init(a.F.seed, KIND_IND, psample, (uint64_t)s);
     V p = ld3(sp.p), n = ld3(sp.n);
     V sb = (a.dbg >= 2) ? n : diffuse_sample(n, sp.ct, rng);
-    C3 Wt = ldc(m.kd) / (double)sp.n_i;
+    C3 Wt = ldc(sp.wt);  // kd / n_i (primary_kernel)
     if (a.dbg != 0) {
       P.base = rgb(sb.x, sb.y, sb.z);
     } else if (!SPLIT) {
@@ -1513,12 +1522,15 @@ hipError_t launch_scan(const uint32_t *in, uint32_t *out, int64_t n, ScanTemp &t
 void launch_primary(const RenderArgs &a, hipStream_t st) {
   primary_kernel<<<nblk(a.nprim, 256), 256, 0, st>>>(a);
 }
+// occupancy: 4 waves per SIMD where the kernel fits 128 VGPRs without spills (triangles and
+// spheres only; C2 ind_kernel 37.8 -> 31.3 ms, frame -2.6 %), else 3 (the 4-wave instances of
+// the other element sets spill 74-129 VGPRs)
 template <uint32_t KINDS>
 void launch_ind(const RenderArgs &a, unsigned g, hipStream_t st) {
-  if (a.ind_waves <= 2) ind_kernel<2, true, KINDS><<<g, 128, 0, st>>>(a);
-  else if (a.ind_waves == 3) ind_kernel<3, true, KINDS><<<g, 128, 0, st>>>(a);
-  else if (a.ind_waves == 4) ind_kernel<4, true, KINDS><<<g, 128, 0, st>>>(a);
-  else ind_kernel<5, true, KINDS><<<g, 128, 0, st>>>(a);
+  const int w = KINDS == KINDS_TRI_SPHERE ? a.ind_waves : (a.ind_waves < 3 ? a.ind_waves : 3);
+  if (w <= 2) ind_kernel<2, true, KINDS><<<g, 128, 0, st>>>(a);
+  else if (w == 3) ind_kernel<3, true, KINDS><<<g, 128, 0, st>>>(a);
+  else ind_kernel<4, true, KINDS><<<g, 128, 0, st>>>(a);
 }
 void launch_cont(const RenderArgs &a, const IndCont *q, const uint32_t *fill, uint32_t cap_s,
                  hipStream_t st) {
@@ -1619,14 +1631,15 @@ void launch_ind_tiles(const uint32_t *nind, int64_t nprim, uint32_t *rows, hipSt
   ind_tile_rows_kernel<<<(unsigned)((nprim + 63) / 64), 64, 0, st>>>(nind, nprim, rows);
 }
 
-// tab[r] = the tile of row r of the tiled indirect entries (thread per tile)
-__global__ void ind_row_tile_kernel(const uint32_t *rows, int64_t ntiles, uint32_t *tab) {
+// tab[r] = T << 32 | s for row r = ind_rows[T] + s of the tiled indirect entries (thread per tile)
+__global__ void ind_row_tile_kernel(const uint32_t *rows, int64_t ntiles, uint64_t *tab) {
   const int64_t T = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (T >= ntiles) return;
-  for (uint32_t r = rows[T]; r < rows[T + 1]; r++) tab[r] = (uint32_t)T;
+  const uint32_t r0 = rows[T];
+  for (uint32_t r = r0; r < rows[T + 1]; r++) tab[r] = ((uint64_t)T << 32) | (r - r0);
 }
 
-void launch_ind_row_tile(const uint32_t *rows, int64_t ntiles, uint32_t *tab, hipStream_t st) {
+void launch_ind_row_tile(const uint32_t *rows, int64_t ntiles, uint64_t *tab, hipStream_t st) {
   if (ntiles > 0) ind_row_tile_kernel<<<nblk(ntiles, 256), 256, 0, st>>>(rows, ntiles, tab);
 }
 

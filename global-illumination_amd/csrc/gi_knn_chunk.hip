@@ -1458,13 +1458,16 @@ bool launch_knn_chunk2(const KnnArgs &a, hipStream_t st) {
 }
 
 // lane-select chunk kernel (K <= 64), 4 waves per SIMD (3 and 2 measured +4 % and +40 %)
+#ifndef LANE_WPE
+#define LANE_WPE 4
+#endif
 bool launch_knn_chunk(const KnnArgs &a, hipStream_t st) {
   if (a.nq == 0) return true;
   if (a.mode == KNN_MODE_LIST || a.K > 64) return false;
   unsigned grid = knn_chunk_grid(a.nq);
   // GI_KNN_DBG & 128: phase counters from the large-K kernel only
   if ((a.dbg & 16) && !(a.dbg & 128)) knn_chunk_lane_kernel<3, true><<<grid, 64, 0, st>>>(a);
-  else knn_chunk_lane_kernel<4, false><<<grid, 64, 0, st>>>(a);
+  else knn_chunk_lane_kernel<LANE_WPE, false><<<grid, 64, 0, st>>>(a);
   return true;
 }
 

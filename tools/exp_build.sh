@@ -10,7 +10,8 @@ mkdir -p $D
 OBJS=""
 for o in build/*.o; do
   if [ "$(basename $o .o)" = "$2" ]; then
-    /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -I../include -Icsrc $3 -c csrc/$2.hip -o $D/$2.o
+    SRC=csrc/$2.hip; [ -f $SRC ] || SRC="-x hip csrc/$2.cpp"
+    /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -I../include -Icsrc $3 -c $SRC -o $D/$2.o
     OBJS="$OBJS $D/$2.o"
   else
     OBJS="$OBJS $o"

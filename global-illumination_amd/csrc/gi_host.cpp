@@ -294,6 +294,7 @@ struct gi_ctx {
   int sel_slack = 64;
   int knn_qpl = 1;
   int ind_waves = 4;              // indirect-path kernel occupancy target (launch_ind)
+  uint32_t dump_fb_max = 0;       // GI_DUMP_FB diagnostics: largest fallback list written
   DBuf ind_cont, ind_ncont;       // indirect paths that continue past their first bounce
   DBuf mc_cont, mc_ncont;         // Monte Carlo paths' indirect sub-paths
   DBuf prim_rgb;                  // per-primary sums of the reduction
@@ -826,6 +827,23 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
       HIPCHK(c, hipGetLastError());
       HIPCHK(c, hipMemcpyAsync(&nfb2, dense + nfb, 4, hipMemcpyDeviceToHost, X.st));
       HIPCHK(c, hipStreamSynchronize(X.st));
+    }
+    if (const char *dp = getenv("GI_DUMP_FB"); dp && ran2 && nfb2 > c->dump_fb_max) {
+      // diagnostics (tools/caustic_fb_dump.py): the launch with the most fallback queries, as
+      // float4 positions of the final fallback list, then of the second pass's list
+      c->dump_fb_max = nfb2;
+      std::vector<uint32_t> i1(nfb), i2(nfb2);
+      HIPCHK(c, hipMemcpy(i1.data(), X.fb_dense.p, (size_t)nfb * 4, hipMemcpyDeviceToHost));
+      HIPCHK(c, hipMemcpy(i2.data(), dense, (size_t)nfb2 * 4, hipMemcpyDeviceToHost));
+      std::vector<float> qp((size_t)nq * 4);
+      HIPCHK(c, hipMemcpy(qp.data(), k.qpos, (size_t)nq * 16, hipMemcpyDeviceToHost));
+      if (FILE *f = fopen(dp, "wb")) {
+        int64_t hdr[4] = {nq, (int64_t)nfb, (int64_t)nfb2, k.stat_off ? 1 : 0};
+        fwrite(hdr, 8, 4, f);
+        for (uint32_t q : i2) fwrite(&qp[(size_t)q * 4], 4, 4, f);
+        for (uint32_t q : i1) fwrite(&qp[(size_t)q * 4], 4, 4, f);
+        fclose(f);
+      }
     }
     HIPCHK(c, hipEventRecord(X.ev3, X.st));
     if (nfb2) {
@@ -2102,6 +2120,11 @@ int gi_knn_bench(gi_ctx *c, int map, int64_t n, const double *pts, const double 
   if (rc) return rc;
   unsigned long long st[ST_COUNT];
   HIPCHK(c, read_stats(c, st));
+  if (const char *kd = getenv("GI_KNN_DBG"); kd && (atoi(kd) & 16)) {
+    fprintf(stderr, "[gi] k-NN phase cycles (sum over waves):");
+    for (int i = 0; i < 16; i++) fprintf(stderr, " %llu", st[ST_PHASE + i]);
+    fprintf(stderr, "\n");
+  }
   if (ms_out) *ms_out = ms / iters;
   int so = map * ST_KNN_MAP;
   double nqd = (double)std::max<unsigned long long>(1, st[ST_KNN + so]);

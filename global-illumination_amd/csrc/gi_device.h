@@ -544,9 +544,12 @@ struct Hit {
 // (hits beyond it are not looked for), and the walk returns 2 as soon as an element is taken
 // with t < t_exit (closest only decreases, so the final hit is nearer still). 0 = no hit below
 // t_init, 1 = hit in h.
+// emask: elements 0..63 whose bit is clear are skipped (their box cannot meet the ray segment
+// searched; soft_light's occluder mask); elements from 64 on are always tested.
 template <uint32_t KINDS = KINDS_ALL>
 __device__ __forceinline__ int scene_intersect_b(const SceneView &S, V org, V dir, Hit &h,
-                                                 double t_init, double t_exit, int hint = -1) {
+                                                 double t_init, double t_exit, int hint = -1,
+                                                 uint64_t emask = ~0ull) {
   double closest = t_init;  // world-frame t (rigid transforms keep t; scale handled below)
   bool found = false;
   V hp = mk(0, 0, 0), hn = mk(0, 0, 0);
@@ -575,7 +578,9 @@ __device__ __forceinline__ int scene_intersect_b(const SceneView &S, V org, V di
     if (!ok) continue;
     const V linv = mk(1.0 / ldir.x, 1.0 / ldir.y, 1.0 / ldir.z);
     for (int ei = 0; ei < nd.elem_count; ei++) {
-      const DElement &el = S.elems[nd.elem_first + ei];
+      const int gei = nd.elem_first + ei;
+      if (gei < 64 && !((emask >> gei) & 1ull)) continue;
+      const DElement &el = S.elems[gei];
       double maxt = closest / scale;
       if (S.elem_pretest && !elem_maybe_hit(el, lo, linv, maxt)) continue;
       auto box_pass = [&]() -> bool {
@@ -725,7 +730,8 @@ struct Counts {  // per-thread -v counters (render.cpp:26-32)
 // (1e-8 relative) cover the rounding between the walk's t and the distance of the transformed
 // hit point. The no-hit case keeps the reference's l = RN_INFINITY.
 template <uint32_t KINDS = KINDS_ALL>
-__device__ __forceinline__ bool illum_test_inl(const SceneView &S, V p_scene, V p_light, Counts &cnt) {
+__device__ __forceinline__ bool illum_test_inl(const SceneView &S, V p_scene, V p_light, Counts &cnt,
+                                               uint64_t emask = ~0ull) {
   double unocc = dist(p_light, p_scene);
   V d = normalize(p_scene - p_light);
   Hit h;
@@ -733,7 +739,7 @@ __device__ __forceinline__ bool illum_test_inl(const SceneView &S, V p_scene, V 
   // R3SceneNode.cpp:449-458, is not the hit's distance, so no bound is derived from it)
   const double mg = 1e-8 * fmax(1.0, unocc);
   const int r = S.rigid ? scene_intersect_b<KINDS>(S, p_light, d, h, fmin(kInf, unocc + kEps + mg),
-                                                   unocc - kEps - mg)
+                                                   unocc - kEps - mg, -1, emask)
                         : scene_intersect_b<KINDS>(S, p_light, d, h, kInf, -1.0);
   cnt.shadow++;
   if (r == 2) return false;
@@ -741,8 +747,9 @@ __device__ __forceinline__ bool illum_test_inl(const SceneView &S, V p_scene, V 
   return fabs(l - unocc) < kEps;
 }
 template <uint32_t KINDS = KINDS_ALL>
-__device__ __noinline__ bool illum_test(const SceneView &S, V p_scene, V p_light, Counts &cnt) {
-  return illum_test_inl<KINDS>(S, p_scene, p_light, cnt);
+__device__ __noinline__ bool illum_test(const SceneView &S, V p_scene, V p_light, Counts &cnt,
+                                        uint64_t emask = ~0ull) {
+  return illum_test_inl<KINDS>(S, p_scene, p_light, cnt, emask);
 }
 
 // TestLightIntersection, illumination_utils.cpp:35-84
@@ -780,6 +787,42 @@ GI_HD V light_sample_point(const DLight &L, Rng &rng) {
   return ((r1 * ld3(L.su) + r2 * ld3(L.sv)) + ld3(L.pos)) + ld3(L.dir) * kEps;
 }
 
+// Occluder mask of the shadow rays between p and light L's samples (rigid scenes of <= 64
+// elements): bit e clear when element e is in world coordinates and its box cannot meet any
+// segment from a sample point to p. Every sample lies in the light's parallelogram (offset by
+// kEps along its normal) and every searched segment in the convex hull of that and p, extended
+// past p by kEps + 1e-8 (illum_test_inl's bound), so it lies inside the hull's bounding box
+// grown by the margin below; an element box disjoint from that box fails R3Intersects(ray, box)
+// (every slab interval or the containment test excludes it, with room for their rounding and the
+// 1e-6 tolerance of box_contains), and scene_intersect_b takes no element whose box test fails.
+// Same result as testing every element.
+__device__ __forceinline__ uint64_t occluder_mask(const SceneView &S, const DLight &L, V p) {
+  if (!S.rigid || S.nelems > 64) return ~0ull;
+  const double h = (L.kind == LK_AREA) ? 1.0 : 0.5;  // sample coefficients in [-h, h]
+  const V c = ld3(L.pos) + ld3(L.dir) * kEps, u = ld3(L.su) * h, v = ld3(L.sv) * h;
+  double lo[3] = {p.x, p.y, p.z}, hi[3] = {p.x, p.y, p.z};
+  for (int k = 0; k < 4; k++) {
+    const V q = c + u * ((k & 1) ? 1.0 : -1.0) + v * ((k & 2) ? 1.0 : -1.0);
+    const double qq[3] = {q.x, q.y, q.z};
+    for (int i = 0; i < 3; i++) {
+      lo[i] = fmin(lo[i], qq[i]);
+      hi[i] = fmax(hi[i], qq[i]);
+    }
+  }
+  double ext = 0.0;
+  for (int i = 0; i < 3; i++) ext = fmax(ext, fmax(fabs(lo[i]), fabs(hi[i])));
+  const double mg = 1e-4 + 1e-6 * ext;
+  uint64_t m = 0ull;
+  for (int e = 0; e < S.nelems; e++) {
+    const DElement &el = S.elems[e];
+    bool overlap = true;
+    for (int i = 0; i < 3; i++)
+      if (el.pmax[i] < lo[i] - mg || el.pmin[i] > hi[i] + mg) overlap = false;
+    if (!el.world || overlap) m |= 1ull << e;
+  }
+  return m;
+}
+
 // ComputeAreaLightReflection / ComputeRectLightReflection, illumination_utils.cpp:91-417
 // (Q1: the whole accumulated colour is scaled by the shadow hit rate)
 template <uint32_t KINDS = KINDS_ALL>
@@ -789,13 +832,15 @@ __device__ __noinline__ void soft_light(const SceneView &S, const DLight &L, C3 
   if (!L.active) return;
   V center = ld3(L.pos), ln = ld3(L.dir);
   if (dot(ln, p - center) < 0) return;
+  // (a fan of a few shadow rays, as in a Monte Carlo path's 2 samples, does not repay the mask)
+  const uint64_t em = (nls + nes >= 16) ? occluder_mask(S, L, p) : ~0ull;
   int tot_s = 0, tot_h = 0;
   if (m.flags & MF_DIFFUSE) {
     double w = 0;
     int hits = 0;
     for (int i = 0; i < nls; i++) {
       V sp = light_sample_point(L, rng);
-      if (illum_test<KINDS>(S, p, sp, cnt)) {
+      if (illum_test<KINDS>(S, p, sp, cnt, em)) {
         hits++;
         double I = L.intensity;
         double dd = dist(p, sp);
@@ -819,7 +864,7 @@ __device__ __noinline__ void soft_light(const SceneView &S, const DLight &L, C3 
     V Vv = normalize(eye - p);
     for (int i = 0; i < n2; i++) {
       V sp = light_sample_point(L, rng);
-      if (illum_test<KINDS>(S, p, sp, cnt)) {
+      if (illum_test<KINDS>(S, p, sp, cnt, em)) {
         hits++;
         double I = L.intensity;
         double dd = dist(p, sp);
@@ -843,7 +888,7 @@ __device__ __noinline__ void soft_light(const SceneView &S, const DLight &L, C3 
   int hits = 0;
   for (int i = 0; i < nes; i++) {
     V sp = light_sample_point(L, rng);
-    if (illum_test<KINDS>(S, p, sp, cnt)) hits++;
+    if (illum_test<KINDS>(S, p, sp, cnt, em)) hits++;
   }
   tot_h += hits;
   tot_s += nes;

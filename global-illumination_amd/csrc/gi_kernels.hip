@@ -76,7 +76,14 @@ __device__ __forceinline__ void decode_primary(const RenderArgs &a, int64_t b, i
 
 // Threadable_RayTracer body (render.cpp:96-132) + RayTrace (raytracer.cpp:174-233) up to the
 // sample fan-outs. Writes the spawn record the path kernels expand.
-__global__ __launch_bounds__(256) void primary_kernel(RenderArgs a) {
+// Occupancy target: left free, the soft-light call chain (direct_illumination -> soft_light ->
+// illum_test) took 256 VGPRs + 110 AGPRs, one wave per SIMD; at 2 (32 VGPRs spilled) the C3
+// frame (jensen.scn, 128 + 128 shadow rays per primary hit) is 10 % faster (3 waves: 5 %), the
+// images unchanged; C2 (one hard shadow ray) is indifferent.
+#ifndef PRIMARY_WPE
+#define PRIMARY_WPE 2
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PRIMARY_WPE))) void primary_kernel(RenderArgs a) {
   int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t c_ray = 0, c_shadow = 0, c_ind = 0;
   if (b < a.nprim) {

@@ -72,7 +72,9 @@ struct DElement {
   // test, so scene_intersect tests the shapes first and the box only for an element that would
   // take a hit (same result: a box test that fails discards the element's hits either way)
   int32_t shapes_first_ok;
-  int32_t pad;
+  // 1 when the owning node and all its ancestors are the identity: bmin/bmax are world
+  // coordinates (soft_light's occluder mask)
+  int32_t world;
 };
 
 constexpr int GI_MAX_DEPTH = 16;  // scene-graph depth supported on the device

@@ -591,6 +591,9 @@ static Bx flatten(Graph &G, int gi_idx, int parent, HostScene &S) {
     de.shape_count = (int)e.shapes.size();
     Bx eb;
     de.shapes_first_ok = 1;
+    de.world = 1;
+    for (int c = id; c >= 0; c = S.nodes[c].parent)
+      if (!S.nodes[c].identity) de.world = 0;
     for (auto &s : e.shapes) {
       if (s.s.kind != SK_TRI && s.s.kind != SK_SPHERE && s.s.kind != SK_CIRCLE)
         de.shapes_first_ok = 0;

@@ -297,6 +297,8 @@ struct gi_ctx {
   uint32_t dump_fb_max = 0;       // GI_DUMP_FB diagnostics: largest fallback list written
   DBuf ind_cont, ind_ncont;       // indirect paths that continue past their first bounce
   DBuf mc_cont, mc_ncont;         // Monte Carlo paths' indirect sub-paths
+  DBuf mc_cont2, mc_ncont2;       // ... those continuing past a glass / mirror first hit
+  bool mc_sub = true;             // sub-paths' first bounce in mc_sub_kernel (GI_MC_SUB=0: all in ind_cont_kernel)
   DBuf prim_rgb;                  // per-primary sums of the reduction
   DBuf ind_tab, mc_tab;           // row -> tile of the tiled indirect entries; owner of MC path 64k
   DBuf ind_trows, ind_rows;       // indirect paths' tiled slots: rows per tile, their scan
@@ -1184,6 +1186,12 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
       a.mc_cont = c->mc_cont.as<IndCont>();
       a.mc_ncont = c->mc_ncont.as<uint32_t>();
       a.mc_cap_s = (uint32_t)full;
+      if (c->mc_sub) {
+        HIPCHK(c, c->mc_cont2.ensure((size_t)IND_QS * full * sizeof(IndCont)));
+        HIPCHK(c, c->mc_ncont2.ensure(IND_QS * 32 * 4));
+        a.mc_cont2 = c->mc_cont2.as<IndCont>();
+        a.mc_ncont2 = c->mc_ncont2.as<uint32_t>();
+      }
     }
     // single Monte Carlo pass; grow the query lists and re-run on overflow
     uint32_t nq[2] = {0, 0};
@@ -1399,6 +1407,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_SPLIT_IND")) c->split_ind = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_DK")) c->use_dk = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_DK")) c->chunk_dk = atoi(s) != 0;
+  if (const char *s = getenv("GI_MC_SUB")) c->mc_sub = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_LOG")) c->knn_log = atoi(s) != 0;
   if (const char *s = getenv("GI_ELEM_PRETEST")) c->elem_pretest = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_FB_ALL")) c->chunk_fb_all = atoi(s) != 0;
@@ -1455,7 +1464,7 @@ void gi_destroy(gi_ctx *c) {
   DBuf *bufs[] = {&c->d_nodes, &c->d_elems, &c->d_shapes, &c->d_tris, &c->d_bvh, &c->d_mats, &c->d_lights,
                   &c->d_lut, &c->d_stats, &c->spawn, &c->npaths, &c->path_off, &c->base,
                   &c->pixels, &c->rgbf, &c->rgb8, &c->qcount,
-                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont, &c->mc_cont, &c->mc_ncont, &c->prim_rgb, &c->ind_tab, &c->mc_tab, &c->ind_trows, &c->ind_rows, &c->ind_masks};
+                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont, &c->mc_cont, &c->mc_ncont, &c->mc_cont2, &c->mc_ncont2, &c->prim_rgb, &c->ind_tab, &c->mc_tab, &c->ind_trows, &c->ind_rows, &c->ind_masks};
   for (DBuf *b : bufs) b->release();
   c->pack.release();
   for (auto &b : c->recv) b.release();

@@ -46,7 +46,7 @@ struct IndCont {
   int32_t mat;
   uint32_t j;             // queries already issued by the path (mat == -1)
   int32_t tri;            // triangle the continued ray leaves from (-1: none), Hit::tri
-  int32_t pad;
+  int32_t sub;            // 1: a Monte Carlo path's indirect sub-path queued at its first hit
 };
 
 // continuation queue stripes: wave w appends to stripe w % IND_QS (one atomic per wave on a
@@ -104,6 +104,8 @@ struct RenderArgs {
   IndCont *mc_cont;     // Monte Carlo paths' indirect sub-paths, striped the same way
   uint32_t *mc_ncont;
   uint32_t mc_cap_s;
+  IndCont *mc_cont2;    // ... those whose first bounce hit glass / a mirror (mc_sub_kernel),
+  uint32_t *mc_ncont2;  // at that hit, same stripes and capacity
   // Indirect paths' slots, tiled: primaries b in tiles of 64 (T = b / 64); tile T holds
   // ind_rows[T+1] - ind_rows[T] = max n_i over its primaries rows of 64 entries, and indirect
   // path s of primary b is entry tau(b, s) = 64 * (ind_rows[T] + s) + b % 64 (ind_tau). Its

@@ -423,6 +423,7 @@ __device__ __forceinline__ void mc_path(PathCtx &P, V org, V dir, Rng &rng, C3 W
           q.mat = -1;
           q.j = P.j;
           q.tri = h.tri;
+          q.sub = 0;
           P.fixed[0] = -2;  // the sub-path owns the global slot now
         } else {
           mc_indirect<KINDS>(P, h.p + s2 * kEps, s2, rng, w2);
@@ -657,6 +658,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void i
           q.qslot = (uint32_t)P.fixed[0];
           q.mat = h.mat;
           q.tri = h.tri;
+          q.sub = 0;
           }
         }
       }
@@ -712,6 +714,8 @@ void ind_cont_kernel(RenderArgs a, const IndCont *queue, const uint32_t *fill, u
     V org = ld3(q.org), dir = org;
     bool go;
     int iter0;
+    const bool sub = q.sub != 0;  // a Monte Carlo sub-path, its first bounce done (mc_sub_kernel)
+    if (sub) P.j = q.j;
     if (q.mat >= 0) {
       Hit h;
       h.p = ld3(q.hp);
@@ -733,7 +737,7 @@ void ind_cont_kernel(RenderArgs a, const IndCont *queue, const uint32_t *fill, u
     const bool used = P.fixed[0] == -2;
     if (P.fixed[0] >= 0) put_none(a, 0, P.fixed[0]);
     double *bp = a.base + 3 * (int64_t)q.g;
-    if (q.mat >= 0) {
+    if (q.mat >= 0 && !sub) {
       // an indirect path's tiled entry (q.qslot = qind_base + tau): its mask bits
       const int64_t tau = (int64_t)q.qslot - a.qind_base;
       const unsigned long long bit = 1ull << (tau & 63);
@@ -751,6 +755,103 @@ void ind_cont_kernel(RenderArgs a, const IndCont *queue, const uint32_t *fill, u
     }
     tot.shadow += P.cnt.shadow; tot.monte += P.cnt.monte; tot.trans += P.cnt.trans;
     tot.spec += P.cnt.spec; tot.indirect += P.cnt.indirect; tot.caustic += P.cnt.caustic;
+  }
+  path_stats(a, tot);
+}
+
+// The Monte Carlo paths' indirect sub-paths (mc_path's deferred IndirectIllumination sample,
+// montecarlo.cpp:177-305 from a diffuse hit): their first bounce, one per thread, in the lean
+// shape of ind_kernel. A sub-path that hits a diffuse-only material ends there (its query, or
+// its background term), as most do; one that hits glass or a mirror is queued at that hit to
+// mc_cont2 (flag `sub`) and finished by ind_cont_kernel with the Fresnel / refraction / lobe
+// sampling code. Same arithmetic, RNG stream and order of additions to the path's base as
+// ind_cont_kernel's whole-loop ray entries, so the same image; the 4-wave lean kernel replaces
+// the 3-wave general loop for the common one-bounce case: C2 1,554 -> 1,536 ms per frame, C3
+// 2,769 -> 2,730 ms, images identical (GI_MC_SUB=0 restores the single queue).
+#ifndef MC_SUB_WPE
+#define MC_SUB_WPE 4  // 3 measured equal (C2 1,536 vs 1,539 ms)
+#endif
+template <uint32_t KINDS>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(MC_SUB_WPE)))
+void mc_sub_kernel(RenderArgs a, const IndCont *queue, const uint32_t *fill, uint32_t cap_s) {
+  const uint32_t stripe = blockIdx.x % IND_QS, part = blockIdx.x / IND_QS;
+  const uint32_t parts = gridDim.x / IND_QS;
+  const uint32_t n = min(fill[stripe * 32], cap_s);
+  Counts tot = {0, 0, 0, 0, 0, 0};
+  const uint32_t rounds = (n + parts * blockDim.x - 1) / (parts * blockDim.x);
+  for (uint32_t r = 0; r < rounds; r++) {
+    const uint32_t idx = (r * parts + part) * blockDim.x + threadIdx.x;
+    const bool on = idx < n;
+    bool queue_it = false;
+    Hit h;
+    // the entry is read where its fields are used (a register copy of all 128 B spilled)
+    const IndCont &q = queue[(size_t)stripe * cap_s + (on ? idx : 0u)];
+    PathCtx P;
+    Rng rng;
+    C3 W = rgb(0, 0, 0);
+    V org = mk(0, 0, 0);
+    if (on) {
+      path_init(P, a, q.g, q.prim, (int)q.pslot);
+      P.fixed[0] = (q.qslot == 0xffffffffu) ? -1 : (int64_t)q.qslot;
+      P.hint = q.tri;
+      P.j = q.j;
+      rng.key = q.rkey;
+      rng.ctr = q.rctr;
+      W = ldc(q.w);
+      org = ld3(q.org);
+      V dir = ld3(q.hp);
+      C3 tw = rgb(1, 1, 1);
+      if (a.F.max_monte_depth > 0) {
+        if (!scene_intersect<KINDS>(a.S, org, dir, h, P.hint)) {
+          P.base += W * (tw * ldc(a.S.background));
+        } else {
+          P.cnt.monte++;
+          P.hint = h.tri;
+          if (diffuse_only(a.S.mats[h.mat])) ind_shade<true>(P, h, org, dir, rng, W, tw);
+          else queue_it = true;
+        }
+      }
+    }
+    // glass / mirror first hits: wave-aggregated append to the same stripe of mc_cont2 (at most
+    // this stripe's fill, so within its capacity)
+    const uint64_t act = __ballot(queue_it);
+    if (act) {
+      const int lane = (int)(threadIdx.x & 63);
+      const int leader = __ffsll((long long)act) - 1;
+      uint32_t base = 0;
+      if (lane == leader) base = atomicAdd(&a.mc_ncont2[stripe * 32], (uint32_t)__popcll(act));
+      base = (uint32_t)__shfl((int)base, leader, 64);
+      if (queue_it) {
+        IndCont &o = a.mc_cont2[(size_t)stripe * cap_s + base +
+                                (uint32_t)__popcll(act & ((1ull << lane) - 1ull))];
+        o.org[0] = org.x; o.org[1] = org.y; o.org[2] = org.z;
+        o.hp[0] = h.p.x; o.hp[1] = h.p.y; o.hp[2] = h.p.z;
+        o.hn[0] = h.n.x; o.hn[1] = h.n.y; o.hn[2] = h.n.z;
+        o.w[0] = W.r; o.w[1] = W.g; o.w[2] = W.b;
+        o.rkey = rng.key;
+        o.rctr = rng.ctr;
+        o.g = q.g;
+        o.prim = q.prim;
+        o.pslot = q.pslot;
+        o.qslot = q.qslot;
+        o.mat = h.mat;
+        o.j = P.j;
+        o.tri = h.tri;
+        o.sub = 1;
+      }
+    }
+    if (on && !queue_it) {
+      if (P.fixed[0] >= 0) put_none(a, 0, P.fixed[0]);
+      // the sub-path's background term is the last addition to the path's sum
+      double *bp = a.base + 3 * (int64_t)q.g;
+      bp[0] = bp[0] + P.base.r;
+      bp[1] = bp[1] + P.base.g;
+      bp[2] = bp[2] + P.base.b;
+    }
+    if (on) {
+      tot.shadow += P.cnt.shadow; tot.monte += P.cnt.monte; tot.trans += P.cnt.trans;
+      tot.spec += P.cnt.spec; tot.indirect += P.cnt.indirect; tot.caustic += P.cnt.caustic;
+    }
   }
   path_stats(a, tot);
 }
@@ -1548,6 +1649,14 @@ void launch_cont(const RenderArgs &a, const IndCont *q, const uint32_t *fill, ui
   else
     ind_cont_kernel<KINDS_ALL><<<IND_QS * 32, 128, 0, st>>>(a, q, fill, cap_s);
 }
+static void launch_mc_sub(const RenderArgs &a, hipStream_t st) {
+  if ((a.S.kinds & ~KINDS_TRI_SPHERE) == 0)
+    mc_sub_kernel<KINDS_TRI_SPHERE><<<IND_QS * 32, 128, 0, st>>>(a, a.mc_cont, a.mc_ncont, a.mc_cap_s);
+  else if ((a.S.kinds & ~KINDS_POLY) == 0)
+    mc_sub_kernel<KINDS_POLY><<<IND_QS * 32, 128, 0, st>>>(a, a.mc_cont, a.mc_ncont, a.mc_cap_s);
+  else
+    mc_sub_kernel<KINDS_ALL><<<IND_QS * 32, 128, 0, st>>>(a, a.mc_cont, a.mc_ncont, a.mc_cap_s);
+}
 // Path expansion of one batch. The Monte Carlo paths (mc_kernel: few, long, one wave per SIMD
 // by its registers) run on the side stream st2 when given, concurrently with the indirect paths
 // on st, so their waves share the CUs instead of running as a low-occupancy tail; st waits for
@@ -1574,7 +1683,13 @@ void launch_path(const RenderArgs &a, hipStream_t st, hipStream_t st2, hipEvent_
       } else {
         mc_kernel<KINDS_ALL, true, false><<<g, 128, 0, ms>>>(a);
       }
-      launch_cont(a, a.mc_cont, a.mc_ncont, a.mc_cap_s, ms);
+      if (a.mc_cont2) {
+        (void)hipMemsetAsync(a.mc_ncont2, 0, IND_QS * 32 * sizeof(uint32_t), ms);
+        launch_mc_sub(a, ms);
+        launch_cont(a, a.mc_cont2, a.mc_ncont2, a.mc_cap_s, ms);
+      } else {
+        launch_cont(a, a.mc_cont, a.mc_ncont, a.mc_cap_s, ms);
+      }
     } else {
       mc_kernel<KINDS_ALL, false, false><<<g, 128, 0, ms>>>(a);
     }

@@ -158,16 +158,18 @@ def test_indirect_continuation_queue_is_exact(name, extra):
     """ind_kernel's continuation queue (GI_SPLIT_IND=1, default) only regroups the bounces of
     MonteCarlo_IndirectSample (montecarlo.cpp:177-305) that follow a glass/mirror hit: the f32
     image and every -v counter equal the one-loop-per-lane kernel's (GI_SPLIT_IND=0), also when
-    the queue starts far too small (GI_IND_FRAC) and the batch is re-run with more room."""
+    the queue starts far too small (GI_IND_FRAC) and the batch is re-run with more room, and
+    when the Monte Carlo paths' sub-paths skip their lean first-bounce kernel (GI_MC_SUB=0)."""
     args = [scene(name), "/tmp/x.png", "-resolution", "32", "32", "-aa", "1", "-it", "32",
             "-tt", "8", "-st", "8", "-seed", "4"] + extra
     p, sc, _o, w, h, aa, real = gi_amd.ParseArgs(args)
     out = []
-    keys = ("GI_SPLIT_IND", "GI_IND_FRAC")
+    keys = ("GI_SPLIT_IND", "GI_IND_FRAC", "GI_MC_SUB")
     old = {k: os.environ.get(k) for k in keys}
     try:
         for env in ({"GI_SPLIT_IND": "0"}, {"GI_SPLIT_IND": "1"},
-                    {"GI_SPLIT_IND": "1", "GI_IND_FRAC": "0.00001"}):
+                    {"GI_SPLIT_IND": "1", "GI_IND_FRAC": "0.00001"},
+                    {"GI_SPLIT_IND": "1", "GI_MC_SUB": "0"}):
             for k in keys:
                 os.environ.pop(k, None)
             os.environ.update(env)

@@ -58,7 +58,58 @@ def parse():
     ap.add_argument("--shard", default="",
                     help="S/N: render only tile shard S of N on this GPU (one GPU's share of an "
                          "N-GPU frame, e.g. C5's 0/8); value = that shard's pixel-samples/s")
+    ap.add_argument("--balance", type=int, default=0,
+                    help="N: render every tile shard s/N of the frame in turn on this GPU and print "
+                         "the per-shard times (min/mean/max: an N-GPU frame takes the slowest)")
     return ap.parse_args()
+
+
+def shard_balance(a):
+    """Shard balance of an N-GPU frame measured on one GPU (render.cpp:90's interleave re-cut as
+    16x16 tiles, tile t on GPU t % N): each shard rendered `steps` times after one warmup render of
+    shard 0 (buffer growth), its time the median. Prints one JSON line."""
+    import torch
+    import gi_amd
+    N = a.balance
+    args = [os.path.join(SCENES, a.scene), "/tmp/bench.png", "-resolution", str(a.res),
+            str(a.res), "-aa", str(a.aa), "-global", str(a.global_photons), "-caustic",
+            str(a.caustic_photons), "-seed", str(a.seed)] + a.extra.split()
+    p, sc, _o, w, h, aa, real = gi_amd.ParseArgs(args)
+    r = gi_amd.Renderer(0, p)
+    r.ReadScene(sc, real)
+    t0 = time.perf_counter()
+    r.MapPhotons()
+    photon_s = time.perf_counter() - t0
+    npix = [r.shard_pixels(w, h, a.tile, s, N) for s in range(N)]
+    buf = torch.zeros((max(npix), 4), dtype=torch.float32, device="cuda:0")
+    torch.cuda.synchronize()
+    for _ in range(a.warmup):
+        r.render_tiles_packed(aa, w, h, a.tile, 0, N, buf.data_ptr(), max(npix))
+    torch.cuda.synchronize()
+    times = []
+    for s in range(N):
+        ts = []
+        for _ in range(max(1, a.steps)):
+            t1 = time.perf_counter()
+            r.render_tiles_packed(aa, w, h, a.tile, s, N, buf.data_ptr(), max(npix))
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t1)
+        times.append(float(np.median(ts)))
+        print(f"shard {s}/{N}: {npix[s]} px, {times[-1] * 1e3:.1f} ms", flush=True)
+    mean = float(np.mean(times))
+    spf = w * h * 4 ** aa * p.dof_test
+    line = {"metric": "shard balance (ms per shard, one GPU each)",
+            "config": {"workload": f"{a.scene} {w}x{h} aa={aa} "
+                                   f"{a.global_photons}+{a.caustic_photons} photons {a.extra}".strip(),
+                       "tile": a.tile, "nshards": N, "photon_map_s": round(photon_s, 3),
+                       "assignment": f"tile t -> shard t % {N}"},
+            "shard_ms": [round(t * 1e3, 1) for t in times], "shard_pixels": npix,
+            "min_ms": round(min(times) * 1e3, 1), "mean_ms": round(mean * 1e3, 1),
+            "max_ms": round(max(times) * 1e3, 1), "max_over_mean": round(max(times) / mean, 4),
+            "sum_ms": round(sum(times) * 1e3, 1),
+            "frame_Mpx_samples_per_s_at_N": round(spf / max(times) / 1e6, 3)}
+    print(json.dumps(line), flush=True)
+    r.close()
 
 
 # the roofline "launch": the chunk k-NN kernel and its per-lane fallback on the global map
@@ -173,6 +224,8 @@ def device_list(n):
 
 def main():
     a = parse()
+    if a.balance:
+        return shard_balance(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -324,6 +377,15 @@ def main():
                               " (global map k-NN + EstimateRadiance; avg_launch_ms = their sum)",
                     "bytes_per_unit": "16 B per photon returned (SURVEY.md 8(d))",
                     "global": g, "caustic_kernel": dict(c, kernel=KNN_KINDS.get(kind[1], str(kind[1])))}
+        # frame-level figure, BASELINE.md section 3.4: every k-NN photon returned (both maps) x 16 B
+        # plus the 12-B output pixel per sample, over the whole frame's wall time, against the
+        # N GPUs' aggregate peak
+        frame_bytes = (agg["ph0"] + agg["ph1"]) * BYTES_PER_PHOTON + \
+            BYTES_PER_SAMPLE * samples_per_step * a.steps
+        frame_ach = frame_bytes / elapsed / 1e9
+        roofline["frame_achieved"] = round(frame_ach, 2)
+        roofline["frame_frac"] = round(frame_ach / (HBM_PEAK_GBPS * n_gpus), 5)
+        roofline["frame_bytes_per_sample"] = round(frame_bytes / (samples_per_step * a.steps), 1)
         cpu = None
         if not a.no_cpu_baseline and n_gpus == 1:
             cpu = cpu_baseline(a)

@@ -100,8 +100,14 @@ def render_sharded_packed(renderer, aa, width, height, tile, rank, world, dist, 
 def render_sharded(renderer, aa, width, height, tile, rank, world, dist, device=None):
     """One frame on `world` ranks: this rank's tiles, then the tile gather to rank 0.
     Returns (full image on rank 0 / None, this rank's render stats): (rgb8, rgbf) on the
-    device path, the f32 image on the host path."""
-    if device is not None and hasattr(renderer, "render_tiles_packed"):
+    device path, the f32 image on the host path.
+
+    The packed path hands raw data_ptr()s to gi_render_tiles_packed / gi_compose_tiles, which
+    take DEVICE pointers (gi.h): it is taken only for a CUDA device, or for a renderer that says
+    its packed entry points read host memory (`packed_host_memory`, the CPU test stand-in)."""
+    packed_ok = device is not None and hasattr(renderer, "render_tiles_packed") and (
+        device.type == "cuda" or getattr(renderer, "packed_host_memory", False))
+    if packed_ok:
         return render_sharded_packed(renderer, aa, width, height, tile, rank, world, dist, device)
     img, st = renderer.render_tiles(aa, width, height, tile, rank, world)
     owner = tile_owner_map(width, height, tile, world)

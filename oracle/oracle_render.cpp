@@ -25,6 +25,14 @@
 
 namespace oracle {
 
+// Diagnostic only (oracle_run_tags): with g_tagging, photons carry in `flags`
+// the material of their first specular / transmissive bounce (+2; the default material -1 -> 1,
+// no such bounce -> 0), and with g_tag_select = m the caustic estimate sums only the photons of
+// material m over the SAME K-set and radius as the full map, so the per-material layers add up
+// to the caustic layer exactly (before clamping and quantisation).
+static bool g_tagging = false;
+static int g_tag_select = -100;   // -100: every photon
+
 // ---------------------------------------------------------------------------------------
 // Per-thread counters (render.cpp:26-41)
 // ---------------------------------------------------------------------------------------
@@ -660,6 +668,7 @@ static void estimate_radiance(const Ctx &c, V3 p, V3 normal, Rgb &color, const B
     V3 inc(c.lut[3 * d], c.lut[3 * d + 1], c.lut[3 * d + 2]);
     double perp = dot(normal, inc);
     if ((cos_theta < 0 && perp < 0) || (cos_theta > 0 && perp > 0)) continue;
+    if (g_tag_select != -100 && &map == &c.cmap && ph.flags != g_tag_select + 2) continue;
     Rgb pc = rgbe_to_rgb(ph.rgbe);
     double ca = dot(exact, -inc);
     if (ca < 0) ca = 0;
@@ -990,7 +999,8 @@ static void ray_trace(const Ctx &c, const Hit &h, V3 eye, Rgb &color, Rng &rng,
 // Photon tracing (photontracer.cpp, photonmap.cpp, photon_utils.cpp StorePhoton)
 // ---------------------------------------------------------------------------------------
 // StorePhoton, photon_utils.cpp:40-65 (direction code clamped to the valid acos domain)
-static void store_photon(const Rgb &power, V3 inc, V3 p, std::vector<Photon> &out) {
+static void store_photon(const Rgb &power, V3 inc, V3 p, std::vector<Photon> &out,
+                         int tag = 0) {
   Photon ph;
   ph.pos[0] = (float)p.x; ph.pos[1] = (float)p.y; ph.pos[2] = (float)p.z;
   rgb_to_rgbe(power, ph.rgbe);
@@ -998,7 +1008,7 @@ static void store_photon(const Rgb &power, V3 inc, V3 p, std::vector<Photon> &ou
   double z = inc.z < -1.0 ? -1.0 : (inc.z > 1.0 ? 1.0 : inc.z);
   int theta = (uint8_t)(255.0 * acos(z) / PI);
   ph.dir = (uint16_t)(phi * 256 + theta);
-  ph.flags = 0;
+  ph.flags = (uint16_t)(g_tagging ? tag : 0);
   out.push_back(ph);
 }
 
@@ -1007,6 +1017,7 @@ static void photon_trace(const Ctx &c, V3 org, V3 dir, Rgb photon, bool caustic,
                          std::vector<Photon> &out) {
   const gi_params &P = c.P;
   bool store = (!caustic && !P.fast_global);
+  int tag = 0;   // diagnostic: material of the first specular / transmissive bounce, + 2
   V3 ray_start = org;
   for (int iter = 0; iter < P.max_photon_depth; iter++) {
     Hit h;
@@ -1014,7 +1025,7 @@ static void photon_trace(const Ctx &c, V3 org, V3 dir, Rgb photon, bool caustic,
     const Brdf &brdf = brdf_of(c, h.material);
     V3 view = normalize(h.point - ray_start);
     double cos_theta = dot(h.normal, -view);
-    if (brdf.isDiffuse() && store) store_photon(photon, view, h.point, out);
+    if (brdf.isDiffuse() && store) store_photon(photon, view, h.point, out, tag);
     double R = 0;
     if (P.fresnel && brdf.isTransparent()) R = reflection_coeff(P.ir_air, cos_theta, brdf.ir);
     double mc = max_channel(photon);
@@ -1033,11 +1044,13 @@ static void photon_trace(const Ctx &c, V3 org, V3 dir, Rgb photon, bool caustic,
       photon *= brdf.kd / pd;
     } else if (rnd < pd + pt) {
       if (caustic) store = true;
+      if (!tag) tag = h.material + 2;
       V3 ex = transmissive_bounce(P.ir_air, h.normal, view, cos_theta, brdf.ir);
       sb = P.distrib_transmissive ? specular_sample(ex, brdf.n, cos_theta, rng) : ex;
       photon *= (1.0 - R) * brdf.kt / pt;
     } else if (rnd < pd + pt + ps) {
       if (caustic) store = true;
+      if (!tag) tag = h.material + 2;
       V3 ex = reflective_bounce(h.normal, view, cos_theta);
       sb = P.distrib_specular ? specular_sample(ex, brdf.n, cos_theta, rng) : ex;
       photon *= (brdf.ks + R * brdf.kt) / ps;
@@ -1548,6 +1561,39 @@ int oracle_run(int argc, char **argv, uint8_t *rgb, int64_t cap, double *stats, 
     memcpy(stats, s, sizeof s);
   }
   if (write && !write_png(out, img)) { delete c; return 3; }
+  delete c;
+  return 0;
+}
+
+// Diagnostic: one photon-map build with tagged caustic photons, then one
+// render per entry of tags[] (-100 = all photons, m = only photons whose first specular /
+// transmissive bounce hit material m, -1 = the default material); rgbf gets ntags box-filtered
+// float images (w*h*3 each), rgb (optional) the 8-bit ones.
+int oracle_run_tags(int argc, char **argv, const int *tags, int ntags, float *rgbf, uint8_t *rgb,
+                    int64_t cap_px) {
+  Ctx *c = new Ctx();
+  std::string out, err;
+  int w, h, aa;
+  if (!setup(*c, argc, argv, out, w, h, aa, err)) {
+    fprintf(stderr, "%s\n", err.c_str());
+    delete c;
+    return 1;
+  }
+  if ((int64_t)w * h > cap_px) { delete c; return 2; }
+  g_tagging = true;
+  gi_photon_stats pst{};
+  if (c->P.indirect_illum || c->P.caustic_illum || c->P.direct_photon_illum) map_photons(*c, &pst);
+  g_tagging = false;
+  for (int t = 0; t < ntags; t++) {
+    g_tag_select = tags[t];
+    Image img;
+    Counters cnt;
+    double rs = 0;
+    render_image(*c, aa, w, h, img, cnt, &rs);
+    memcpy(rgbf + (size_t)t * w * h * 3, img.rgbf.data(), sizeof(float) * w * h * 3);
+    if (rgb) memcpy(rgb + (size_t)t * w * h * 3, img.rgb.data(), (size_t)w * h * 3);
+  }
+  g_tag_select = -100;
   delete c;
   return 0;
 }

@@ -35,6 +35,8 @@ class FakeTiles:
 class FakePacked:
     """gi_render_tiles_packed / gi_compose_tiles contract on host memory: the shard's pixels in
     packed order, 16 B each (f32 RGB + u8 RGB bits), written through a raw pointer."""
+    packed_host_memory = True   # opts in to the packed path with a CPU device
+
     @staticmethod
     def _view(ptr, n):
         import ctypes as C
@@ -58,6 +60,16 @@ class FakePacked:
         return (full * 255).astype(np.uint8), full
 
 
+class DevicePacked(FakeTiles):
+    """A renderer whose packed entry points take device pointers only (like gi_amd.Renderer):
+    given a CPU device, render_sharded must take the host path and never call them."""
+    def render_tiles_packed(self, *a):
+        raise AssertionError("packed path taken with a CPU device")
+
+    def compose_tiles(self, *a, **k):
+        raise AssertionError("packed path taken with a CPU device")
+
+
 def _worker(rank, world, port, w, h, tile, q, packed=False):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -71,7 +83,11 @@ def _worker(rank, world, port, w, h, tile, q, packed=False):
             sent.append(t.numel())
             return real_gather(t, parts, dst=dst)
         dist.gather = spy
-        if packed:
+        if packed == "device_only":
+            import torch
+            img, st = gi_dist.render_sharded(DevicePacked(), 0, w, h, tile, rank, world, dist,
+                                             torch.device("cpu"))
+        elif packed:
             import torch
             img, st = gi_dist.render_sharded(FakePacked(), 0, w, h, tile, rank, world, dist,
                                              torch.device("cpu"))
@@ -83,7 +99,8 @@ def _worker(rank, world, port, w, h, tile, q, packed=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("packed", [False, True], ids=["host", "packed"])
+@pytest.mark.parametrize("packed", [False, True, "device_only"],
+                         ids=["host", "packed", "cpu_device_host_path"])
 @pytest.mark.parametrize("world,w,h,tile", [(2, 70, 45, 16), (3, 64, 64, 16)])
 def test_sharded_gather_equals_full_frame(world, w, h, tile, packed):
     ctx = mp.get_context("spawn")
@@ -104,7 +121,7 @@ def test_sharded_gather_equals_full_frame(world, w, h, tile, packed):
     # one gather per rank of at most the largest shard (not the whole frame)
     biggest = int(np.bincount(gi_dist.tile_owner_map(w, h, tile, world).ravel()).max())
     for o in out:
-        assert o[3] == [biggest * (4 if packed else 3)]
+        assert o[3] == [biggest * (4 if packed is True else 3)]
         assert biggest * world < w * h + tile * tile * world
 
 

@@ -321,6 +321,12 @@ struct gi_ctx {
   DBuf scan_lvl[8], scan_out[8];
   // photon tracing scratch
   DBuf pcounts, poffs, pbuf;
+  DBuf pkeys, pcursor, ptmp;      // single pass: slot keys, slot counter, sorted photons (host sink)
+  DBuf pacc, pglob;               // maps being traced on the device (emission order), held global map
+  int64_t pacc_n = 0;
+  KeySortScratch psort;
+  double prate[2] = {2.0, 2.0};   // stored per emitted photon in the last launch, per map
+  bool photon_2pass = false;      // GI_PHOTON_2PASS=1: count pass + scan + re-trace (r03)
   // Primary samples per batch. Denser query batches make the chunk k-NN's 64 Morton-adjacent
   // queries span less of a K-neighbourhood (fewer LDS candidates per query): C2 at 2^19 / 2^20 /
   // 2^21 / 2^22 ran 6.85 / 7.44 / 7.89 / 7.69 Mpixel-samples/s. A batch is also capped by the
@@ -484,12 +490,13 @@ int upload_map(gi_ctx *c, int mi) {
 
 // the device build (f1): the emission-ordered photons go up once, the tree, the kd-order
 // arrays and the permutation come back (perm only to the host, for the test seams' indices)
-int build_map_device(gi_ctx *c, int mi) {
+int build_map_device(gi_ctx *c, int mi, bool upload_storage = true) {
   HostMap &H = c->hmap[mi];
   DevMap &D = c->dmap[mi];
   const int64_t n = (int64_t)H.storage.size();
   static_assert(sizeof(gi_photon) == sizeof(KdPhoton), "photon record layout");
-  HIPCHK(c, upload(c->kd_ph, H.storage.data(), (size_t)n * sizeof(gi_photon), c->stream));
+  if (upload_storage)  // else kd_ph already holds H.storage (traced on this device)
+    HIPCHK(c, upload(c->kd_ph, H.storage.data(), (size_t)n * sizeof(gi_photon), c->stream));
   int64_t L = 1;
   while (L * c->leaf_size[mi] < n) L *= 2;
   HIPCHK(c, D.pos4.ensure((size_t)n * 16));
@@ -526,6 +533,36 @@ int set_map(gi_ctx *c, int mi, const gi_photon *ph, int64_t n) {
   return build_map(c, mi);
 }
 
+// map mi from n emission-ordered photons already in device buffer `dev` (traced here): one copy
+// to the host (the map's storage order, gi_get_photon_map) and, for the device build, `dev`
+// becomes the build's input buffer without a re-upload
+int set_map_device(gi_ctx *c, int mi, DBuf &dev, int64_t n) {
+  HostMap &H = c->hmap[mi];
+  H = HostMap();
+  H.storage.resize(n);
+  if (n) {
+    HIPCHK(c, hipMemcpyAsync(H.storage.data(), dev.p, (size_t)n * sizeof(gi_photon),
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  if (!c->gpu_kd) return build_map(c, mi);
+  std::swap(c->kd_ph, dev);
+  return build_map_device(c, mi, false);
+}
+
+// grow a device buffer to `want` bytes keeping its first `used` bytes
+hipError_t grow_keep(DBuf &b, size_t used, size_t want, hipStream_t st) {
+  if (want <= b.cap && b.p) return hipSuccess;
+  DBuf nb;
+  hipError_t e = nb.ensure(std::max(want, b.cap + b.cap / 2));
+  if (e != hipSuccess) return e;
+  if (used) e = hipMemcpyAsync(nb.p, b.p, used, hipMemcpyDeviceToDevice, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  b.release();
+  b = nb;
+  return e;
+}
+
 // LightPower, graphics_utils.cpp:223-258
 double light_power(const HostScene &S, const DLight &L) {
   const double PI = 3.14159265358979323846;
@@ -550,15 +587,21 @@ double light_power(const HostScene &S, const DLight &L) {
   return (L.color[0] + L.color[1] + L.color[2]) * area * flux;
 }
 
-// trace photons [e0, e0+n) of one light on this context's device and append the stored ones
-// (emission order)
+// trace photons [e0, e0+n) of one light on this context's device and append the stored ones in
+// emission order: to `host` when given (device sets concatenate their parts there), else to the
+// device map being built (pacc / pacc_n).
+//
+// One pass (PhotonTrace, photontracer.cpp:28-176): every stored photon takes a slot from one
+// atomic per wave (StorePhoton's local buffer + flush, photon_utils.cpp:19-65, re-cut as a wave
+// ballot + prefix) with the key (emission index, store ordinal); a radix sort of the keys and a
+// gather restore emission order, so the map is the same photon for photon as the count pass +
+// scan + re-trace (GI_PHOTON_2PASS=1) it replaces. A launch that stores more photons than the
+// slots it was given is re-run with room (the RNG is keyed by emission index: same photons).
 int trace_batch_dev(gi_ctx *c, int caustic, int light, int64_t e0, int64_t n,
-                    std::vector<gi_photon> &out) {
+                    std::vector<gi_photon> *host) {
   const int64_t CH = 1 << 22;
   for (int64_t s = 0; s < n; s += CH) {
     int64_t m = std::min(CH, n - s);
-    HIPCHK(c, c->pcounts.ensure((size_t)m * 4));
-    HIPCHK(c, c->poffs.ensure((size_t)(m + 1) * 4));
     PhotonArgs a;
     memset(&a, 0, sizeof a);
     a.S = make_view(c);
@@ -567,26 +610,88 @@ int trace_batch_dev(gi_ctx *c, int caustic, int light, int64_t e0, int64_t n,
     a.caustic = caustic;
     a.e0 = e0 + s;
     a.n = m;
-    a.counts = c->pcounts.as<uint32_t>();
-    a.offsets = c->poffs.as<uint32_t>();
-    launch_photons(a, false, c->stream);
-    HIPCHK(c, hipGetLastError());
-    ScanTemp t = scan_temp(c, m);
-    HIPCHK(c, launch_scan(c->pcounts.as<uint32_t>(), c->poffs.as<uint32_t>(), m, t, c->stream));
     uint32_t total = 0;
-    HIPCHK(c, hipMemcpyAsync(&total, c->poffs.as<uint32_t>() + m, 4, hipMemcpyDeviceToHost,
-                             c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (total == 0) continue;
-    HIPCHK(c, c->pbuf.ensure((size_t)total * sizeof(gi_photon_dev)));
-    a.out = c->pbuf.as<gi_photon_dev>();
-    launch_photons(a, true, c->stream);
-    HIPCHK(c, hipGetLastError());
-    size_t old = out.size();
-    out.resize(old + total);
-    HIPCHK(c, hipMemcpyAsync(out.data() + old, c->pbuf.p, (size_t)total * sizeof(gi_photon),
-                             hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    gi_photon_dev *sorted = nullptr;  // emission-ordered photons of this launch (device)
+    if (c->photon_2pass) {
+      HIPCHK(c, c->pcounts.ensure((size_t)m * 4));
+      HIPCHK(c, c->poffs.ensure((size_t)(m + 1) * 4));
+      a.counts = c->pcounts.as<uint32_t>();
+      a.offsets = c->poffs.as<uint32_t>();
+      launch_photons(a, PM_COUNT, c->stream);
+      HIPCHK(c, hipGetLastError());
+      ScanTemp t = scan_temp(c, m);
+      HIPCHK(c, launch_scan(c->pcounts.as<uint32_t>(), c->poffs.as<uint32_t>(), m, t, c->stream));
+      HIPCHK(c, hipMemcpyAsync(&total, c->poffs.as<uint32_t>() + m, 4, hipMemcpyDeviceToHost,
+                               c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      if (total == 0) continue;
+      HIPCHK(c, c->pbuf.ensure((size_t)total * sizeof(gi_photon_dev)));
+      a.out = c->pbuf.as<gi_photon_dev>();
+      launch_photons(a, PM_EMIT, c->stream);
+      HIPCHK(c, hipGetLastError());
+      sorted = c->pbuf.as<gi_photon_dev>();
+    } else {
+      int obits = 1;
+      while (obits < 40 && (1LL << obits) < (int64_t)c->P.max_photon_depth) obits++;
+      int jbits = 1;
+      while ((1LL << jbits) < m) jbits++;
+      double want = (double)m * (c->prate[caustic] * 1.25 + 0.02) + 4096.0;
+      uint32_t cap = (uint32_t)std::min(want, 4.0e9);
+      HIPCHK(c, c->pcursor.ensure(4));
+      for (;;) {
+        HIPCHK(c, c->pbuf.ensure((size_t)cap * sizeof(gi_photon_dev)));
+        HIPCHK(c, c->pkeys.ensure((size_t)cap * 8));
+        HIPCHK(c, hipMemsetAsync(c->pcursor.p, 0, 4, c->stream));
+        a.out = c->pbuf.as<gi_photon_dev>();
+        a.keys = c->pkeys.as<uint64_t>();
+        a.cursor = c->pcursor.as<uint32_t>();
+        a.cap = cap;
+        a.obits = obits;
+        launch_photons(a, PM_APPEND, c->stream);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(&total, c->pcursor.p, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (total <= cap) break;
+        if ((double)total * 1.1 + 4096.0 > 4.0e9)
+          return fail(c, GI_ERR_ALLOC, "photon launch stores more than 2^32 photons");
+        cap = (uint32_t)((double)total * 1.1 + 4096.0);
+      }
+      c->prate[caustic] = (double)total / (double)m;
+      if (total == 0) continue;
+      uint64_t *skeys = nullptr;
+      uint32_t *slots = nullptr;
+      HIPCHK(c, key_order(c->pkeys.as<uint64_t>(), total, jbits + obits, c->psort, &skeys,
+                          &slots, c->stream));
+      gi_photon_dev *dst;
+      if (host) {
+        HIPCHK(c, c->ptmp.ensure((size_t)total * sizeof(gi_photon_dev)));
+        dst = c->ptmp.as<gi_photon_dev>();
+      } else {
+        HIPCHK(c, grow_keep(c->pacc, (size_t)c->pacc_n * sizeof(gi_photon_dev),
+                            (size_t)(c->pacc_n + total) * sizeof(gi_photon_dev), c->stream));
+        dst = c->pacc.as<gi_photon_dev>() + c->pacc_n;
+      }
+      launch_photon_gather(c->pbuf.as<gi_photon_dev>(), slots, total, dst, c->stream);
+      HIPCHK(c, hipGetLastError());
+      sorted = dst;
+    }
+    if (host) {
+      size_t old = host->size();
+      host->resize(old + total);
+      HIPCHK(c, hipMemcpyAsync(host->data() + old, sorted, (size_t)total * sizeof(gi_photon),
+                               hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+    } else if (sorted != c->pacc.as<gi_photon_dev>() + c->pacc_n) {  // 2-pass: append the launch
+      HIPCHK(c, grow_keep(c->pacc, (size_t)c->pacc_n * sizeof(gi_photon_dev),
+                          (size_t)(c->pacc_n + total) * sizeof(gi_photon_dev), c->stream));
+      HIPCHK(c, hipMemcpyAsync(c->pacc.as<gi_photon_dev>() + c->pacc_n, sorted,
+                               (size_t)total * sizeof(gi_photon_dev), hipMemcpyDeviceToDevice,
+                               c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      c->pacc_n += total;
+    } else {
+      c->pacc_n += total;
+    }
   }
   return GI_OK;
 }
@@ -629,23 +734,25 @@ int on_devices(gi_ctx *c, Fn fn) {
 // piece per device (the RNG is keyed by emission index, so the concatenation in device order
 // is the one-device result photon for photon)
 int trace_batch(gi_ctx *c, int caustic, int light, int64_t e0, int64_t n,
-                std::vector<gi_photon> &out) {
+                std::vector<gi_photon> *out) {
   const int nd = 1 + (int)c->peers.size();
   if (nd == 1 || n < 4096 * (int64_t)nd) return trace_batch_dev(c, caustic, light, e0, n, out);
   std::vector<std::vector<gi_photon>> part(nd);
   int rc = on_devices(c, [&](int k, gi_ctx *d) -> int {
     int64_t a = e0 + n * k / nd, b = e0 + n * (k + 1) / nd;
-    return trace_batch_dev(d, caustic, light, a, b - a, part[k]);
+    return trace_batch_dev(d, caustic, light, a, b - a, &part[k]);
   });
   if (rc) return rc;
-  for (auto &p : part) out.insert(out.end(), p.begin(), p.end());
+  for (auto &p : part) out->insert(out->end(), p.begin(), p.end());
   return GI_OK;
 }
 
-// adaptive emission rounds of Threadable_PhotonTracer (photonmap.cpp:145-257), one emitter
+// adaptive emission rounds of Threadable_PhotonTracer (photonmap.cpp:145-257), one emitter.
+// The map grows in `map` (device sets) or, when `map` is null, on this device (pacc / pacc_n).
 int trace_map(gi_ctx *c, int caustic, int64_t goal, const std::vector<double> &powers,
-              double total_power, std::vector<gi_photon> &map, int64_t &emitted) {
+              double total_power, std::vector<gi_photon> *map, int64_t &emitted) {
   int64_t stored = 0;
+  if (!map) c->pacc_n = 0;
   emitted = 0;
   double rate = caustic ? (double)c->P.max_photon_depth : 4.0;
   double slowdown = 1.0;
@@ -663,7 +770,7 @@ int trace_map(gi_ctx *c, int caustic, int64_t goal, const std::vector<double> &p
       assigned += num;
     }
     emitted += assigned;
-    stored = (int64_t)map.size();
+    stored = map ? (int64_t)map->size() : c->pacc_n;
     if (c->progress && goal > 0) c->progress(caustic ? 2 : 1, (double)stored / goal, c->progress_user);
     if (stored > 0 && emitted > 0) {
       rate = (double)stored / emitted;
@@ -1402,6 +1509,9 @@ int gi_create(gi_ctx **out, int dev) {
   // tuning knobs (measurement only; defaults are the measured best)
   if (const char *s = getenv("GI_LEAF_SIZE")) c->leaf_size[0] = c->leaf_size[1] = std::max(1, atoi(s));
   if (const char *s = getenv("GI_KD_BUILD")) c->gpu_kd = strcmp(s, "host") != 0;
+  if (const char *s = getenv("GI_PHOTON_2PASS")) c->photon_2pass = atoi(s) != 0;
+  if (const char *s = getenv("GI_PHOTON_RATE0"))  // test knob: first launch's slots per photon
+    c->prate[0] = c->prate[1] = std::max(0.0, atof(s));
   if (const char *s = getenv("GI_CHUNK_MINSUB_BIG")) c->chunk_minsub_big = std::min(64, std::max(1, atoi(s)));
   if (const char *s = getenv("GI_CHUNK_MINSUB")) c->chunk_minsub = std::min(64, std::max(1, atoi(s)));
   if (const char *s = getenv("GI_SPLIT_IND")) c->split_ind = atoi(s) != 0;
@@ -1464,7 +1574,7 @@ void gi_destroy(gi_ctx *c) {
   DBuf *bufs[] = {&c->d_nodes, &c->d_elems, &c->d_shapes, &c->d_tris, &c->d_bvh, &c->d_mats, &c->d_lights,
                   &c->d_lut, &c->d_stats, &c->spawn, &c->npaths, &c->path_off, &c->base,
                   &c->pixels, &c->rgbf, &c->rgb8, &c->qcount,
-                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->ind_cont, &c->ind_ncont, &c->mc_cont, &c->mc_ncont, &c->mc_cont2, &c->mc_ncont2, &c->prim_rgb, &c->ind_tab, &c->mc_tab, &c->ind_trows, &c->ind_rows, &c->ind_masks};
+                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->pkeys, &c->pcursor, &c->ptmp, &c->pacc, &c->pglob, &c->ind_cont, &c->ind_ncont, &c->mc_cont, &c->mc_ncont, &c->mc_cont2, &c->mc_ncont2, &c->prim_rgb, &c->ind_tab, &c->mc_tab, &c->ind_trows, &c->ind_rows, &c->ind_masks};
   for (DBuf *b : bufs) b->release();
   c->pack.release();
   for (auto &b : c->recv) b.release();
@@ -1484,6 +1594,7 @@ void gi_destroy(gi_ctx *c) {
     c->qpos[l].release(); c->qshade[l].release(); c->qkey[l].release(); c->qout[l].release();
     sort_scratch_release(c->keysort[l]);
   }
+  sort_scratch_release(c->psort);
   for (int l = 0; l < 8; l++) { c->scan_lvl[l].release(); c->scan_out[l].release(); }
   for (int m = 0; m < 2; m++) {
     c->dmap[m].pos4.release();
@@ -1564,46 +1675,71 @@ int gi_map_photons(gi_ctx *c, gi_photon_stats *st) {
     total += powers[i];
   }
   if (total <= 0) return GI_OK;
+  // one device: the maps grow on the device across the emission rounds (pacc; the global map is
+  // then held in pglob while the caustic map is traced); device sets: on the host
+  const bool on_dev = c->peers.empty();
   std::vector<gi_photon> gph, cph;
+  int64_t gn = 0, cn = 0;
   if (P.indirect_illum || P.direct_photon_illum) {
-    rc = trace_map(c, 0, P.global_photon_count, powers, total, gph, gem);
+    rc = trace_map(c, 0, P.global_photon_count, powers, total, on_dev ? nullptr : &gph, gem);
     if (rc) return rc;
+    gn = on_dev ? c->pacc_n : (int64_t)gph.size();
+    if (on_dev) std::swap(c->pglob, c->pacc);
   }
   if (P.caustic_illum) {
-    rc = trace_map(c, 1, P.caustic_photon_count, powers, total, cph, cem);
+    rc = trace_map(c, 1, P.caustic_photon_count, powers, total, on_dev ? nullptr : &cph, cem);
     if (rc) return rc;
+    cn = on_dev ? c->pacc_n : (int64_t)cph.size();
   }
   auto t1 = std::chrono::steady_clock::now();
-  // power rescale (Q9), photonmap.cpp:339-361
-  auto rescale = [&](std::vector<gi_photon> &v, int64_t emitted) {
+  // power rescale (Q9), photonmap.cpp:339-361: RGBE -> colour * total / emitted -> RGBE
+  auto rescale = [&](std::vector<gi_photon> &v, DBuf &dv, int64_t n, int64_t emitted) -> int {
     double pp = total / (double)emitted;
+    if (on_dev) {
+      launch_photon_rescale(dv.as<gi_photon_dev>(), n, pp, c->stream);
+      HIPCHK(c, hipGetLastError());
+      return GI_OK;
+    }
     for (auto &p : v) {
       double col[3];
       rgbe_dec(p.rgbe, col);
       for (int i = 0; i < 3; i++) col[i] *= pp;
       rgbe_enc(col, p.rgbe);
     }
+    return GI_OK;
   };
-  if ((P.indirect_illum || P.direct_photon_illum) && !gph.empty()) {
-    P.global_photon_count = (int)gph.size();
-    rescale(gph, gem);
+  if ((P.indirect_illum || P.direct_photon_illum) && gn > 0) {
+    P.global_photon_count = (int)gn;
+    if ((rc = rescale(gph, c->pglob, gn, gem))) return rc;
   } else if (P.indirect_illum || P.direct_photon_illum) {
     P.indirect_illum = 0;
     P.direct_photon_illum = 0;
   }
-  if (P.caustic_illum && !cph.empty()) {
-    P.caustic_photon_count = (int)cph.size();
-    rescale(cph, cem);
+  if (P.caustic_illum && cn > 0) {
+    P.caustic_photon_count = (int)cn;
+    if ((rc = rescale(cph, c->pacc, cn, cem))) return rc;
   } else if (P.caustic_illum) {
     P.caustic_illum = 0;
   }
-  rc = set_map(c, GI_MAP_GLOBAL, gph.data(), (int64_t)gph.size());
-  if (rc) return rc;
-  rc = set_map(c, GI_MAP_CAUSTIC, cph.data(), (int64_t)cph.size());
-  if (rc) return rc;
+  if (on_dev) {
+    rc = set_map_device(c, GI_MAP_GLOBAL, c->pglob, gn);
+    if (rc) return rc;
+    rc = set_map_device(c, GI_MAP_CAUSTIC, c->pacc, cn);
+    if (rc) return rc;
+    // tracing scratch is not needed by the render
+    DBuf *rel[] = {&c->pbuf, &c->pkeys, &c->ptmp, &c->pacc, &c->pglob};
+    for (DBuf *b : rel) b->release();
+    sort_scratch_release(c->psort);
+    c->pacc_n = 0;
+  } else {
+    rc = set_map(c, GI_MAP_GLOBAL, gph.data(), (int64_t)gph.size());
+    if (rc) return rc;
+    rc = set_map(c, GI_MAP_CAUSTIC, cph.data(), (int64_t)cph.size());
+    if (rc) return rc;
+  }
   auto t2 = std::chrono::steady_clock::now();
   // irradiance cache, photonmap.cpp:381-413: irradiance = own power + EstimateIrradiance
-  if (P.irradiance_cache && (P.indirect_illum || P.direct_photon_illum) && !gph.empty()) {
+  if (P.irradiance_cache && (P.indirect_illum || P.direct_photon_illum) && gn > 0) {
     HostMap &H = c->hmap[GI_MAP_GLOBAL];
     int64_t n = (int64_t)H.storage.size();
     std::vector<float> q(4 * n);

@@ -313,10 +313,15 @@ struct PhotonArgs {
   int32_t caustic;
   int64_t e0;     // first emission index
   int64_t n;      // photons in this launch
-  uint32_t *counts;
-  const uint32_t *offsets;
+  uint32_t *counts;        // PM_COUNT: photons each emitted photon stores
+  const uint32_t *offsets; // PM_EMIT: their exclusive scan
   gi_photon_dev *out;
+  uint32_t *cursor;        // PM_APPEND: slot counter (one atomic per wave per bounce)
+  uint64_t *keys;          // PM_APPEND: (emission index << obits) | store ordinal per slot
+  uint32_t cap;            // PM_APPEND: slots in out / keys
+  int32_t obits;           // PM_APPEND: bits of the store ordinal (max_photon_depth)
 };
+enum { PM_COUNT = 0, PM_EMIT = 1, PM_APPEND = 2 };
 
 struct ScanTemp {
   uint32_t *level[8];
@@ -357,7 +362,10 @@ bool launch_knn_chunk_big(const KnnArgs &a, int cap, hipStream_t st);  // K > 64
 unsigned knn_chunk_grid(int64_t nq);
 void launch_list_estimate(const KnnArgs &a, hipStream_t st);
 void launch_cached(const KnnArgs &a, hipStream_t st);
-void launch_photons(const PhotonArgs &a, bool emit, hipStream_t st);
+void launch_photons(const PhotonArgs &a, int mode, hipStream_t st);
+void launch_photon_gather(const gi_photon_dev *src, const uint32_t *slot, int64_t n,
+                          gi_photon_dev *dst, hipStream_t st);
+void launch_photon_rescale(gi_photon_dev *ph, int64_t n, double pp, hipStream_t st);
 void launch_intersect(const SceneView &S, int64_t n, const double *org, const double *dir,
                       int32_t *hit, double *t, double *point, double *normal, int32_t *mat,
                       hipStream_t st);

@@ -1440,13 +1440,22 @@ __device__ __forceinline__ uint32_t rgbe_encode(C3 c) {
 
 struct PhotonOut {
   gi_photon_dev *out;
-  uint32_t off;
-  uint32_t count;
+  uint32_t off;     // PM_EMIT: this photon's first slot (scan of the PM_COUNT pass)
+  uint32_t count;   // photons stored so far by this emitted photon (its store ordinal)
+  // PM_APPEND
+  uint32_t *cursor;
+  uint64_t *keys;
+  uint32_t cap;
+  uint32_t obits;
+  uint64_t j;       // emission index within the launch
 };
 
-// StorePhoton, photon_utils.cpp:40-65
-__device__ __forceinline__ void store_photon(bool emit, PhotonOut &o, C3 power, V inc, V p) {
-  if (emit) {
+// StorePhoton, photon_utils.cpp:40-65. PM_COUNT only counts; PM_EMIT writes at the slot the
+// scan of the count pass gave; PM_APPEND takes a slot from one atomic per wave (ballot of the
+// lanes storing at this bounce, prefix by popcount) and records the (emission index, store
+// ordinal) key that restores emission order afterwards (photon_sort).
+__device__ __forceinline__ void store_photon(int mode, PhotonOut &o, C3 power, V inc, V p) {
+  if (mode != PM_COUNT) {
     gi_photon_dev ph;
     ph.pos[0] = (float)p.x;
     ph.pos[1] = (float)p.y;
@@ -1457,14 +1466,29 @@ __device__ __forceinline__ void store_photon(bool emit, PhotonOut &o, C3 power, 
     int theta = (uint8_t)(255.0 * acos(z) / kPi);
     ph.dir = (uint16_t)(phi * 256 + theta);
     ph.flags = 0;
-    o.out[o.off + o.count] = ph;
+    if (mode == PM_EMIT) {
+      o.out[o.off + o.count] = ph;
+    } else {
+      uint64_t act = __ballot(1);
+      int lane = (int)(threadIdx.x & 63);
+      int leader = __ffsll((long long)act) - 1;
+      uint32_t rank = (uint32_t)__popcll(act & ((1ull << lane) - 1ull));
+      uint32_t base = 0;
+      if (lane == leader) base = atomicAdd(o.cursor, (uint32_t)__popcll(act));
+      base = (uint32_t)__shfl((int)base, leader, 64);
+      uint32_t slot = base + rank;
+      if (slot < o.cap) {   // an overflowing launch is re-run with room (trace_batch_dev)
+        o.out[slot] = ph;
+        o.keys[slot] = (o.j << o.obits) | (uint64_t)o.count;
+      }
+    }
   }
   o.count++;
 }
 
 // PhotonTrace, photontracer.cpp:28-176
 __device__ __noinline__ void photon_trace(const SceneView &S, const Flags &F, V org, V dir,
-                                          C3 photon, bool caustic, Rng &rng, bool emit,
+                                          C3 photon, bool caustic, Rng &rng, int mode,
                                           PhotonOut &o) {
   bool store = (!caustic && !F.fast_global);
   V ray_start = org;
@@ -1476,7 +1500,7 @@ __device__ __noinline__ void photon_trace(const SceneView &S, const Flags &F, V 
     const DMaterial &m = S.mats[h.mat];
     V view = normalize(h.p - ray_start);
     double ct = dot(h.n, -view);
-    if ((m.flags & MF_DIFFUSE) && store) store_photon(emit, o, photon, view, h.p);
+    if ((m.flags & MF_DIFFUSE) && store) store_photon(mode, o, photon, view, h.p);
     double R = 0;
     if (F.fresnel && (m.flags & MF_TRANSPARENT)) R = reflection_coeff(F.ir_air, ct, m.ir);
     double mc = maxch(photon);
@@ -1513,7 +1537,7 @@ __device__ __noinline__ void photon_trace(const SceneView &S, const Flags &F, V 
 }
 
 // EmitPhotons, photontracer.cpp:182-373, one photon per lane (emission index e0 + lane)
-template <bool EMIT>
+template <int MODE>
 __global__ __launch_bounds__(128) void photon_kernel(PhotonArgs a) {
   int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= a.n) return;
@@ -1574,10 +1598,40 @@ __global__ __launch_bounds__(128) void photon_kernel(PhotonArgs a) {
   }
   PhotonOut o;
   o.out = a.out;
-  o.off = EMIT ? a.offsets[j] : 0u;
+  o.off = MODE == PM_EMIT ? a.offsets[j] : 0u;
   o.count = 0;
-  photon_trace(S, F, org, dir, photon, a.caustic != 0, rng, EMIT, o);
-  if (!EMIT) a.counts[j] = o.count;
+  o.cursor = a.cursor;
+  o.keys = a.keys;
+  o.cap = a.cap;
+  o.obits = (uint32_t)a.obits;
+  o.j = (uint64_t)j;
+  photon_trace(S, F, org, dir, photon, a.caustic != 0, rng, MODE, o);
+  if (MODE == PM_COUNT) a.counts[j] = o.count;
+}
+
+// the appended photons in (emission index, store ordinal) order: dst[i] = src[slot[i]]
+__global__ __launch_bounds__(256) void photon_gather_kernel(const gi_photon_dev *src,
+                                                            const uint32_t *slot, int64_t n,
+                                                            gi_photon_dev *dst) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[slot[i]];
+}
+
+// power rescale (Q9, photonmap.cpp:339-361) of a device map: RGBE -> RNRgb, * pp, -> RGBE
+__global__ __launch_bounds__(256) void photon_rescale_kernel(gi_photon_dev *ph, int64_t n,
+                                                             double pp) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t v = ph[i].rgbe;
+  uint32_t e = v >> 24;
+  C3 c = rgb(0.0, 0.0, 0.0);
+  if (e) {
+    double inv = ldexp(1.0, (int)e - 128 - 8);   // RGBE_to_RNRgb, graphics_utils.cpp:64-77
+    c = rgb((double)(v & 255u) * inv, (double)((v >> 8) & 255u) * inv,
+            (double)((v >> 16) & 255u) * inv);
+  }
+  c = c * pp;
+  ph[i].rgbe = rgbe_encode(c);
 }
 
 // directional-light disk basis needs the scene radius: computed on host (gi_host.cpp)
@@ -1784,10 +1838,18 @@ void launch_cached(const KnnArgs &a, hipStream_t st) {
   if (a.nq == 0) return;
   cached_kernel<<<nblk(a.nq, 64), 64, 0, st>>>(a);
 }
-void launch_photons(const PhotonArgs &a, bool emit, hipStream_t st) {
+void launch_photons(const PhotonArgs &a, int mode, hipStream_t st) {
   if (a.n == 0) return;
-  if (emit) photon_kernel<true><<<nblk(a.n, 128), 128, 0, st>>>(a);
-  else photon_kernel<false><<<nblk(a.n, 128), 128, 0, st>>>(a);
+  if (mode == PM_EMIT) photon_kernel<PM_EMIT><<<nblk(a.n, 128), 128, 0, st>>>(a);
+  else if (mode == PM_COUNT) photon_kernel<PM_COUNT><<<nblk(a.n, 128), 128, 0, st>>>(a);
+  else photon_kernel<PM_APPEND><<<nblk(a.n, 128), 128, 0, st>>>(a);
+}
+void launch_photon_gather(const gi_photon_dev *src, const uint32_t *slot, int64_t n,
+                          gi_photon_dev *dst, hipStream_t st) {
+  if (n > 0) photon_gather_kernel<<<nblk(n, 256), 256, 0, st>>>(src, slot, n, dst);
+}
+void launch_photon_rescale(gi_photon_dev *ph, int64_t n, double pp, hipStream_t st) {
+  if (n > 0) photon_rescale_kernel<<<nblk(n, 256), 256, 0, st>>>(ph, n, pp);
 }
 void launch_intersect(const SceneView &S, int64_t n, const double *org, const double *dir,
                       int32_t *hit, double *t, double *point, double *normal, int32_t *mat,

@@ -29,7 +29,9 @@ namespace oracle {
 // the material of their first specular / transmissive bounce (+2; the default material -1 -> 1,
 // no such bounce -> 0), and with g_tag_select = m the caustic estimate sums only the photons of
 // material m over the SAME K-set and radius as the full map, so the per-material layers add up
-// to the caustic layer exactly (before clamping and quantisation).
+// to the caustic layer exactly (before clamping and quantisation); g_tag_select = 100 + b selects
+// the photons whose incidence cosine |N.I| lies in [b/5, (b+1)/5) instead, 200 + b those whose
+// emission direction's cosine to the light normal does, 300 + c the path class c (photon_trace).
 static bool g_tagging = false;
 static int g_tag_select = -100;   // -100: every photon
 
@@ -668,7 +670,19 @@ static void estimate_radiance(const Ctx &c, V3 p, V3 normal, Rgb &color, const B
     V3 inc(c.lut[3 * d], c.lut[3 * d + 1], c.lut[3 * d + 2]);
     double perp = dot(normal, inc);
     if ((cos_theta < 0 && perp < 0) || (cos_theta > 0 && perp > 0)) continue;
-    if (g_tag_select != -100 && &map == &c.cmap && ph.flags != g_tag_select + 2) continue;
+    if (g_tag_select != -100 && &map == &c.cmap) {
+      // >= 100: incidence-angle bins instead of materials, |N.I| in [(s-100)/5, (s-99)/5)
+      if (g_tag_select >= 300) {          // path class (300 + c)
+        if ((ph.flags >> 12) != g_tag_select - 300) continue;
+      } else if (g_tag_select >= 200) {   // emission-cosine bin (200 + b)
+        if (((ph.flags >> 8) & 15) != g_tag_select - 200) continue;
+      } else if (g_tag_select >= 100) {   // incidence-cosine bin at the query (100 + b)
+        int b = std::min(4, (int)(fabs(perp) * 5.0));
+        if (b != g_tag_select - 100) continue;
+      } else if ((ph.flags & 255) != g_tag_select + 2) {
+        continue;
+      }
+    }
     Rgb pc = rgbe_to_rgb(ph.rgbe);
     double ca = dot(exact, -inc);
     if (ca < 0) ca = 0;
@@ -1014,10 +1028,12 @@ static void store_photon(const Rgb &power, V3 inc, V3 p, std::vector<Photon> &ou
 
 // PhotonTrace, photontracer.cpp:28-176
 static void photon_trace(const Ctx &c, V3 org, V3 dir, Rgb photon, bool caustic, Rng &rng,
-                         std::vector<Photon> &out) {
+                         std::vector<Photon> &out, int emit_bin = 0) {
   const gi_params &P = c.P;
   bool store = (!caustic && !P.fast_global);
-  int tag = 0;   // diagnostic: material of the first specular / transmissive bounce, + 2
+  int tag = emit_bin << 8;   // diagnostic: emission bin | material of the first specular bounce + 2
+  int nT = 0, nS = 0;        // diagnostic: transmissions / reflections so far
+  bool first_s_transparent = false;
   V3 ray_start = org;
   for (int iter = 0; iter < P.max_photon_depth; iter++) {
     Hit h;
@@ -1025,7 +1041,17 @@ static void photon_trace(const Ctx &c, V3 org, V3 dir, Rgb photon, bool caustic,
     const Brdf &brdf = brdf_of(c, h.material);
     V3 view = normalize(h.point - ray_start);
     double cos_theta = dot(h.normal, -view);
-    if (brdf.isDiffuse() && store) store_photon(photon, view, h.point, out, tag);
+    if (brdf.isDiffuse() && store) {
+      // diagnostic path class of the stored photon (bits 12-15): 1 in-out transmission (T2),
+      // 2 one mirror reflection, 3 one reflection off a transparent surface (Fresnel), 4 T2 with
+      // reflections inside, 5 reflections only (>= 2), 6 anything else
+      int cls = 6;
+      if (nT == 2 && nS == 0) cls = 1;
+      else if (nT == 0 && nS == 1) cls = first_s_transparent ? 3 : 2;
+      else if (nT == 2 && nS >= 1) cls = 4;
+      else if (nT == 0 && nS >= 2) cls = 5;
+      store_photon(photon, view, h.point, out, tag | (cls << 12));
+    }
     double R = 0;
     if (P.fresnel && brdf.isTransparent()) R = reflection_coeff(P.ir_air, cos_theta, brdf.ir);
     double mc = max_channel(photon);
@@ -1044,13 +1070,15 @@ static void photon_trace(const Ctx &c, V3 org, V3 dir, Rgb photon, bool caustic,
       photon *= brdf.kd / pd;
     } else if (rnd < pd + pt) {
       if (caustic) store = true;
-      if (!tag) tag = h.material + 2;
+      if (!(tag & 255)) tag |= h.material + 2;
+      nT++;
       V3 ex = transmissive_bounce(P.ir_air, h.normal, view, cos_theta, brdf.ir);
       sb = P.distrib_transmissive ? specular_sample(ex, brdf.n, cos_theta, rng) : ex;
       photon *= (1.0 - R) * brdf.kt / pt;
     } else if (rnd < pd + pt + ps) {
       if (caustic) store = true;
-      if (!tag) tag = h.material + 2;
+      if (!(tag & 255)) tag |= h.material + 2;
+      if (nS++ == 0 && nT == 0) first_s_transparent = brdf.isTransparent();
       V3 ex = reflective_bounce(h.normal, view, cos_theta);
       sb = P.distrib_specular ? specular_sample(ex, brdf.n, cos_theta, rng) : ex;
       photon *= (brdf.ks + R * brdf.kt) / ps;
@@ -1120,7 +1148,10 @@ static void emit_one(const Ctx &c, const Light &L, bool caustic, Rng &rng,
     org = ((r1 * a1 + r2 * a2) + L.pos) + ln * EPS;
     dir = diffuse_sample(ln, 1.0, rng);
   }
-  photon_trace(c, org, dir, photon, caustic, rng, out);
+  // diagnostic tag: cosine of the emission direction to the light's normal in five bins
+  int emit_bin = 0;
+  if (g_tagging && L.type != L_POINT) emit_bin = std::min(4, (int)(fabs(dot(dir, L.dir)) * 5.0));
+  photon_trace(c, org, dir, photon, caustic, rng, out, emit_bin);
 }
 
 // LightPower, graphics_utils.cpp:223-258

@@ -313,3 +313,40 @@ def test_device_set_matches_one_device(devices, name, extra):
               "specular_samples", "indirect_samples", "caustic_samples", "knn_queries",
               "knn_photons"):
         assert s1[k] == s2[k], k
+
+
+@pytest.mark.parametrize("name,extra,rate0", [
+    ("stilllife.scn", ["-global", "300000", "-caustic", "300000"], None),
+    ("display.scn", ["-global", "50000", "-caustic", "200000", "-pd", "5"], None),
+    ("jensen.scn", ["-global", "20000", "-caustic", "100000"], "0.0001"),
+])
+def test_single_pass_photon_maps_equal_two_pass(name, extra, rate0, monkeypatch):
+    """Single-pass photon tracing (one atomic per wave per bounce, then a sort on (emission
+    index, store ordinal); gi_host.cpp trace_batch_dev) builds the maps the count pass + scan +
+    re-trace (GI_PHOTON_2PASS=1, r03) built: byte for byte, in the same emission order, with the
+    same emitted counts. Covers several lights and emission rounds (stilllife), a short -pd
+    (few ordinal bits), and launches that overflow their first slot estimate and are re-run
+    (GI_PHOTON_RATE0)."""
+    import gpu_util
+    args = [gpu_util.scene(name), "/tmp/x.png", "-seed", "3"] + extra
+    p, sc, *_ = gi_amd.ParseArgs(args)
+    out = []
+    for env in ({"GI_PHOTON_2PASS": "1"}, {"GI_PHOTON_2PASS": "0"}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        if rate0 and env["GI_PHOTON_2PASS"] == "0":
+            monkeypatch.setenv("GI_PHOTON_RATE0", rate0)
+        r = gi_amd.Renderer(0, p)
+        try:
+            r.ReadScene(sc)
+            st = r.MapPhotons()
+            out.append((st, [r.photon_map(m) for m in (gi_amd.GLOBAL, gi_amd.CAUSTIC)]))
+        finally:
+            r.close()
+    (s2, m2), (s1, m1) = out
+    for k in ("global_stored", "caustic_stored", "global_emitted", "caustic_emitted"):
+        assert s1[k] == s2[k], k
+    assert s1["caustic_stored"] > 0
+    for a, b in zip(m1, m2):
+        assert len(a) == len(b)
+        assert a.tobytes() == b.tobytes()

@@ -227,3 +227,54 @@ def test_c5_settings_match_oracle(renderer):
     assert gp["global_stored"] == ost["global_stored"]
     assert gst["screen_rays"] == ost["screen_rays"] > 0  # primary hits (render.cpp:119-121)
     compare(g, o, 0.99, 0.99, 0.5)
+
+
+def _threads():
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return min(n, int(omp)) if omp.isdigit() and int(omp) > 0 else n
+
+
+C2_MAPS = ["-global", "1000000", "-caustic", "1000000"]
+
+
+def test_c2_config_matches_oracle(renderer):
+    """C2 exactly as bench.py runs it (cornell.scn, aa 2, 1M global + 1M caustic photons, every
+    other flag at the reference default: -it 256, -tt/-st 128, K 50 / 225) at an oracle-sized
+    16 x 16 resolution: photon maps of the same size, the same per-sample work."""
+    args = [scene("cornell.scn"), "/tmp/x.png", "-resolution", "16", "16", "-aa", "2",
+            "-seed", "1", "-threads", str(_threads())] + C2_MAPS
+    g, gst, gp = run_gpu(renderer, args)
+    o, ost = oracle_lib.render(args, 16, 16)
+    assert gp["global_stored"] == ost["global_stored"] >= 1000000
+    assert gp["caustic_stored"] == ost["caustic_stored"] >= 1000000
+    assert gst["screen_rays"] == ost["screen_rays"]
+    assert abs(gst["knn_queries"] - ost["knn_queries"]) <= 0.001 * ost["knn_queries"]
+    compare(g, o, 0.99, 0.995, 0.5)
+
+
+def test_c2_full_frame_properties():
+    """The full C2 frame (1024^2, aa 2, 1M + 1M photons): finite and clamped to [0, 1] per pixel
+    (render.cpp:236-249), the same image twice over the resident maps, and the same image from
+    a two-entry device set on one GPU (tiles dealt over the set and gathered, render.cpp:90)."""
+    import hashlib
+    args = [scene("cornell.scn"), "/tmp/x.png", "-resolution", "1024", "1024", "-aa", "2",
+            "-seed", "1"] + C2_MAPS
+    p, sc, _o, w, h, aa, real = gi_amd.ParseArgs(args)
+    hashes = []
+    for devs in (None, [0, 0]):
+        r = gi_amd.Renderer(0, p, devices=devs)
+        try:
+            r.ReadScene(sc, real)
+            ps = r.MapPhotons()
+            assert ps["global_stored"] >= 1000000 and ps["caustic_stored"] >= 1000000
+            runs = 2 if devs is None else 1
+            for _ in range(runs):
+                rgb, f, st = r.RenderImage(aa, w, h, want_float=True)
+                assert rgb.shape == (h, w, 3) and f.shape == (h, w, 3)
+                assert np.isfinite(f).all() and f.min() >= 0.0 and f.max() <= 1.0
+                assert st["screen_rays"] > 0.9 * w * h * 4 ** aa
+                hashes.append(hashlib.sha256(rgb.tobytes()).hexdigest())
+        finally:
+            r.close()
+    assert len(set(hashes)) == 1, hashes

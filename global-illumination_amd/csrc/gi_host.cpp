@@ -299,6 +299,8 @@ struct gi_ctx {
   DBuf mc_cont, mc_ncont;         // Monte Carlo paths' indirect sub-paths
   DBuf mc_cont2, mc_ncont2;       // ... those continuing past a glass / mirror first hit
   bool mc_sub = true;             // sub-paths' first bounce in mc_sub_kernel (GI_MC_SUB=0: all in ind_cont_kernel)
+  int mc_persist = 1024;          // Monte Carlo paths in mc_persist_kernel with this many blocks
+                                  // (GI_MC_PERSIST; 0: mc_kernel, one path per lane)
   DBuf prim_rgb;                  // per-primary sums of the reduction
   DBuf ind_tab, mc_tab;           // row -> tile of the tiled indirect entries; owner of MC path 64k
   DBuf ind_trows, ind_rows;       // indirect paths' tiled slots: rows per tile, their scan
@@ -332,6 +334,7 @@ struct gi_ctx {
   // 2^21 / 2^22 ran 6.85 / 7.44 / 7.89 / 7.69 Mpixel-samples/s. A batch is also capped by the
   // query budget below (queries per primary sample vary ~10x between scenes).
   int64_t prim_per_batch = 1 << 21;
+  int64_t batch_reruns = 0;          // batches re-run smaller for 32-bit path slots (render_pixels)
   int64_t query_budget = 400000000;  // photon-map queries per batch (~120 B each: ~48 GB)
   double q_per_prim = 0.0;           // largest queries per primary sample seen so far
   float sbmin[3] = {0, 0, 0}, sbmax[3] = {1, 1, 1};
@@ -937,9 +940,12 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
       HIPCHK(c, hipMemcpyAsync(&nfb2, dense + nfb, 4, hipMemcpyDeviceToHost, X.st));
       HIPCHK(c, hipStreamSynchronize(X.st));
     }
+    bool dumped = false;
     if (const char *dp = getenv("GI_DUMP_FB"); dp && ran2 && nfb2 > c->dump_fb_max) {
       // diagnostics (tools/caustic_fb_dump.py): the launch with the most fallback queries, as
-      // float4 positions of the final fallback list, then of the second pass's list
+      // float4 positions of the final fallback list, then of the second pass's list. Its copies
+      // and file writes sit between the events, so this launch is left out of the timings.
+      dumped = true;
       c->dump_fb_max = nfb2;
       std::vector<uint32_t> i1(nfb), i2(nfb2);
       HIPCHK(c, hipMemcpy(i1.data(), X.fb_dense.p, (size_t)nfb * 4, hipMemcpyDeviceToHost));
@@ -965,7 +971,7 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
       HIPCHK(c, hipGetLastError());
     }
     HIPCHK(c, hipEventRecord(X.ev1, X.st));
-    if (ms) {
+    if (ms && !dumped) {
       HIPCHK(c, hipEventSynchronize(X.ev1));
       float t = 0, tf = 0, t2 = 0;
       HIPCHK(c, hipEventElapsedTime(&t, X.ev0, X.ev1));
@@ -1191,6 +1197,11 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
   HIPCHK(c, upload(c->pixels, pix_xy.data(), pix_xy.size() * 4, c->stream));
   HIPCHK(c, c->qcount.ensure(16));
   HIPCHK(c, c->stats_bak.ensure(ST_BYTES));
+  // path slots are 32-bit: a batch whose paths (with the indirect tiles' padding) would not fit
+  // is re-run at half the primary samples, as often as needed (slot_limit: GI_SLOT_LIMIT, tests)
+  int64_t shrink = 1;
+  uint64_t slot_limit = 0xFFFFFFF0ull;
+  if (const char *s = getenv("GI_SLOT_LIMIT")) slot_limit = std::max(1ULL, strtoull(s, nullptr, 10));
   for (int64_t p0 = 0, npix = 0; p0 < npix_total; p0 += npix) {
     // batch size: prim_per_batch primary samples, fewer when the query rate seen so far would
     // exceed the query budget (the first batch of a scene starts at 1/8 to measure that rate)
@@ -1199,6 +1210,7 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
       prim_cap = std::min<int64_t>(prim_cap, (int64_t)(c->query_budget / c->q_per_prim));
     else
       prim_cap = std::max<int64_t>(1, prim_cap / 8);
+    prim_cap = std::max<int64_t>(1, prim_cap / shrink);
     const int64_t pix_batch = std::max<int64_t>(1, prim_cap / per_pix);
     npix = std::min(pix_batch, npix_total - p0);
     int64_t nprim = npix * per_pix;
@@ -1232,6 +1244,9 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     a.path_off = c->path_off.as<uint32_t>();
     a.mc_off = c->mc_off.as<uint32_t>();
     a.ind_off = c->ind_off.as<uint32_t>();
+    // counters before the primary kernel, restored if the batch is re-run smaller
+    HIPCHK(c, hipMemcpyAsync(c->stats_bak.p, c->d_stats.p, ST_BYTES, hipMemcpyDeviceToDevice,
+                             c->stream));
     launch_primary(a, c->stream);
     HIPCHK(c, hipGetLastError());
     ScanTemp t = scan_temp(c, nprim);
@@ -1267,8 +1282,17 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
                              c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const uint64_t tind = 64ull * trows;  // tiled entries (>= total_ind)
-    if ((uint64_t)total_paths + tind + (uint64_t)nprim > 0xFFFFFFF0ull)
-      return fail(c, GI_ERR_ALLOC, "batch too large for 32-bit path slots");
+    if ((uint64_t)total_paths + tind + (uint64_t)nprim > slot_limit) {
+      if (npix == 1)
+        return fail(c, GI_ERR_ALLOC, "one output pixel's samples need more than 2^32 path slots");
+      HIPCHK(c, hipMemcpyAsync(c->d_stats.p, c->stats_bak.p, ST_BYTES, hipMemcpyDeviceToDevice,
+                               c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      shrink *= 2;
+      c->batch_reruns++;
+      npix = 0;  // same pixels again, half as many per batch
+      continue;
+    }
     a.ind_rows = c->ind_rows.as<uint32_t>();
     a.ind_g0 = total_paths;
     a.tind = (int64_t)tind;
@@ -1293,6 +1317,10 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
       a.mc_cont = c->mc_cont.as<IndCont>();
       a.mc_ncont = c->mc_ncont.as<uint32_t>();
       a.mc_cap_s = (uint32_t)full;
+      if (c->mc_persist > 0) {  // mc_persist_kernel: path counter in the spare qcount word
+        a.mc_next = c->qcount.as<uint32_t>() + 2;
+        a.mc_persist_blocks = c->mc_persist;
+      }
       if (c->mc_sub) {
         HIPCHK(c, c->mc_cont2.ensure((size_t)IND_QS * full * sizeof(IndCont)));
         HIPCHK(c, c->mc_ncont2.ensure(IND_QS * 32 * 4));
@@ -1518,6 +1546,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_KNN_DK")) c->use_dk = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_DK")) c->chunk_dk = atoi(s) != 0;
   if (const char *s = getenv("GI_MC_SUB")) c->mc_sub = atoi(s) != 0;
+  if (const char *s = getenv("GI_MC_PERSIST")) c->mc_persist = std::max(0, atoi(s));
   if (const char *s = getenv("GI_KNN_LOG")) c->knn_log = atoi(s) != 0;
   if (const char *s = getenv("GI_ELEM_PRETEST")) c->elem_pretest = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_FB_ALL")) c->chunk_fb_all = atoi(s) != 0;
@@ -2061,11 +2090,24 @@ int gi_render_tiles(gi_ctx *c, int aa, int w, int h, int tile, int shard, int ns
 
 // One rank's shard, left on the device and packed (torchrun: each rank gathers these buffers to
 // rank 0 over RCCL and rank 0 composes them with gi_compose_tiles; nothing else crosses).
+// the calling thread's current HIP device, restored on scope exit (the packed entry points run
+// inside processes whose torch shares that device setting)
+struct DeviceScope {
+  int prev = -1;
+  explicit DeviceScope(int d) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    hipSetDevice(d);
+  }
+  ~DeviceScope() {
+    if (prev >= 0) hipSetDevice(prev);
+  }
+};
+
 int gi_render_tiles_packed(gi_ctx *c, int aa, int w, int h, int tile, int shard, int nshards,
                            void *packed, int64_t cap, int64_t *npix, gi_render_stats *st) {
   if (!c || !npix || tile <= 0 || nshards <= 0 || shard < 0 || shard >= nshards || w <= 0 || h <= 0)
     return GI_ERR_ARG;
-  hipSetDevice(c->device);
+  DeviceScope dev(c->device);
   std::vector<int32_t> pix = shard_pixels(w, h, tile, shard, nshards);
   const int64_t n = (int64_t)pix.size() / 2;
   *npix = n;
@@ -2084,7 +2126,7 @@ int gi_render_tiles_packed(gi_ctx *c, int aa, int w, int h, int tile, int shard,
 int gi_compose_tiles(gi_ctx *c, int w, int h, int tile, int nshards, const void *packed,
                      int64_t stride, uint8_t *rgb8, float *rgbf) {
   if (!c || !packed || tile <= 0 || nshards <= 0 || w <= 0 || h <= 0) return GI_ERR_ARG;
-  hipSetDevice(c->device);
+  DeviceScope dev(c->device);
   const size_t npx = (size_t)w * h * 3;
   HIPCHK(c, c->rgbf.ensure(npx * 4));
   HIPCHK(c, c->rgb8.ensure(npx));

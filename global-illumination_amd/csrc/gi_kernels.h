@@ -104,6 +104,8 @@ struct RenderArgs {
   IndCont *mc_cont;     // Monte Carlo paths' indirect sub-paths, striped the same way
   uint32_t *mc_ncont;
   uint32_t mc_cap_s;
+  uint32_t *mc_next;    // mc_persist_kernel's path counter (null: mc_kernel, one path per lane)
+  int32_t mc_persist_blocks;  // its grid
   IndCont *mc_cont2;    // ... those whose first bounce hit glass / a mirror (mc_sub_kernel),
   uint32_t *mc_ncont2;  // at that hit, same stripes and capacity
   // Indirect paths' slots, tiled: primaries b in tiles of 64 (T = b / 64); tile T holds

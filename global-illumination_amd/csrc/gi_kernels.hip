@@ -217,6 +217,8 @@ struct PathCtx {
   Counts cnt;
   int64_t fixed[2]; // deterministic query slot per list (>= 0), -1 append, -2 used
   int hint;         // triangle the path's current ray leaves from (ray_mesh_bvh), -1 none
+  uint32_t qstripe; // mc_cont stripe of the path's deferred sub-path (gi_host.cpp sizes a stripe
+                    // for the paths of every IND_QS-th group of 64)
 };
 
 // the indirect paths' tiled global-list slots carry no key: the reduction reads their row
@@ -350,110 +352,150 @@ __device__ __noinline__ void mc_indirect(PathCtx &P, V org, V dir, Rng &rng, C3 
   mc_indirect_body<KINDS>(P, org, dir, rng, W);
 }
 
-// MonteCarlo_PathTrace, montecarlo.cpp:16-171 (DEFER: indirect sub-paths go to the mc_cont queue)
+// MonteCarlo_PathTrace's loop state (montecarlo.cpp:16-171): the current ray, the loop's
+// ray_start, the throughput, the path's outer weight and RNG stream, the iteration count
+struct McLoop {
+  V org, dir, ray_start;
+  C3 tw, W;
+  Rng rng;
+  int iter;
+};
+
+__device__ __forceinline__ void mc_begin(McLoop &L, V org, V dir, const Rng &rng, C3 W) {
+  L.org = org;
+  L.dir = dir;
+  L.ray_start = org;
+  L.tw = rgb(1, 1, 1);
+  L.W = W;
+  L.rng = rng;
+  L.iter = 0;
+}
+
+// One iteration of MonteCarlo_PathTrace's loop (DEFER: indirect sub-paths go to the mc_cont
+// queue). Returns false when the path has ended.
 template <uint32_t KINDS = KINDS_ALL, bool DEFER = false, bool HARD = false>
-__device__ __forceinline__ void mc_path(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
+__device__ __forceinline__ bool mc_step(PathCtx &P, McLoop &L) {
   const SceneView &S = *P.S;
   const Flags &F = *P.F;
-  if (!F.monte_carlo) return;
-  C3 tw = rgb(1, 1, 1);
-  V ray_start = org;
-  for (int iter = 0; iter < F.max_monte_depth; iter++) {
-    Hit h;
-    if (!scene_intersect<KINDS>(S, org, dir, h, P.hint)) {
-      P.base += W * (tw * ldc(S.background));
-      break;
-    }
-    P.cnt.monte++;
-    P.hint = h.tri;
-    const DMaterial &m = S.mats[h.mat];
-    C3 cb = rgb(0, 0, 0);
-    if (F.ambient) cb += ldc(S.ambient);
-    V view = normalize(h.p - ray_start);
-    double ct = dot(h.n, -view);
-    if (m.flags & (MF_DIFFUSE | MF_SPECULAR)) {
-      if (HARD) direct_illumination_hard<KINDS>(S, F, h.p, h.n, ray_start, cb, m, ct, true, P.cnt);
-      else direct_illumination<KINDS>(S, F, h.p, h.n, ray_start, cb, m, ct, true, rng, P.cnt);
-    }
-    if (F.caustic && (m.flags & MF_DIFFUSE)) {
-      V ex = reflective_bounce(h.n, view, ct);
-      put_query(P, 1, h.p, h.n, ex, ct, h.mat, W * tw);
-      P.cnt.caustic++;
-    }
-    P.base += W * (cb * tw);
-    double R = 0;
-    if (F.specular && F.transmissive && F.fresnel && (m.flags & MF_TRANSPARENT))
-      R = reflection_coeff_nc(F.ir_air, ct, m.ir);
-    double pd = m.max_kd, pt = m.max_kt;
-    double ps = m.max_ks + R * pt;
-    pt *= (1.0 - R);
-    double pterm = m.max_e + F.prob_absorb;
-    double ptot = pd + pt + ps + pterm;
-    double rnd = rng.next();
-    if (ptot > 1.0) rnd *= ptot;
-    V sb;
-    if (rnd < pd) {
-      C3 kd = ldc(m.kd);
-      if (F.indirect) {
-        // IndirectIllumination(inMC): one sample continuing this path's stream. Queued (the
-        // path ends here, so its trace is this path's last work and its background term the
-        // last addition to the path's sum) and traced compacted in ind_cont_kernel.
-        V s2 = diffuse_sample_call(h.n, ct, rng);
-        C3 w2 = W * ((kd * kd * tw) / pd);
-        if (DEFER) {
-          V o2 = h.p + s2 * kEps;
-          uint64_t act = __ballot(1);
-          int lane = (int)(threadIdx.x & 63);
-          int leader = __ffsll((long long)act) - 1;
-          const uint32_t stripe = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) & (IND_QS - 1);
-          uint32_t qb = 0;
-          if (lane == leader) qb = atomicAdd(&P.A->mc_ncont[stripe * 32], (uint32_t)__popcll(act));
-          qb = (uint32_t)__shfl((int)qb, leader, 64);
-          IndCont &q = P.A->mc_cont[(size_t)stripe * P.A->mc_cap_s + qb +
-                                    (uint32_t)__popcll(act & ((1ull << lane) - 1ull))];
-          q.org[0] = o2.x; q.org[1] = o2.y; q.org[2] = o2.z;
-          q.hp[0] = s2.x; q.hp[1] = s2.y; q.hp[2] = s2.z;
-          q.w[0] = w2.r; q.w[1] = w2.g; q.w[2] = w2.b;
-          q.rkey = rng.key;
-          q.rctr = rng.ctr;
-          q.g = (uint32_t)P.g;
-          q.prim = P.prim;
-          q.pslot = P.pslot;
-          q.qslot = P.fixed[0] >= 0 ? (uint32_t)P.fixed[0] : 0xffffffffu;
-          q.mat = -1;
-          q.j = P.j;
-          q.tri = h.tri;
-          q.sub = 0;
-          P.fixed[0] = -2;  // the sub-path owns the global slot now
-        } else {
-          mc_indirect<KINDS>(P, h.p + s2 * kEps, s2, rng, w2);
-        }
-        P.cnt.indirect++;
-      } else if (F.fast_global) {
-        V ex = reflective_bounce(h.n, view, ct);
-        global_query(P, h.p, h.n, ex, ct, h.mat, W * (kd * tw / pd));
-        if (!F.cache) P.cnt.indirect++;
-      }
-      break;
-    } else if (rnd < pd + pt) {
-      if (!F.transmissive) break;
-      V ex = transmissive_bounce_nc(F.ir_air, h.n, view, ct, m.ir);
-      sb = F.distrib_trans ? specular_sample_call(ex, m.n, ct, rng) : ex;
-      P.cnt.trans++;
-      tw *= (1.0 - R) * ldc(m.kt) / pt;
-    } else if (rnd < pd + pt + ps) {
-      if (!F.specular) break;
-      V ex = reflective_bounce(h.n, view, ct);
-      sb = F.distrib_spec ? specular_sample_call(ex, m.n, ct, rng) : ex;
-      P.cnt.spec++;
-      tw *= (ldc(m.ks) + R * ldc(m.kt)) / ps;
-    } else {
-      break;
-    }
-    ray_start = h.p + sb * kEps;
-    org = ray_start;
-    dir = sb;
+  if (L.iter >= F.max_monte_depth) return false;
+  L.iter++;
+  const C3 W = L.W;
+  Rng &rng = L.rng;
+  C3 &tw = L.tw;
+  Hit h;
+  if (!scene_intersect<KINDS>(S, L.org, L.dir, h, P.hint)) {
+    P.base += W * (tw * ldc(S.background));
+    return false;
   }
+  P.cnt.monte++;
+  P.hint = h.tri;
+  const DMaterial &m = S.mats[h.mat];
+  C3 cb = rgb(0, 0, 0);
+  if (F.ambient) cb += ldc(S.ambient);
+  V view = normalize(h.p - L.ray_start);
+  double ct = dot(h.n, -view);
+  if (m.flags & (MF_DIFFUSE | MF_SPECULAR)) {
+    if (HARD) direct_illumination_hard<KINDS>(S, F, h.p, h.n, L.ray_start, cb, m, ct, true, P.cnt);
+    else direct_illumination<KINDS>(S, F, h.p, h.n, L.ray_start, cb, m, ct, true, rng, P.cnt);
+  }
+  if (F.caustic && (m.flags & MF_DIFFUSE)) {
+    V ex = reflective_bounce(h.n, view, ct);
+    put_query(P, 1, h.p, h.n, ex, ct, h.mat, W * tw);
+    P.cnt.caustic++;
+  }
+  P.base += W * (cb * tw);
+  double R = 0;
+  if (F.specular && F.transmissive && F.fresnel && (m.flags & MF_TRANSPARENT))
+    R = reflection_coeff_nc(F.ir_air, ct, m.ir);
+  double pd = m.max_kd, pt = m.max_kt;
+  double ps = m.max_ks + R * pt;
+  pt *= (1.0 - R);
+  double pterm = m.max_e + F.prob_absorb;
+  double ptot = pd + pt + ps + pterm;
+  double rnd = rng.next();
+  if (ptot > 1.0) rnd *= ptot;
+  V sb;
+  if (rnd < pd) {
+    C3 kd = ldc(m.kd);
+    if (F.indirect) {
+      // IndirectIllumination(inMC): one sample continuing this path's stream. Queued (the
+      // path ends here, so its trace is this path's last work and its background term the
+      // last addition to the path's sum) and traced compacted in ind_cont_kernel.
+      V s2 = diffuse_sample_call(h.n, ct, rng);
+      C3 w2 = W * ((kd * kd * tw) / pd);
+      if (DEFER) {
+        V o2 = h.p + s2 * kEps;
+        // one atomic per stripe present among the appending lanes (one in mc_kernel, where the
+        // stripe is the wave's; a few in mc_persist_kernel, where it is the path's)
+        int lane = (int)(threadIdx.x & 63);
+        const uint32_t stripe = P.qstripe;
+        uint64_t pend = __ballot(1);
+        uint32_t qslot = 0;
+        while (pend) {
+          int leader = __ffsll((long long)pend) - 1;
+          uint32_t sl = (uint32_t)__shfl((int)stripe, leader, 64);
+          uint64_t grp = __ballot(stripe == sl);
+          uint32_t qb = 0;
+          if (lane == leader) qb = atomicAdd(&P.A->mc_ncont[sl * 32], (uint32_t)__popcll(grp));
+          qb = (uint32_t)__shfl((int)qb, leader, 64);
+          if (stripe == sl) qslot = qb + (uint32_t)__popcll(grp & ((1ull << lane) - 1ull));
+          pend &= ~grp;
+        }
+        IndCont &q = P.A->mc_cont[(size_t)stripe * P.A->mc_cap_s + qslot];
+        q.org[0] = o2.x; q.org[1] = o2.y; q.org[2] = o2.z;
+        q.hp[0] = s2.x; q.hp[1] = s2.y; q.hp[2] = s2.z;
+        q.w[0] = w2.r; q.w[1] = w2.g; q.w[2] = w2.b;
+        q.rkey = rng.key;
+        q.rctr = rng.ctr;
+        q.g = (uint32_t)P.g;
+        q.prim = P.prim;
+        q.pslot = P.pslot;
+        q.qslot = P.fixed[0] >= 0 ? (uint32_t)P.fixed[0] : 0xffffffffu;
+        q.mat = -1;
+        q.j = P.j;
+        q.tri = h.tri;
+        q.sub = 0;
+        P.fixed[0] = -2;  // the sub-path owns the global slot now
+      } else {
+        mc_indirect<KINDS>(P, h.p + s2 * kEps, s2, rng, w2);
+      }
+      P.cnt.indirect++;
+    } else if (F.fast_global) {
+      V ex = reflective_bounce(h.n, view, ct);
+      global_query(P, h.p, h.n, ex, ct, h.mat, W * (kd * tw / pd));
+      if (!F.cache) P.cnt.indirect++;
+    }
+    return false;
+  } else if (rnd < pd + pt) {
+    if (!F.transmissive) return false;
+    V ex = transmissive_bounce_nc(F.ir_air, h.n, view, ct, m.ir);
+    sb = F.distrib_trans ? specular_sample_call(ex, m.n, ct, rng) : ex;
+    P.cnt.trans++;
+    tw *= (1.0 - R) * ldc(m.kt) / pt;
+  } else if (rnd < pd + pt + ps) {
+    if (!F.specular) return false;
+    V ex = reflective_bounce(h.n, view, ct);
+    sb = F.distrib_spec ? specular_sample_call(ex, m.n, ct, rng) : ex;
+    P.cnt.spec++;
+    tw *= (ldc(m.ks) + R * ldc(m.kt)) / ps;
+  } else {
+    return false;
+  }
+  L.ray_start = h.p + sb * kEps;
+  L.org = L.ray_start;
+  L.dir = sb;
+  return true;
+}
+
+// MonteCarlo_PathTrace, montecarlo.cpp:16-171
+template <uint32_t KINDS = KINDS_ALL, bool DEFER = false, bool HARD = false>
+__device__ __forceinline__ void mc_path(PathCtx &P, V org, V dir, Rng &rng, C3 W) {
+  if (!P.F->monte_carlo) return;
+  McLoop L;
+  mc_begin(L, org, dir, rng, W);
+  while (mc_step<KINDS, DEFER, HARD>(P, L)) {
+  }
+  rng = L.rng;
 }
 
 // last p in [0, n) with off[p] <= t (off is an exclusive scan, off[0] = 0)
@@ -538,6 +580,7 @@ __device__ __forceinline__ void path_init(PathCtx &P, const RenderArgs &a, int64
   P.cnt = z;
   P.fixed[0] = P.fixed[1] = -1;
   P.hint = -1;
+  P.qstripe = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) & (IND_QS - 1);
 }
 
 __device__ __forceinline__ void path_stats(const RenderArgs &a, const Counts &cnt) {
@@ -901,6 +944,82 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(MC_WPE))) v
     a.base[3 * g + 1] = P.base.g;
     a.base[3 * g + 2] = P.base.b;
     cnt = P.cnt;
+  }
+  path_stats(a, cnt);
+}
+
+// The same Monte Carlo paths with a lane that finishes its path taking the next one (Aila &
+// Laine's persistent "while-while" loop): every lane of a wave runs one iteration of
+// MonteCarlo_PathTrace per trip, whatever path and depth it is at, instead of the wave running
+// as long as its longest path with the finished lanes idle. Paths are handed out in order by one
+// atomic per wave per refill (mc_next); a path's arithmetic, RNG stream, query keys and base
+// slot do not depend on the lane that runs it, so the image and counters equal mc_kernel's.
+template <uint32_t KINDS, bool DEFER, bool HARD>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(MC_WPE)))
+void mc_persist_kernel(RenderArgs a) {
+  const int lane = (int)(threadIdx.x & 63);
+  const SceneView &S = a.S;
+  const Flags &F = a.F;
+  Counts cnt = {0, 0, 0, 0, 0, 0};
+  PathCtx P;
+  McLoop L;
+  bool active = false, more = true;
+  while (true) {
+    if (!active && more) {
+      uint64_t need = __ballot(1);
+      int leader = __ffsll((long long)need) - 1;
+      uint32_t b = 0;
+      if (lane == leader) b = atomicAdd(a.mc_next, (uint32_t)__popcll(need));
+      b = (uint32_t)__shfl((int)b, leader, 64);
+      int64_t t = (int64_t)b + __popcll(need & ((1ull << lane) - 1ull));
+      if (t < a.total_mc) {
+        // mc_kernel's prologue: the path's primary, its first (transmissive / specular) sample
+        int64_t pb = wave_owner(a.mc_off, a.nprim, t, a.total_mc, a.mc_tab);
+        int s = (int)(t - a.mc_off[pb]);
+        const Spawn &sp = a.spawn[pb];
+        int64_t g = (int64_t)a.path_off[pb] + 1 + s;
+        int pix, i, j, k;
+        uint64_t psample;
+        decode_primary(a, pb, pix, i, j, k, psample);
+        const DMaterial &m = S.mats[sp.mat];
+        V p = ld3(sp.p), n = ld3(sp.n), view = ld3(sp.v);
+        double ct = sp.ct, R = sp.R;
+        path_init(P, a, g, pb, 1 + s);
+        P.hint = sp.tri;
+        P.qstripe = (uint32_t)((t >> 6) & (IND_QS - 1));
+        Rng rng;
+        V sb;
+        C3 w;
+        if (s < sp.n_t) {
+          rng.init(F.seed, KIND_TRANS, psample, (uint64_t)s);
+          V ex = transmissive_bounce_nc(F.ir_air, n, view, ct, m.ir);
+          sb = F.distrib_trans ? specular_sample_call(ex, m.n, ct, rng) : ex;
+          w = ((1.0 - R) * ldc(m.kt)) / (double)sp.n_t;
+          P.cnt.trans++;
+        } else {
+          s -= sp.n_t;
+          rng.init(F.seed, KIND_SPEC, psample, (uint64_t)s);
+          V ex = reflective_bounce(n, view, ct);
+          sb = F.distrib_spec ? specular_sample_call(ex, m.n, ct, rng) : ex;
+          w = (ldc(m.kt) * R + ldc(m.ks)) / (double)sp.n_s;
+          P.cnt.spec++;
+        }
+        mc_begin(L, p + sb * kEps, sb, rng, w);
+        if (!F.monte_carlo) L.iter = F.max_monte_depth;  // MonteCarlo_PathTrace returns at once
+        active = true;
+      } else {
+        more = false;  // the counter only grows: this lane will find no more paths
+      }
+    }
+    if (!__any(active)) break;
+    if (active && !mc_step<KINDS, DEFER, HARD>(P, L)) {
+      a.base[3 * P.g] = P.base.r;
+      a.base[3 * P.g + 1] = P.base.g;
+      a.base[3 * P.g + 2] = P.base.b;
+      cnt.shadow += P.cnt.shadow; cnt.monte += P.cnt.monte; cnt.trans += P.cnt.trans;
+      cnt.spec += P.cnt.spec; cnt.indirect += P.cnt.indirect; cnt.caustic += P.cnt.caustic;
+      active = false;
+    }
   }
   path_stats(a, cnt);
 }
@@ -1727,7 +1846,20 @@ void launch_path(const RenderArgs &a, hipStream_t st, hipStream_t st2, hipEvent_
   if (a.total_mc > 0) {
     unsigned g = nblk(a.total_mc, 128);
     if (a.mc_cont) (void)hipMemsetAsync(a.mc_ncont, 0, IND_QS * 32 * sizeof(uint32_t), ms);
-    if (a.mc_cont) {
+    if (a.mc_cont && a.mc_next) {
+      // persistent: enough blocks to fill the chip at MC_WPE waves per SIMD, or one per 128 paths
+      (void)hipMemsetAsync(a.mc_next, 0, sizeof(uint32_t), ms);
+      unsigned gp = std::min(g, (unsigned)(a.mc_persist_blocks > 0 ? a.mc_persist_blocks : 1024));
+      if ((a.S.kinds & ~KINDS_TRI_SPHERE) == 0) {
+        if (a.S.hard_lights) mc_persist_kernel<KINDS_TRI_SPHERE, true, true><<<gp, 128, 0, ms>>>(a);
+        else mc_persist_kernel<KINDS_TRI_SPHERE, true, false><<<gp, 128, 0, ms>>>(a);
+      } else if ((a.S.kinds & ~KINDS_POLY) == 0) {
+        if (a.S.hard_lights) mc_persist_kernel<KINDS_POLY, true, true><<<gp, 128, 0, ms>>>(a);
+        else mc_persist_kernel<KINDS_POLY, true, false><<<gp, 128, 0, ms>>>(a);
+      } else {
+        mc_persist_kernel<KINDS_ALL, true, false><<<gp, 128, 0, ms>>>(a);
+      }
+    } else if (a.mc_cont) {
       if ((a.S.kinds & ~KINDS_TRI_SPHERE) == 0) {
         if (a.S.hard_lights) mc_kernel<KINDS_TRI_SPHERE, true, true><<<g, 128, 0, ms>>>(a);
         else mc_kernel<KINDS_TRI_SPHERE, true, false><<<g, 128, 0, ms>>>(a);
@@ -1737,6 +1869,8 @@ void launch_path(const RenderArgs &a, hipStream_t st, hipStream_t st2, hipEvent_
       } else {
         mc_kernel<KINDS_ALL, true, false><<<g, 128, 0, ms>>>(a);
       }
+    }
+    if (a.mc_cont) {
       if (a.mc_cont2) {
         (void)hipMemsetAsync(a.mc_ncont2, 0, IND_QS * 32 * sizeof(uint32_t), ms);
         launch_mc_sub(a, ms);

@@ -227,8 +227,10 @@ int gi_render_tiles_packed(gi_ctx *ctx, int aa, int width, int height, int tile_
                            gi_render_stats *stats);
 /* Compose the frame from every shard's packed pixels: `packed` is a DEVICE pointer on the
  * context's device to nshards buffers of `stride` pixels (16 B each), shard s at s * stride
- * (the layout of a gather of gi_render_tiles_packed outputs). rgb8 / rgbf (host, optional)
- * receive the full image as gi_render_image returns it. */
+ * (the layout of a gather of gi_render_tiles_packed outputs); the caller must have allocated
+ * all stride * nshards * 16 bytes (each shard's pixel count must be <= stride, checked).
+ * rgb8 / rgbf (host, optional) receive the full image as gi_render_image returns it.
+ * Both packed entry points restore the calling thread's current HIP device on return. */
 int gi_compose_tiles(gi_ctx *ctx, int width, int height, int tile_px, int nshards,
                      const void *packed, int64_t stride, uint8_t *rgb8, float *rgbf);
 /* Quantise a full float image like RenderImage's SetPixelRGB (truncate 255*c). */

@@ -17,8 +17,12 @@ How they were rendered, established by fitting ("Pinning"):
     three channels and independently of distance, angle and light type. No term of the current
     sources (R3PointLight.cpp:214-244, R3DirectionalLight.cpp:134-166, ComputeIllumination
     illumination_utils.cpp:425-494, RenderImage render.cpp:155-259, R2Image::SetPixelRGB) has
-    such a factor, so it is revision drift between the figures and the code; it is applied by
-    scaling the light colours of the scene (direct lighting is linear in them).
+    such a factor, and the lighting code itself is not the cause: the direct layer of
+    display.scn under its rect light (fig_25a, photon_figs.py) matches the current code at gain
+    1 (ratio 1.000, 0.12 LSB RMS over 1,972 blocks). So the four pointlight / dirlight scene
+    files were rendered with dimmer lights than they now hold (as fig_6a/6b come from other
+    spot-light files); the gain is applied by scaling the light colours of the scene (direct
+    lighting is linear in them).
   * fig_6a/6b (spot lights) come from different scene files: with spotlight1.scn as shipped the
     sphere lies outside the 0.331-rad cone (R3SpotLight.cpp:105-115) but the figure shows it lit.
 With aa 2, -no_specular and the gain, >= 99.3 % of the unsaturated pixels of fig_5a/5b/7a/7b

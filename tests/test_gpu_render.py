@@ -159,17 +159,22 @@ def test_indirect_continuation_queue_is_exact(name, extra):
     MonteCarlo_IndirectSample (montecarlo.cpp:177-305) that follow a glass/mirror hit: the f32
     image and every -v counter equal the one-loop-per-lane kernel's (GI_SPLIT_IND=0), also when
     the queue starts far too small (GI_IND_FRAC) and the batch is re-run with more room, and
-    when the Monte Carlo paths' sub-paths skip their lean first-bounce kernel (GI_MC_SUB=0)."""
+    when the Monte Carlo paths' sub-paths skip their lean first-bounce kernel (GI_MC_SUB=0).
+    The Monte Carlo paths (MonteCarlo_PathTrace, montecarlo.cpp:16-171) give the same image and
+    counters in the persistent kernel (a lane takes the next path when its own ends; default,
+    and with a 3-block grid: thousands of refills per wave) and one path per lane
+    (GI_MC_PERSIST=0)."""
     args = [scene(name), "/tmp/x.png", "-resolution", "32", "32", "-aa", "1", "-it", "32",
             "-tt", "8", "-st", "8", "-seed", "4"] + extra
     p, sc, _o, w, h, aa, real = gi_amd.ParseArgs(args)
     out = []
-    keys = ("GI_SPLIT_IND", "GI_IND_FRAC", "GI_MC_SUB")
+    keys = ("GI_SPLIT_IND", "GI_IND_FRAC", "GI_MC_SUB", "GI_MC_PERSIST")
     old = {k: os.environ.get(k) for k in keys}
     try:
         for env in ({"GI_SPLIT_IND": "0"}, {"GI_SPLIT_IND": "1"},
                     {"GI_SPLIT_IND": "1", "GI_IND_FRAC": "0.00001"},
-                    {"GI_SPLIT_IND": "1", "GI_MC_SUB": "0"}):
+                    {"GI_SPLIT_IND": "1", "GI_MC_SUB": "0"}, {"GI_MC_PERSIST": "0"},
+                    {"GI_MC_PERSIST": "3"}):
             for k in keys:
                 os.environ.pop(k, None)
             os.environ.update(env)
@@ -278,3 +283,33 @@ def test_c2_full_frame_properties():
         finally:
             r.close()
     assert len(set(hashes)) == 1, hashes
+
+
+def test_batch_rerun_on_slot_guard_is_exact(monkeypatch):
+    """A batch whose path slots (with the indirect tiles' padding to the largest indirect count
+    of each 64-primary tile) exceed the 32-bit guard is re-run at half the primary samples
+    instead of failing (gi_host.cpp render_pixels): with the guard lowered (GI_SLOT_LIMIT) the
+    image and every counter equal the unconstrained render's. The frame is 37 x 21 (partial
+    tiles), -it 96 makes the indirect counts vary inside tiles (diffuse vs glass / background)."""
+    args = [scene("cornell.scn"), "/tmp/x.png", "-resolution", "37", "21", "-aa", "1",
+            "-global", "20000", "-caustic", "20000", "-it", "96", "-tt", "8", "-st", "8",
+            "-seed", "2"]
+    p, sc, _o, w, h, aa, real = gi_amd.ParseArgs(args)
+    out = []
+    for lim in (None, "60000"):
+        if lim:
+            monkeypatch.setenv("GI_SLOT_LIMIT", lim)
+        r = gi_amd.Renderer(0, p)
+        try:
+            r.ReadScene(sc, real)
+            r.MapPhotons()
+            rgb, f, st = r.RenderImage(aa, w, h, want_float=True)
+            out.append((f, st, rgb))
+        finally:
+            r.close()
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    for k in ("screen_rays", "shadow_rays", "monte_carlo_rays", "transmissive_samples",
+              "specular_samples", "indirect_samples", "caustic_samples", "knn_queries"):
+        assert out[0][1][k] == out[1][1][k], k
+    o, _ = oracle_lib.render(args, w, h)
+    compare(out[1][2], o, 0.99, 0.995, 0.5)

@@ -106,6 +106,7 @@ struct RenderArgs {
   uint32_t mc_cap_s;
   uint32_t *mc_next;    // mc_persist_kernel's path counter (null: mc_kernel, one path per lane)
   int32_t mc_persist_blocks;  // its grid
+  int32_t cont_persist_blocks;  // > 0: continuation queues in ind_cont_persist_kernel, this grid
   IndCont *mc_cont2;    // ... those whose first bounce hit glass / a mirror (mc_sub_kernel),
   uint32_t *mc_ncont2;  // at that hit, same stripes and capacity
   // Indirect paths' slots, tiled: primaries b in tiles of 64 (T = b / 64); tile T holds

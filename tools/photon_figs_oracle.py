@@ -28,19 +28,19 @@ import photon_figs as pf  # noqa: E402
 
 
 def main():
-    names = sys.argv[1:] or list(pf.FIGS)
+    names = sys.argv[1:] or list(pf.FIGS) + list(pf.EVIDENCE)
     old = dict(np.load(pf.STATS)) if os.path.exists(pf.STATS) else {}
     threads = len(os.sched_getaffinity(0))
     for name in names:
         t0 = time.time()
         old[name + "/figure"] = pf.figure_blocks(name).astype(np.float32)
         old[name + "/mask"] = pf.block_mask(name, oracle_lib.intersect)
-        if not pf.FIGS[name][4]:  # GPU twin only: the figure's blocks and mask
+        if not pf.config(name)[4]:  # GPU twin only: the figure's blocks and mask
             np.savez_compressed(pf.STATS, **old)
             print(f"{name}: figure blocks and mask only", flush=True)
             continue
         blocks = []
-        for s in pf.SEEDS:
+        for s in pf.seeds(name):
             args, w, h = pf.render_args(name, s, threads=threads)
             rgb, _st = oracle_lib.render(args, w, h)
             blocks.append(pf.render_blocks(rgb, name))

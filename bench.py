@@ -313,8 +313,11 @@ def main():
             "fbq0", "fbq1", "p2ms0", "p2ms1", "p2q0", "p2q1", "devmax", "devmin", "gather")
     agg = dict.fromkeys(keys, 0.0)
     kind = [-1, -1]
+    step_ms = []
     for _ in range(a.steps):
+        ts = time.perf_counter()
         st = step()
+        step_ms.append(round((time.perf_counter() - ts) * 1e3, 1))
         kind = list(st.get("knn_map_kind", kind))
         for m in (0, 1):
             agg[f"q{m}"] += st["knn_map_queries"][m]
@@ -413,6 +416,7 @@ def main():
             "image_sha16": (hashlib.sha256(rgb.tobytes()).hexdigest()[:16]
                             if rgb is not None else None),
             "roofline": roofline, "cpu_baseline": cpu,
+            "step_ms": step_ms,
         }
         if shard is not None:
             line["shard"] = {"shard": shard[0], "nshards": shard[1], "pixels": npix_shard,

@@ -299,8 +299,6 @@ struct gi_ctx {
   DBuf mc_cont, mc_ncont;         // Monte Carlo paths' indirect sub-paths
   DBuf mc_cont2, mc_ncont2;       // ... those continuing past a glass / mirror first hit
   bool mc_sub = true;             // sub-paths' first bounce in mc_sub_kernel (GI_MC_SUB=0: all in ind_cont_kernel)
-  int cont_persist = 1024;        // continuation queues in ind_cont_persist_kernel with this many
-                                  // blocks (GI_CONT_PERSIST; 0: ind_cont_kernel, one entry per lane)
   int mc_persist = 1024;          // Monte Carlo paths in mc_persist_kernel with this many blocks
                                   // (GI_MC_PERSIST; 0: mc_kernel, one path per lane)
   DBuf prim_rgb;                  // per-primary sums of the reduction
@@ -1306,7 +1304,6 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     a.ind_bmask = a.ind_qmask + trows + 1;
     HIPCHK(c, c->base.ensure(((size_t)total_paths + tind) * 24));
     a.base = c->base.as<double>();
-    a.cont_persist_blocks = c->cont_persist;
     // continuation queue: stripe s takes the appends of waves w with w % IND_QS == s (<= 64
     // paths per wave, so `full` entries per stripe can never overflow); sized from the fill
     // seen so far (c->ind_frac of full), re-run with more room when a stripe overflows
@@ -1550,7 +1547,6 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_CHUNK_DK")) c->chunk_dk = atoi(s) != 0;
   if (const char *s = getenv("GI_MC_SUB")) c->mc_sub = atoi(s) != 0;
   if (const char *s = getenv("GI_MC_PERSIST")) c->mc_persist = std::max(0, atoi(s));
-  if (const char *s = getenv("GI_CONT_PERSIST")) c->cont_persist = std::max(0, atoi(s));
   if (const char *s = getenv("GI_KNN_LOG")) c->knn_log = atoi(s) != 0;
   if (const char *s = getenv("GI_ELEM_PRETEST")) c->elem_pretest = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_FB_ALL")) c->chunk_fb_all = atoi(s) != 0;

@@ -52,6 +52,8 @@ struct IndCont {
 // continuation queue stripes: wave w appends to stripe w % IND_QS (one atomic per wave on a
 // counter shared by 1/IND_QS of the waves)
 constexpr int IND_QS = 64;
+// IndCont::g of an empty entry of the dense Monte Carlo sub-path queue (mc_persist_kernel)
+constexpr uint32_t IND_EMPTY = 0xffffffffu;
 // chunk k-NN fallback list stripes: block b appends to stripe b % FB_QS
 constexpr int FB_QS = 64;
 
@@ -106,7 +108,6 @@ struct RenderArgs {
   uint32_t mc_cap_s;
   uint32_t *mc_next;    // mc_persist_kernel's path counter (null: mc_kernel, one path per lane)
   int32_t mc_persist_blocks;  // its grid
-  int32_t cont_persist_blocks;  // > 0: continuation queues in ind_cont_persist_kernel, this grid
   IndCont *mc_cont2;    // ... those whose first bounce hit glass / a mirror (mc_sub_kernel),
   uint32_t *mc_ncont2;  // at that hit, same stripes and capacity
   // Indirect paths' slots, tiled: primaries b in tiles of 64 (T = b / 64); tile T holds

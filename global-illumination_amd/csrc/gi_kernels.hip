@@ -219,6 +219,8 @@ struct PathCtx {
   int hint;         // triangle the path's current ray leaves from (ray_mesh_bvh), -1 none
   uint32_t qstripe; // mc_cont stripe of the path's deferred sub-path (gi_host.cpp sizes a stripe
                     // for the paths of every IND_QS-th group of 64)
+  int64_t cont_slot;  // >= 0: the sub-path's fixed mc_cont entry (mc_persist_kernel: the path's
+                      // index, so the queue stays in path order); -1: striped append
 };
 
 // the indirect paths' tiled global-list slots carry no key: the reduction reads their row
@@ -425,23 +427,19 @@ __device__ __forceinline__ bool mc_step(PathCtx &P, McLoop &L) {
       C3 w2 = W * ((kd * kd * tw) / pd);
       if (DEFER) {
         V o2 = h.p + s2 * kEps;
-        // one atomic per stripe present among the appending lanes (one in mc_kernel, where the
-        // stripe is the wave's; a few in mc_persist_kernel, where it is the path's)
-        int lane = (int)(threadIdx.x & 63);
-        const uint32_t stripe = P.qstripe;
-        uint64_t pend = __ballot(1);
-        uint32_t qslot = 0;
-        while (pend) {
-          int leader = __ffsll((long long)pend) - 1;
-          uint32_t sl = (uint32_t)__shfl((int)stripe, leader, 64);
-          uint64_t grp = __ballot(stripe == sl);
+        size_t e;
+        if (P.cont_slot >= 0) {
+          e = (size_t)P.cont_slot;  // mc_persist_kernel: the entry of path t is slot t
+        } else {  // mc_kernel: one atomic per wave on its stripe
+          int lane = (int)(threadIdx.x & 63);
+          uint64_t act = __ballot(1);
+          int leader = __ffsll((long long)act) - 1;
           uint32_t qb = 0;
-          if (lane == leader) qb = atomicAdd(&P.A->mc_ncont[sl * 32], (uint32_t)__popcll(grp));
+          if (lane == leader) qb = atomicAdd(&P.A->mc_ncont[P.qstripe * 32], (uint32_t)__popcll(act));
           qb = (uint32_t)__shfl((int)qb, leader, 64);
-          if (stripe == sl) qslot = qb + (uint32_t)__popcll(grp & ((1ull << lane) - 1ull));
-          pend &= ~grp;
+          e = (size_t)P.qstripe * P.A->mc_cap_s + qb + (uint32_t)__popcll(act & ((1ull << lane) - 1ull));
         }
-        IndCont &q = P.A->mc_cont[(size_t)stripe * P.A->mc_cap_s + qslot];
+        IndCont &q = P.A->mc_cont[e];
         q.org[0] = o2.x; q.org[1] = o2.y; q.org[2] = o2.z;
         q.hp[0] = s2.x; q.hp[1] = s2.y; q.hp[2] = s2.z;
         q.w[0] = w2.r; q.w[1] = w2.g; q.w[2] = w2.b;
@@ -581,6 +579,7 @@ __device__ __forceinline__ void path_init(PathCtx &P, const RenderArgs &a, int64
   P.fixed[0] = P.fixed[1] = -1;
   P.hint = -1;
   P.qstripe = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) & (IND_QS - 1);
+  P.cont_slot = -1;
 }
 
 __device__ __forceinline__ void path_stats(const RenderArgs &a, const Counts &cnt) {
@@ -746,6 +745,7 @@ void ind_cont_kernel(RenderArgs a, const IndCont *queue, const uint32_t *fill, u
     uint32_t idx = (r * parts + part) * blockDim.x + threadIdx.x;
     if (idx >= n) continue;
     const IndCont &q = queue[(size_t)stripe * cap_s + idx];
+    if (q.g == IND_EMPTY) continue;  // a Monte Carlo path that deferred no sub-path
     PathCtx P;
     path_init(P, a, q.g, q.prim, (int)q.pslot);
     P.fixed[0] = (q.qslot == 0xffffffffu) ? -1 : (int64_t)q.qslot;
@@ -802,113 +802,6 @@ void ind_cont_kernel(RenderArgs a, const IndCont *queue, const uint32_t *fill, u
   path_stats(a, tot);
 }
 
-// ind_cont_kernel with a lane that finishes its entry taking the next one (as mc_persist_kernel):
-// a block starts on stripe blockIdx % IND_QS, takes entries from the stripe's second counter word
-// (fill[32 s + 1], zeroed with the fills) one atomic per wave per refill, and moves on to the next
-// stripe when its own is drained, so no wave idles behind its longest path and no block behind
-// its stripe. Each entry's arithmetic, RNG stream, query slot and base writes are as in
-// ind_cont_kernel, so the image and counters are the same.
-template <uint32_t KINDS>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3)))
-void ind_cont_persist_kernel(RenderArgs a, const IndCont *queue, uint32_t *fill, uint32_t cap_s) {
-  const int lane = (int)(threadIdx.x & 63);
-  Counts tot = {0, 0, 0, 0, 0, 0};
-  PathCtx P;
-  Rng rng;
-  C3 tw = rgb(1, 1, 1), W = rgb(0, 0, 0);
-  V org = mk(0, 0, 0), dir = mk(0, 0, 0);
-  int iter = 0;
-  uint32_t g = 0, qslot = 0;
-  bool at_hit = false, sub = false;
-  bool active = false;
-  uint32_t s = blockIdx.x % IND_QS;  // wave-uniform: the stripe this wave takes entries from
-  int stripes_left = IND_QS;
-  const int maxd = a.F.max_monte_depth;
-  while (true) {
-    // refill (converged: every lane takes part in the ballots); a drained stripe sends the
-    // wave's hungry lanes on to the next one
-    while (stripes_left > 0) {
-      const uint64_t need = __ballot(!active);
-      if (need == 0) break;
-      const uint32_t n = min(fill[s * 32], cap_s);
-      const int leader = __ffsll((long long)need) - 1;
-      uint32_t b = 0;
-      if (lane == leader) b = atomicAdd(&fill[s * 32 + 1], (uint32_t)__popcll(need));
-      b = (uint32_t)__shfl((int)b, leader, 64);
-      if (!active) {
-        const uint32_t idx = b + (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
-        if (idx < n) {
-          const IndCont &q = queue[(size_t)s * cap_s + idx];
-          path_init(P, a, q.g, q.prim, (int)q.pslot);
-          P.fixed[0] = (q.qslot == 0xffffffffu) ? -1 : (int64_t)q.qslot;
-          P.hint = q.tri;
-          rng.key = q.rkey;
-          rng.ctr = q.rctr;
-          tw = rgb(1, 1, 1);
-          W = ldc(q.w);
-          org = ld3(q.org);
-          dir = org;
-          g = q.g;
-          qslot = q.qslot;
-          at_hit = q.mat >= 0;
-          sub = q.sub != 0;
-          if (sub) P.j = q.j;
-          bool go;
-          if (at_hit) {
-            Hit h;
-            h.p = ld3(q.hp);
-            h.n = ld3(q.hn);
-            h.t = 0.0;
-            h.mat = q.mat;
-            h.tri = q.tri;
-            go = ind_shade<false>(P, h, org, dir, rng, W, tw);
-            iter = 1;
-          } else {
-            P.j = q.j;
-            dir = ld3(q.hp);
-            go = true;
-            iter = 0;
-          }
-          if (!go) iter = maxd;  // ends at its first step below
-          active = true;
-        }
-      }
-      if (__ballot(!active) == 0) break;
-      s = (s + 1) % IND_QS;  // some lanes found stripe s drained
-      stripes_left--;
-    }
-    if (!__any(active)) break;
-    if (active) {
-      bool cont = iter < maxd && ind_bounce<KINDS>(P, org, dir, rng, W, tw);
-      iter++;
-      if (!cont) {
-        const bool used = P.fixed[0] == -2;
-        if (P.fixed[0] >= 0) put_none(a, 0, P.fixed[0]);
-        double *bp = a.base + 3 * (int64_t)g;
-        if (at_hit && !sub) {
-          const int64_t tau = (int64_t)qslot - a.qind_base;
-          const unsigned long long bit = 1ull << (tau & 63);
-          if (used) atomicOr((unsigned long long *)&a.ind_qmask[tau >> 6], bit);
-          if (!base_is_pzero(P.base)) {
-            bp[0] = P.base.r;
-            bp[1] = P.base.g;
-            bp[2] = P.base.b;
-            atomicOr((unsigned long long *)&a.ind_bmask[tau >> 6], bit);
-          }
-        } else {  // the sub-path's background term is the last addition to the path's sum
-          bp[0] = bp[0] + P.base.r;
-          bp[1] = bp[1] + P.base.g;
-          bp[2] = bp[2] + P.base.b;
-        }
-        tot.shadow += P.cnt.shadow; tot.monte += P.cnt.monte; tot.trans += P.cnt.trans;
-        tot.spec += P.cnt.spec; tot.indirect += P.cnt.indirect; tot.caustic += P.cnt.caustic;
-        active = false;
-      }
-    }
-  }
-  path_stats(a, tot);
-}
-
 // The Monte Carlo paths' indirect sub-paths (mc_path's deferred IndirectIllumination sample,
 // montecarlo.cpp:177-305 from a diffuse hit): their first bounce, one per thread, in the lean
 // shape of ind_kernel. A sub-path that hits a diffuse-only material ends there (its query, or
@@ -931,11 +824,12 @@ void mc_sub_kernel(RenderArgs a, const IndCont *queue, const uint32_t *fill, uin
   const uint32_t rounds = (n + parts * blockDim.x - 1) / (parts * blockDim.x);
   for (uint32_t r = 0; r < rounds; r++) {
     const uint32_t idx = (r * parts + part) * blockDim.x + threadIdx.x;
-    const bool on = idx < n;
+    bool on = idx < n;
     bool queue_it = false;
     Hit h;
     // the entry is read where its fields are used (a register copy of all 128 B spilled)
     const IndCont &q = queue[(size_t)stripe * cap_s + (on ? idx : 0u)];
+    if (on && q.g == IND_EMPTY) on = false;  // a Monte Carlo path that deferred no sub-path
     PathCtx P;
     Rng rng;
     C3 W = rgb(0, 0, 0);
@@ -1071,6 +965,12 @@ void mc_persist_kernel(RenderArgs a) {
   PathCtx P;
   McLoop L;
   bool active = false, more = true;
+  if (DEFER && blockIdx.x == 0 && threadIdx.x < IND_QS) {
+    // the dense queue as the striped consumers read it: stripe s = paths [s cap, (s + 1) cap)
+    const int64_t lo = (int64_t)threadIdx.x * a.mc_cap_s;
+    const int64_t nf = a.total_mc - lo;
+    a.mc_ncont[threadIdx.x * 32] = (uint32_t)(nf < 0 ? 0 : (nf > a.mc_cap_s ? a.mc_cap_s : nf));
+  }
   while (true) {
     if (!active && more) {
       uint64_t need = __ballot(1);
@@ -1093,7 +993,7 @@ void mc_persist_kernel(RenderArgs a) {
         double ct = sp.ct, R = sp.R;
         path_init(P, a, g, pb, 1 + s);
         P.hint = sp.tri;
-        P.qstripe = (uint32_t)((t >> 6) & (IND_QS - 1));
+        P.cont_slot = t;
         Rng rng;
         V sb;
         C3 w;
@@ -1120,6 +1020,9 @@ void mc_persist_kernel(RenderArgs a) {
     }
     if (!__any(active)) break;
     if (active && !mc_step<KINDS, DEFER, HARD>(P, L)) {
+      // a path that deferred no sub-path marks its mc_cont entry empty (P.fixed[0] == -2 after
+      // a deferral)
+      if (DEFER && P.fixed[0] != -2) a.mc_cont[P.cont_slot].g = IND_EMPTY;
       a.base[3 * P.g] = P.base.r;
       a.base[3 * P.g + 1] = P.base.g;
       a.base[3 * P.g + 2] = P.base.b;
@@ -1922,17 +1825,6 @@ void launch_ind(const RenderArgs &a, unsigned g, hipStream_t st) {
 }
 void launch_cont(const RenderArgs &a, const IndCont *q, const uint32_t *fill, uint32_t cap_s,
                  hipStream_t st) {
-  if (a.cont_persist_blocks > 0) {
-    uint32_t *f = const_cast<uint32_t *>(fill);  // the refill counters live beside the fills
-    const unsigned gp = (unsigned)a.cont_persist_blocks;
-    if ((a.S.kinds & ~KINDS_TRI_SPHERE) == 0)
-      ind_cont_persist_kernel<KINDS_TRI_SPHERE><<<gp, 128, 0, st>>>(a, q, f, cap_s);
-    else if ((a.S.kinds & ~KINDS_POLY) == 0)
-      ind_cont_persist_kernel<KINDS_POLY><<<gp, 128, 0, st>>>(a, q, f, cap_s);
-    else
-      ind_cont_persist_kernel<KINDS_ALL><<<gp, 128, 0, st>>>(a, q, f, cap_s);
-    return;
-  }
   if ((a.S.kinds & ~KINDS_TRI_SPHERE) == 0)
     ind_cont_kernel<KINDS_TRI_SPHERE><<<IND_QS * 32, 128, 0, st>>>(a, q, fill, cap_s);
   else if ((a.S.kinds & ~KINDS_POLY) == 0)

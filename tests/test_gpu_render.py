@@ -163,22 +163,18 @@ def test_indirect_continuation_queue_is_exact(name, extra):
     The Monte Carlo paths (MonteCarlo_PathTrace, montecarlo.cpp:16-171) give the same image and
     counters in the persistent kernel (a lane takes the next path when its own ends; default,
     and with a 3-block grid: thousands of refills per wave) and one path per lane
-    (GI_MC_PERSIST=0); and the continuation queues the same in their persistent kernel (default;
-    with a 2-block grid every wave drains all 64 stripes in turn) and one entry per lane
-    (GI_CONT_PERSIST=0)."""
+    (GI_MC_PERSIST=0), also with their sub-paths going straight to ind_cont_kernel."""
     args = [scene(name), "/tmp/x.png", "-resolution", "32", "32", "-aa", "1", "-it", "32",
             "-tt", "8", "-st", "8", "-seed", "4"] + extra
     p, sc, _o, w, h, aa, real = gi_amd.ParseArgs(args)
     out = []
-    keys = ("GI_SPLIT_IND", "GI_IND_FRAC", "GI_MC_SUB", "GI_MC_PERSIST", "GI_CONT_PERSIST")
+    keys = ("GI_SPLIT_IND", "GI_IND_FRAC", "GI_MC_SUB", "GI_MC_PERSIST")
     old = {k: os.environ.get(k) for k in keys}
     try:
         for env in ({"GI_SPLIT_IND": "0"}, {"GI_SPLIT_IND": "1"},
                     {"GI_SPLIT_IND": "1", "GI_IND_FRAC": "0.00001"},
                     {"GI_SPLIT_IND": "1", "GI_MC_SUB": "0"}, {"GI_MC_PERSIST": "0"},
-                    {"GI_MC_PERSIST": "3"}, {"GI_CONT_PERSIST": "0"},
-                    {"GI_CONT_PERSIST": "2"},
-                    {"GI_CONT_PERSIST": "2", "GI_IND_FRAC": "0.00001", "GI_MC_SUB": "0"}):
+                    {"GI_MC_PERSIST": "3"}, {"GI_MC_PERSIST": "3", "GI_MC_SUB": "0"}):
             for k in keys:
                 os.environ.pop(k, None)
             os.environ.update(env)

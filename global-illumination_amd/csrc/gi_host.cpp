@@ -335,6 +335,7 @@ struct gi_ctx {
   // query budget below (queries per primary sample vary ~10x between scenes).
   int64_t prim_per_batch = 1 << 21;
   int64_t batch_reruns = 0;          // batches re-run smaller for 32-bit path slots (render_pixels)
+  bool batch_log = false;            // GI_BATCH_LOG: per-batch sizes and times on stderr
   int64_t query_budget = 400000000;  // photon-map queries per batch (~120 B each: ~48 GB)
   double q_per_prim = 0.0;           // largest queries per primary sample seen so far
   float sbmin[3] = {0, 0, 0}, sbmax[3] = {1, 1, 1};
@@ -1202,7 +1203,10 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
   int64_t shrink = 1;
   uint64_t slot_limit = 0xFFFFFFF0ull;
   if (const char *s = getenv("GI_SLOT_LIMIT")) slot_limit = std::max(1ULL, strtoull(s, nullptr, 10));
+  int64_t nbatch = 0;
   for (int64_t p0 = 0, npix = 0; p0 < npix_total; p0 += npix) {
+    auto tb0 = std::chrono::steady_clock::now();
+    int attempts_used = 0;
     // batch size: prim_per_batch primary samples, fewer when the query rate seen so far would
     // exceed the query budget (the first batch of a scene starts at 1/8 to measure that rate)
     int64_t prim_cap = c->prim_per_batch;
@@ -1364,6 +1368,7 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
       if (a.split_ind && a.total_ind > 0)
         HIPCHK(c, hipMemcpyAsync(fills, c->ind_ncont.p, sizeof fills, hipMemcpyDeviceToHost, c->stream));
       HIPCHK(c, hipStreamSynchronize(c->stream));
+      attempts_used = attempt + 1;
       bool ok = nq[0] <= a.qcap[0] && nq[1] <= a.qcap[1];
       if (a.split_ind && a.total_ind > 0) {
         uint32_t mx = 0;
@@ -1439,6 +1444,15 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     launch_reduce(a, c->stream);
     HIPCHK(c, hipGetLastError());
     if (c->progress) c->progress(0, (double)(p0 + npix) / (double)npix_total, c->progress_user);
+    if (c->batch_log) {  // GI_BATCH_LOG: one stderr line per batch (synchronises the batch)
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count();
+      fprintf(stderr, "[gi] batch %lld: pixels %lld primaries %lld paths %u tiled %llu mc %lld "
+              "queries %u + %u, path passes %d, %.1f ms\n", (long long)nbatch, (long long)npix,
+              (long long)nprim, total_paths, (unsigned long long)tind, (long long)a.total_mc,
+              nq[0], nq[1], attempts_used, ms);
+    }
+    nbatch++;
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (rs) {
@@ -1547,6 +1561,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_CHUNK_DK")) c->chunk_dk = atoi(s) != 0;
   if (const char *s = getenv("GI_MC_SUB")) c->mc_sub = atoi(s) != 0;
   if (const char *s = getenv("GI_MC_PERSIST")) c->mc_persist = std::max(0, atoi(s));
+  if (const char *s = getenv("GI_BATCH_LOG")) c->batch_log = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_LOG")) c->knn_log = atoi(s) != 0;
   if (const char *s = getenv("GI_ELEM_PRETEST")) c->elem_pretest = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_FB_ALL")) c->chunk_fb_all = atoi(s) != 0;

@@ -41,6 +41,7 @@ hipError_t morton_order(const float4 *q, int64_t n, const float bmin[3], const f
   hipError_t e;
   auto grow = [&](void *&p, size_t &cap, size_t bytes) -> hipError_t {
     if (bytes <= cap && p) return hipSuccess;
+    if (cap) bytes = std::max(bytes, cap + cap / 2);  // growth with headroom (gi_host.cpp DBuf)
     if (p) hipFree(p);
     p = nullptr;
     cap = 0;
@@ -90,6 +91,7 @@ hipError_t key_order(const uint64_t *keys, int64_t n, int key_bits, KeySortScrat
   hipError_t e;
   auto grow = [&](void *&p, size_t &cap, size_t bytes) -> hipError_t {
     if (bytes <= cap && p) return hipSuccess;
+    if (cap) bytes = std::max(bytes, cap + cap / 2);  // growth with headroom (gi_host.cpp DBuf)
     if (p) hipFree(p);
     p = nullptr;
     cap = 0;

@@ -309,8 +309,8 @@ struct gi_ctx {
   DBuf mc_cont, mc_ncont;         // Monte Carlo paths' indirect sub-paths
   DBuf mc_cont2, mc_ncont2;       // ... those continuing past a glass / mirror first hit
   bool mc_sub = true;             // sub-paths' first bounce in mc_sub_kernel (GI_MC_SUB=0: all in ind_cont_kernel)
-  int mc_persist = 1024;          // Monte Carlo paths in mc_persist_kernel with this many blocks
-                                  // (GI_MC_PERSIST; 0: mc_kernel, one path per lane)
+  int mc_persist = -1;            // Monte Carlo paths in mc_persist_kernel with this many blocks
+                                  // (GI_MC_PERSIST; 0: mc_kernel, one path per lane; -1: auto)
   DBuf prim_rgb;                  // per-primary sums of the reduction
   DBuf ind_tab, mc_tab;           // row -> tile of the tiled indirect entries; owner of MC path 64k
   DBuf ind_trows, ind_rows;       // indirect paths' tiled slots: rows per tile, their scan
@@ -1331,9 +1331,14 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
       a.mc_cont = c->mc_cont.as<IndCont>();
       a.mc_ncont = c->mc_ncont.as<uint32_t>();
       a.mc_cap_s = (uint32_t)full;
-      if (c->mc_persist > 0) {  // mc_persist_kernel: path counter in the spare qcount word
+      // mc_persist_kernel (path counter in the spare qcount word): always with a grid given,
+      // and by default (-1) where a bounce's direct light is a soft-shadow fan, the only case it
+      // was measured faster (C3 +5.5 %; with hard lights the plain kernel wins: C2 -0.4 %, C4
+      // -7.4 %, since the persistent waves hold every SIMD's registers while the indirect kernel
+      // on the other stream waits)
+      if (c->mc_persist > 0 || (c->mc_persist < 0 && !a.S.hard_lights)) {
         a.mc_next = c->qcount.as<uint32_t>() + 2;
-        a.mc_persist_blocks = c->mc_persist;
+        a.mc_persist_blocks = c->mc_persist > 0 ? c->mc_persist : 1024;
       }
       if (c->mc_sub) {
         HIPCHK(c, c->mc_cont2.ensure((size_t)IND_QS * full * sizeof(IndCont)));
@@ -1570,7 +1575,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_KNN_DK")) c->use_dk = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_DK")) c->chunk_dk = atoi(s) != 0;
   if (const char *s = getenv("GI_MC_SUB")) c->mc_sub = atoi(s) != 0;
-  if (const char *s = getenv("GI_MC_PERSIST")) c->mc_persist = std::max(0, atoi(s));
+  if (const char *s = getenv("GI_MC_PERSIST")) c->mc_persist = std::max(-1, atoi(s));
   if (const char *s = getenv("GI_BATCH_LOG")) c->batch_log = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_LOG")) c->knn_log = atoi(s) != 0;
   if (const char *s = getenv("GI_ELEM_PRETEST")) c->elem_pretest = atoi(s) != 0;

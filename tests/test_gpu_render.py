@@ -161,8 +161,8 @@ def test_indirect_continuation_queue_is_exact(name, extra):
     the queue starts far too small (GI_IND_FRAC) and the batch is re-run with more room, and
     when the Monte Carlo paths' sub-paths skip their lean first-bounce kernel (GI_MC_SUB=0).
     The Monte Carlo paths (MonteCarlo_PathTrace, montecarlo.cpp:16-171) give the same image and
-    counters in the persistent kernel (a lane takes the next path when its own ends; default,
-    and with a 3-block grid: thousands of refills per wave) and one path per lane
+    counters in the persistent kernel (a lane takes the next path when its own ends; jensen's
+    default, and forced with a 3-block grid: thousands of refills per wave) and one path per lane
     (GI_MC_PERSIST=0), also with their sub-paths going straight to ind_cont_kernel."""
     args = [scene(name), "/tmp/x.png", "-resolution", "32", "32", "-aa", "1", "-it", "32",
             "-tt", "8", "-st", "8", "-seed", "4"] + extra

@@ -40,10 +40,14 @@ struct DBuf {
   size_t cap = 0;
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap && p) return hipSuccess;
-    const size_t grown = cap ? cap + cap / 2 : 0;
+    size_t grown = cap ? cap + cap / 2 : 0;
     if (p) hipFree(p);
     p = nullptr;
     cap = 0;
+    if (grown > bytes) {  // headroom only while a quarter of the device stays free after it
+      size_t fr = 0, tot = 0;
+      if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < grown + tot / 4) grown = 0;
+    }
     size_t want = std::max(std::max(bytes, grown), (size_t)256);
     hipError_t e = hipMalloc(&p, want);
     if (e != hipSuccess && want > bytes) {  // no room for the headroom: exactly what is asked

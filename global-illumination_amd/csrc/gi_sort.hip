@@ -41,12 +41,21 @@ hipError_t morton_order(const float4 *q, int64_t n, const float bmin[3], const f
   hipError_t e;
   auto grow = [&](void *&p, size_t &cap, size_t bytes) -> hipError_t {
     if (bytes <= cap && p) return hipSuccess;
-    if (cap) bytes = std::max(bytes, cap + cap / 2);  // growth with headroom (gi_host.cpp DBuf)
+    size_t want = cap ? std::max(bytes, cap + cap / 2) : bytes;  // headroom (gi_host.cpp DBuf)
     if (p) hipFree(p);
     p = nullptr;
     cap = 0;
-    hipError_t r = hipMalloc(&p, bytes);
-    if (r == hipSuccess) cap = bytes;
+    if (want > bytes) {
+      size_t fr = 0, tot = 0;
+      if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < want + tot / 4) want = bytes;
+    }
+    hipError_t r = hipMalloc(&p, want);
+    if (r != hipSuccess && want > bytes) {
+      (void)hipGetLastError();
+      want = bytes;
+      r = hipMalloc(&p, want);
+    }
+    if (r == hipSuccess) cap = want;
     return r;
   };
   size_t b4 = (size_t)n * 4;
@@ -91,12 +100,21 @@ hipError_t key_order(const uint64_t *keys, int64_t n, int key_bits, KeySortScrat
   hipError_t e;
   auto grow = [&](void *&p, size_t &cap, size_t bytes) -> hipError_t {
     if (bytes <= cap && p) return hipSuccess;
-    if (cap) bytes = std::max(bytes, cap + cap / 2);  // growth with headroom (gi_host.cpp DBuf)
+    size_t want = cap ? std::max(bytes, cap + cap / 2) : bytes;  // headroom (gi_host.cpp DBuf)
     if (p) hipFree(p);
     p = nullptr;
     cap = 0;
-    hipError_t r = hipMalloc(&p, bytes);
-    if (r == hipSuccess) cap = bytes;
+    if (want > bytes) {
+      size_t fr = 0, tot = 0;
+      if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < want + tot / 4) want = bytes;
+    }
+    hipError_t r = hipMalloc(&p, want);
+    if (r != hipSuccess && want > bytes) {
+      (void)hipGetLastError();
+      want = bytes;
+      r = hipMalloc(&p, want);
+    }
+    if (r == hipSuccess) cap = want;
     return r;
   };
   if ((e = grow(s.k1, s.k1_cap, (size_t)n * 8)) != hipSuccess) return e;

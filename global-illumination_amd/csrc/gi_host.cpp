@@ -2354,6 +2354,24 @@ int gi_knn_bench(gi_ctx *c, int map, int64_t n, const double *pts, const double 
   return GI_OK;
 }
 
+int gi_math_probe(gi_ctx *c, int fn, int64_t n, const double *x, const double *y, double *out) {
+  if (!c || n < 0 || fn < 0 || fn > 5 || (n > 0 && (!x || !y || !out))) return GI_ERR_ARG;
+  if (n == 0) return GI_OK;
+  hipSetDevice(c->device);
+  DBuf dx, dy, dout;
+  HIPCHK(c, upload(dx, x, (size_t)n * 8, c->stream));
+  HIPCHK(c, upload(dy, y, (size_t)n * 8, c->stream));
+  HIPCHK(c, dout.ensure((size_t)n * 8));
+  launch_math_probe(fn, n, dx.as<double>(), dy.as<double>(), dout.as<double>(), c->stream);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(out, dout.p, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  dx.release();
+  dy.release();
+  dout.release();
+  return GI_OK;
+}
+
 int gi_intersect_batch(gi_ctx *c, int64_t n, const double *org, const double *dir, int32_t *hit,
                        double *t, double *point, double *normal, int32_t *material) {
   if (!c) return GI_ERR_ARG;

@@ -370,6 +370,8 @@ void launch_photons(const PhotonArgs &a, int mode, hipStream_t st);
 void launch_photon_gather(const gi_photon_dev *src, const uint32_t *slot, int64_t n,
                           gi_photon_dev *dst, hipStream_t st);
 void launch_photon_rescale(gi_photon_dev *ph, int64_t n, double pp, hipStream_t st);
+void launch_math_probe(int fn, int64_t n, const double *x, const double *y, double *out,
+                       hipStream_t st);
 void launch_intersect(const SceneView &S, int64_t n, const double *org, const double *dir,
                       int32_t *hit, double *t, double *point, double *normal, int32_t *mat,
                       hipStream_t st);

@@ -1995,6 +1995,26 @@ void launch_photon_gather(const gi_photon_dev *src, const uint32_t *slot, int64_
 void launch_photon_rescale(gi_photon_dev *ph, int64_t n, double pp, hipStream_t st) {
   if (n > 0) photon_rescale_kernel<<<nblk(n, 256), 256, 0, st>>>(ph, n, pp);
 }
+// gi_math_probe: the device's fp64 math as the path kernels call it (-ffp-contract=off build)
+__global__ void math_probe_kernel(int fn, int64_t n, const double *x, const double *y,
+                                  double *out) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double a = x[i], b = y[i], r = 0.0;
+  switch (fn) {
+    case 0: r = acos(a); break;
+    case 1: r = sin(a); break;
+    case 2: r = cos(a); break;
+    case 3: r = pow(a, b); break;
+    case 4: r = atan2(a, b); break;
+    default: r = sqrt(a); break;
+  }
+  out[i] = r;
+}
+void launch_math_probe(int fn, int64_t n, const double *x, const double *y, double *out,
+                       hipStream_t st) {
+  if (n > 0) math_probe_kernel<<<nblk(n, 256), 256, 0, st>>>(fn, n, x, y, out);
+}
 void launch_intersect(const SceneView &S, int64_t n, const double *org, const double *dir,
                       int32_t *hit, double *t, double *point, double *normal, int32_t *mat,
                       hipStream_t st) {

@@ -31,6 +31,7 @@ EXPORTED = [
     "gi_get_photon_map", "gi_get_kd_tree", "gi_set_progress", "gi_render_image", "gi_render_tiles",
     "gi_render_tiles_packed", "gi_compose_tiles", "gi_quantize",
     "gi_estimate_radiance_batch", "gi_knn_batch", "gi_knn_bench", "gi_intersect_batch",
+    "gi_math_probe",
     "gi_write_image",
 ]
 
@@ -152,6 +153,8 @@ def lib():
         L.gi_knn_bench.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p,
                                    C.c_void_p, C.c_int, C.c_int, C.c_int, P(C.c_double),
                                    P(C.c_double), P(C.c_double)]
+        L.gi_math_probe.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p,
+                                    C.c_void_p]
         L.gi_intersect_batch.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
                                          C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_void_p]
@@ -353,6 +356,19 @@ class Renderer:
                                              hit.ctypes.data, t.ctypes.data, p.ctypes.data,
                                              nr.ctypes.data, m.ctypes.data))
         return hit, t, p, nr, m
+
+
+MATH_FNS = {"acos": 0, "sin": 1, "cos": 2, "pow": 3, "atan2": 4, "sqrt": 5}
+
+
+def math_probe(renderer, fn, x, y=None):
+    """The device's fp64 acos / sin / cos / pow / atan2 / sqrt of host inputs (gi_math_probe)."""
+    x = np.ascontiguousarray(x, dtype=np.float64).ravel()
+    y = np.ascontiguousarray(np.zeros_like(x) if y is None else y, dtype=np.float64).ravel()
+    out = np.zeros_like(x)
+    renderer._check(lib().gi_math_probe(renderer._ctx, MATH_FNS[fn], len(x), x.ctypes.data,
+                                        y.ctypes.data, out.ctypes.data))
+    return out
 
 
 def write_image(path, rgb):

@@ -99,3 +99,64 @@ def test_circle_intersections_match_oracle(renderer):
     np.testing.assert_allclose(gt[both], ot[both], rtol=1e-12, atol=1e-12)
     np.testing.assert_allclose(gn[both], on[both], atol=1e-12)
     np.testing.assert_array_equal(gm[both], om[both])
+
+
+def _glibc(fn, x, y):
+    """The host C library's fp64 function (the oracle's <cmath> calls), one call per element."""
+    import ctypes as C
+    libm = C.CDLL("libm.so.6")
+    f = getattr(libm, fn)
+    two = fn in ("pow", "atan2")
+    f.argtypes = [C.c_double, C.c_double] if two else [C.c_double]
+    f.restype = C.c_double
+    if two:
+        return np.array([f(float(a), float(b)) for a, b in zip(x, y)])
+    return np.array([f(float(a)) for a in x])
+
+
+def test_device_math_differs_from_host_libm_by_one_ulp(renderer):
+    """The fork source that the small-map scene tests above allow for (their 1 % stored-count
+    and L2 tolerances): the device's fp64 acos / sin / cos / pow / atan2 (ROCm's math library)
+    and the host C library the oracle calls agree to within one ulp, but not bit for bit, on the
+    argument ranges the samplers and StorePhoton use (graphics_utils.cpp:162-216,
+    photon_utils.cpp:56-60); sqrt is correctly rounded on both sides."""
+    import gi_amd
+    rng = np.random.default_rng(11)
+    n = 20000
+    u = rng.random(n)
+    cases = {
+        "acos": (2.0 * u - 1.0, None),                    # acos(cos theta), acos(z)
+        "sin": (u * np.pi, None),                          # sin(theta), sin(alpha)
+        "cos": (u * 2.0 * np.pi, None),                    # cos(phi) of the samplers' rotation
+        "pow": (u, 1.0 / (rng.integers(1, 10000, n) + 1.0)),  # pow(r, 1 / (n + 1))
+        "atan2": (2.0 * u - 1.0, 2.0 * rng.random(n) - 1.0),  # atan2(y, x) of the direction code
+        "sqrt": (u, None),
+    }
+    differ = {}
+    for fn, (x, y) in cases.items():
+        dev = gi_amd.math_probe(renderer, fn, x, y)
+        host = _glibc(fn, x, np.zeros_like(x) if y is None else y)
+        ulp = np.abs(dev - host) / np.spacing(np.abs(host))
+        assert ulp.max() <= 1.0, (fn, float(ulp.max()))
+        differ[fn] = float((dev != host).mean())
+    print("\nfraction of inputs where device != host libm:", differ)
+    assert differ["sqrt"] == 0.0
+    assert max(v for k, v in differ.items() if k != "sqrt") > 0.0
+
+
+def test_cylinder_scene_is_exact_without_bounce_chains(renderer):
+    """cylinder.scn's full-GI comparison above needs its own loose bound (L2 RMS 3.0) because a
+    photon or indirect path leaving the infinite cylinder re-hits it at t ~ 0 (R3Isect.cpp:
+    1049-1095), so its chains run many bounces on the surface and a one-ulp libm difference
+    (test above) forks them. With the chains cut to one bounce (-pd 1: photons store at their
+    first hit and stop; -md 1: Monte Carlo paths one bounce) the same scene meets the standard
+    tolerance: the stored counts are equal and the image within L2 RMS 0.5."""
+    path = os.path.join(INP, "cylinder.scn")
+    args = [path, "/tmp/s.png", "-resolution", "24", "16", "-aa", "0", "-global", "3000",
+            "-caustic", "3000", "-it", "4", "-seed", "4", "-pd", "1", "-lt", "4", "-ss", "4",
+            "-tt", "4", "-st", "4", "-md", "1"]
+    g, gst, gp = run_gpu(renderer, args)
+    o, ost = oracle_lib.render(args, 24, 16)
+    assert gp["global_stored"] == ost["global_stored"]
+    assert gp["caustic_stored"] == ost["caustic_stored"]
+    compare(g, o, 0.99, 0.995, 0.5)

@@ -1626,20 +1626,16 @@ int gi_create_devices(gi_ctx **out, const gi_device_set *set) {
   return GI_OK;
 }
 
-void gi_destroy(gi_ctx *c) {
-  if (!c) return;
-  for (ncclComm_t m : c->comms)
-    if (m) g_rccl.commDestroy(m);
-  c->comms.clear();
-  for (gi_ctx *d : c->peers) gi_destroy(d);
-  c->peers.clear();
-  hipSetDevice(c->device);
-  DBuf *bufs[] = {&c->d_nodes, &c->d_elems, &c->d_shapes, &c->d_tris, &c->d_bvh, &c->d_mats, &c->d_lights,
-                  &c->d_lut, &c->d_stats, &c->spawn, &c->npaths, &c->path_off, &c->base,
-                  &c->pixels, &c->rgbf, &c->rgb8, &c->qcount,
-                  &c->stats_bak, &c->pcounts, &c->poffs, &c->pbuf, &c->pkeys, &c->pcursor, &c->ptmp, &c->pacc, &c->pglob, &c->ind_cont, &c->ind_ncont, &c->mc_cont, &c->mc_ncont, &c->mc_cont2, &c->mc_ncont2, &c->prim_rgb, &c->ind_tab, &c->mc_tab, &c->ind_trows, &c->ind_rows, &c->ind_masks};
+// the render's and the photon tracer's device scratch (everything but the scene, the maps, the
+// counters and the streams); the next call re-allocates what it needs
+static void release_scratch(gi_ctx *c) {
+  DBuf *bufs[] = {&c->spawn, &c->npaths, &c->path_off, &c->nmc, &c->mc_off, &c->nind,
+                  &c->ind_off, &c->base, &c->pixels, &c->rgbf, &c->rgb8, &c->stats_bak,
+                  &c->pcounts, &c->poffs, &c->pbuf, &c->pkeys, &c->pcursor, &c->ptmp, &c->pacc,
+                  &c->pglob, &c->ind_cont, &c->ind_ncont, &c->mc_cont, &c->mc_ncont,
+                  &c->mc_cont2, &c->mc_ncont2, &c->prim_rgb, &c->ind_tab, &c->mc_tab,
+                  &c->ind_trows, &c->ind_rows, &c->ind_masks, &c->pack};
   for (DBuf *b : bufs) b->release();
-  c->pack.release();
   for (auto &b : c->recv) b.release();
   for (auto &b : c->peer_pix) b.release();
   for (int m = 0; m < 2; m++) {
@@ -1648,25 +1644,56 @@ void gi_destroy(gi_ctx *c) {
                   &X.fb_dense, &X.fb_list2, &X.fb_count2, &X.fb_dense2, &X.dk_q};
     for (DBuf *b : xb) b->release();
     sort_scratch_release(X.sorter);
+  }
+  for (int l = 0; l < 2; l++) {
+    c->qpos[l].release(); c->qshade[l].release(); c->qkey[l].release(); c->qout[l].release();
+    c->qseg[l].release();
+    sort_scratch_release(c->keysort[l]);
+  }
+  sort_scratch_release(c->psort);
+  for (int l = 0; l < 8; l++) { c->scan_lvl[l].release(); c->scan_out[l].release(); }
+  c->kdb.release();
+  c->kd_ph.release();
+}
+
+int gi_release_scratch(gi_ctx *c) {
+  if (!c) return GI_ERR_ARG;
+  for (gi_ctx *d : c->peers) {
+    hipSetDevice(d->device);
+    hipDeviceSynchronize();
+    release_scratch(d);
+  }
+  hipSetDevice(c->device);
+  hipDeviceSynchronize();
+  release_scratch(c);
+  return GI_OK;
+}
+
+void gi_destroy(gi_ctx *c) {
+  if (!c) return;
+  for (ncclComm_t m : c->comms)
+    if (m) g_rccl.commDestroy(m);
+  c->comms.clear();
+  for (gi_ctx *d : c->peers) gi_destroy(d);
+  c->peers.clear();
+  hipSetDevice(c->device);
+  release_scratch(c);
+  DBuf *bufs[] = {&c->d_nodes, &c->d_elems, &c->d_shapes, &c->d_tris, &c->d_bvh, &c->d_mats,
+                  &c->d_lights, &c->d_lut, &c->d_stats, &c->qcount};
+  for (DBuf *b : bufs) b->release();
+  for (int m = 0; m < 2; m++) {
+    MapExec &X = c->mx[m];
     if (X.ev0) hipEventDestroy(X.ev0);
     if (X.ev1) hipEventDestroy(X.ev1);
     if (X.ev2) hipEventDestroy(X.ev2);
     if (X.ev3) hipEventDestroy(X.ev3);
   }
-  for (int l = 0; l < 2; l++) {
-    c->qpos[l].release(); c->qshade[l].release(); c->qkey[l].release(); c->qout[l].release();
-    sort_scratch_release(c->keysort[l]);
-  }
-  sort_scratch_release(c->psort);
-  for (int l = 0; l < 8; l++) { c->scan_lvl[l].release(); c->scan_out[l].release(); }
   for (int m = 0; m < 2; m++) {
     c->dmap[m].pos4.release();
     c->dmap[m].rgbe.release();
     c->dmap[m].nodes.release();
     c->dmap[m].dk.release();
   }
-  c->kdb.release();
-  c->kd_ph.release();
   if (c->ev_fork) hipEventDestroy(c->ev_fork);
   if (c->ev_join) hipEventDestroy(c->ev_join);
   if (c->stream2) hipStreamDestroy(c->stream2);

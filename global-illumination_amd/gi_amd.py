@@ -31,7 +31,7 @@ EXPORTED = [
     "gi_get_photon_map", "gi_get_kd_tree", "gi_set_progress", "gi_render_image", "gi_render_tiles",
     "gi_render_tiles_packed", "gi_compose_tiles", "gi_quantize",
     "gi_estimate_radiance_batch", "gi_knn_batch", "gi_knn_bench", "gi_intersect_batch",
-    "gi_math_probe",
+    "gi_math_probe", "gi_release_scratch",
     "gi_write_image",
 ]
 
@@ -153,6 +153,7 @@ def lib():
         L.gi_knn_bench.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p,
                                    C.c_void_p, C.c_int, C.c_int, C.c_int, P(C.c_double),
                                    P(C.c_double), P(C.c_double)]
+        L.gi_release_scratch.argtypes = [C.c_void_p]
         L.gi_math_probe.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p,
                                     C.c_void_p]
         L.gi_intersect_batch.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
@@ -209,6 +210,10 @@ class Renderer:
                 raise GiError(f"gi_create failed (rc={rc}): no usable HIP device {device}")
         self.params = params if params is not None else default_params()
         self._check(lib().gi_set_params(self._ctx, C.byref(self.params)))
+
+    def release_scratch(self):
+        """Free the device scratch of renders and map builds; scene and maps stay resident."""
+        self._check(lib().gi_release_scratch(self._ctx))
 
     def close(self):
         if self._ctx:

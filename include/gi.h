@@ -257,6 +257,12 @@ int gi_intersect_batch(gi_ctx *ctx, int64_t n, const double *org, const double *
  * the device's results with the host C library's one for one. */
 int gi_math_probe(gi_ctx *ctx, int fn, int64_t n, const double *x, const double *y, double *out);
 
+/* Free the context's render and photon-tracing device scratch (all devices of a device set),
+ * keeping the scene, the photon maps and their kd trees; the next render or map build
+ * re-allocates what it needs. For a long-lived context that must share the GPU with another
+ * large one. No reference counterpart (the reference's buffers are host memory). */
+int gi_release_scratch(gi_ctx *ctx);
+
 /* ---- output --------------------------------------------------------------------------- */
 int gi_write_image(const char *path, int width, int height, const uint8_t *rgb8);
 

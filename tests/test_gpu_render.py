@@ -258,11 +258,16 @@ def test_c2_config_matches_oracle(renderer):
     compare(g, o, 0.99, 0.995, 0.5)
 
 
-def test_c2_full_frame_properties():
+def test_c2_full_frame_properties(renderer):
     """The full C2 frame (1024^2, aa 2, 1M + 1M photons): finite and clamped to [0, 1] per pixel
     (render.cpp:236-249), the same image twice over the resident maps, and the same image from
-    a two-entry device set on one GPU (tiles dealt over the set and gathered, render.cpp:90)."""
+    a two-entry device set on one GPU (tiles dealt over the set and gathered, render.cpp:90).
+    Three C2-sized contexts share the card over the test, so the session renderer's scratch
+    from earlier tests is released first (gi_release_scratch)."""
+    import gc
     import hashlib
+    gc.collect()
+    renderer.release_scratch()
     args = [scene("cornell.scn"), "/tmp/x.png", "-resolution", "1024", "1024", "-aa", "2",
             "-seed", "1"] + C2_MAPS
     p, sc, _o, w, h, aa, real = gi_amd.ParseArgs(args)

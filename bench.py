@@ -66,7 +66,7 @@ def parse():
 
 def shard_balance(a):
     """Shard balance of an N-GPU frame measured on one GPU (render.cpp:90's interleave re-cut as
-    16x16 tiles, tile t on GPU t % N): each shard rendered `steps` times after one warmup render of
+    16x16 tiles, tile (tx, ty) on GPU (tx + ty) % N): each shard rendered `steps` times after one warmup render of
     shard 0 (buffer growth), its time the median. Prints one JSON line."""
     import torch
     import gi_amd
@@ -102,7 +102,7 @@ def shard_balance(a):
             "config": {"workload": f"{a.scene} {w}x{h} aa={aa} "
                                    f"{a.global_photons}+{a.caustic_photons} photons {a.extra}".strip(),
                        "tile": a.tile, "nshards": N, "photon_map_s": round(photon_s, 3),
-                       "assignment": f"tile t -> shard t % {N}"},
+                       "assignment": f"tile (tx, ty) -> shard (tx + ty) % {N}"},
             "shard_ms": [round(t * 1e3, 1) for t in times], "shard_pixels": npix,
             "min_ms": round(min(times) * 1e3, 1), "mean_ms": round(mean * 1e3, 1),
             "max_ms": round(max(times) * 1e3, 1), "max_over_mean": round(max(times) / mean, 4),

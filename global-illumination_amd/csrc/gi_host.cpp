@@ -2010,12 +2010,16 @@ static int render_common(gi_ctx *c, int aa, int w, int h, const std::vector<int3
   return GI_OK;
 }
 
-// output pixels of tiles t (tile x tile, row-major tile id) with t % nshards == shard
+// output pixels of the tiles (tile x tile, row-major tile id t = ty * tx + tx_i) that shard owns:
+// tile (tx_i, ty_i) goes to shard (tx_i + ty_i) % nshards, a diagonal deal, so every run of
+// nshards tiles along a row or a column meets every shard (t % nshards with tx a multiple of
+// nshards deals whole tile columns, and a compact expensive region -- the glass sphere -- then
+// lands on a few shards in proportion to the columns it spans)
 static std::vector<int32_t> shard_pixels(int w, int h, int tile, int shard, int nshards) {
   int tx = (w + tile - 1) / tile, ty = (h + tile - 1) / tile;
   std::vector<int32_t> pix;
   for (int t = 0; t < tx * ty; t++) {
-    if (t % nshards != shard) continue;
+    if (((t % tx) + (t / tx)) % nshards != shard) continue;
     int x0 = (t % tx) * tile, y0 = (t / tx) * tile;
     for (int y = y0; y < std::min(h, y0 + tile); y++)
       for (int x = x0; x < std::min(w, x0 + tile); x++) {
@@ -2026,8 +2030,9 @@ static std::vector<int32_t> shard_pixels(int w, int h, int tile, int shard, int 
   return pix;
 }
 
-// RenderImage on a device set: device k renders the 16x16 output tiles
-// t % ndev == k (the reference's column interleave, render.cpp:90, re-cut as tiles), packs its
+// RenderImage on a device set: device k renders the 16x16 output tiles of
+// shard k (shard_pixels: the reference's column interleave, render.cpp:90, re-cut as diagonally
+// dealt tiles), packs its
 // pixels (16 B each) and sends them to the first device: ncclSend / ncclRecv in one group over
 // xGMI when the devices are distinct (each peer's stream feeds its own link into device 0), a
 // peer copy otherwise. Device 0 scatters them into the image; nothing else is exchanged.

@@ -1,8 +1,11 @@
 """Multi-GPU image-tile sharding for RenderImage (one process per GPU, torchrun).
 
 The reference's render threads each take the column interleave i % THREADS
-(render.cpp:90). Here the frame is cut into tile x tile output-pixel tiles instead, and rank r
-renders tiles t with t % world == r. Tile t sits at ((t % ntx) * tile, (t // ntx) * tile).
+(render.cpp:90). Here the frame is cut into tile x tile output-pixel tiles instead, dealt
+diagonally: tile (tx, ty) goes to rank (tx + ty) % world, so every run of `world` tiles along a
+row or a column meets every rank (a plain t % world deals whole tile columns when the row's tile
+count is a multiple of world, and the glass sphere's expensive tiles then fall on few ranks).
+Tile t sits at ((t % ntx) * tile, (t // ntx) * tile).
 There is no other communication: every rank builds the identical photon maps from the same
 seed, and each rank sends only its own pixels to rank 0 in one gather.
 
@@ -23,8 +26,7 @@ def tile_owner_map(width, height, tile, world):
     """[height, width] int array: the rank that renders each output pixel."""
     ntx = (width + tile - 1) // tile
     ys, xs = np.mgrid[0:height, 0:width]
-    t = (ys // tile) * ntx + (xs // tile)
-    return (t % world).astype(np.int32)
+    return (((ys // tile) + (xs // tile)) % world).astype(np.int32)
 
 
 def shard_pixel_list(width, height, tile, shard, world):
@@ -32,7 +34,9 @@ def shard_pixel_list(width, height, tile, shard, world):
     rows then columns inside a tile."""
     ntx, nty = (width + tile - 1) // tile, (height + tile - 1) // tile
     out = []
-    for t in range(shard, ntx * nty, world):
+    for t in range(ntx * nty):
+        if (t % ntx + t // ntx) % world != shard:
+            continue
         x0, y0 = (t % ntx) * tile, (t // ntx) * tile
         for y in range(y0, min(height, y0 + tile)):
             for x in range(x0, min(width, x0 + tile)):

@@ -173,7 +173,7 @@ int gi_create(gi_ctx **out, int hip_device);
  * gi_device_set*); render.cpp:90's thread interleave re-cut as a device shard). Every call on
  * it drives all of them: the scene and photon maps are replicated (photon emission ranges are
  * split across the devices, the maps built once), gi_render_image deals 16x16 output tiles
- * t % count to device t and gathers the tiles onto devices[0] (RCCL send/recv over xGMI when the
+ * (tx, ty) to device (tx + ty) % count and gathers the tiles onto devices[0] (RCCL send/recv over xGMI when the
  * devices are distinct, else a peer copy). Test seams (gi_*_batch) run on devices[0]. */
 #define GI_MAX_DEVICES 64
 typedef struct gi_device_set {
@@ -212,8 +212,9 @@ int gi_get_kd_tree(gi_ctx *ctx, int map, float *nodes, int64_t node_floats, int3
  * rgbf (optional) receives the clamped box-filtered colour in [0,1]. */
 int gi_render_image(gi_ctx *ctx, int aa, int width, int height, uint8_t *rgb8, float *rgbf,
                     gi_render_stats *stats);
-/* Shard: render only output tiles t (tile_px x tile_px pixels, row-major tile id) with
- * t % nshards == shard; rgbf is the full W*H*3 image, untouched outside the shard. */
+/* Shard: render only the output tiles (tile_px x tile_px pixels; tile column tx, row ty) with
+ * (tx + ty) % nshards == shard (a diagonal deal: every run of nshards tiles along a row or a
+ * column meets every shard), packed shards in row-major tile order; rgbf is the full W*H*3 image, untouched outside the shard. */
 int gi_render_tiles(gi_ctx *ctx, int aa, int width, int height, int tile_px, int shard,
                     int nshards, float *rgbf, gi_render_stats *stats);
 /* Shard left on the device (one-process-per-GPU ranks, e.g. torchrun): renders the same tiles

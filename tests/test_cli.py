@@ -108,7 +108,7 @@ def test_cli_render_matches_oracle_cli(tmp_path):
 @pytest.mark.gpu
 def test_cli_device_set_matches_one_device(tmp_path):
     """`-gpus N` (extension flag) runs the drop-in over a device set; GI_DEVICES=0,0 lets one GPU
-    stand in for two (tiles t % 2, gathered by peer copy). The PNG equals the one-device PNG."""
+    stand in for two (tiles dealt (tx + ty) % 2, gathered by peer copy). The PNG equals the one-device PNG."""
     flags = ["-resolution", "40", "24", "-aa", "1", "-global", "20000", "-caustic", "20000",
              "-it", "8", "-tt", "8", "-st", "8"]
     scn = os.path.join(SCENES, "cornell.scn")

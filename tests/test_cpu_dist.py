@@ -138,8 +138,15 @@ def test_shard_pixel_list_matches_owner_map():
     assert np.all(seen == 1)
 
 
-def test_tile_owner_map_round_robin():
+def test_tile_owner_map_diagonal():
     m = gi_dist.tile_owner_map(40, 20, 16, 2)
-    # 3 x 2 tiles, ids row-major, owner = id % 2
+    # 3 x 2 tiles, owner = (tile x + tile y) % 2
     assert m[0, 0] == 0 and m[0, 16] == 1 and m[0, 32] == 0
     assert m[16, 0] == 1 and m[16, 16] == 0 and m[16, 39] == 1
+    # 64 tiles per row (C2's 1024^2 in 16^2 tiles) on 8 ranks: every run of 8 tiles along a row
+    # or a column meets all 8 ranks (t % 8 would give each rank whole tile columns)
+    m = gi_dist.tile_owner_map(1024, 1024, 16, 8)[::16, ::16]
+    for k in range(0, 64, 8):
+        assert sorted(m[5, k:k + 8]) == list(range(8))
+        assert sorted(m[k:k + 8, 7]) == list(range(8))
+    assert np.bincount(m.ravel()).tolist() == [512] * 8

@@ -285,7 +285,7 @@ def test_mesh_bvh_matches_linear_loop(renderer, kind, scn, off):
 ])
 def test_device_set_matches_one_device(devices, name, extra):
     """gi_create_devices: photon emission split across the set, maps replicated, 16x16 tiles
-    dealt t % ndev and gathered onto the first device. On one GPU the set repeats device 0 (the
+    dealt (tx + ty) % ndev and gathered onto the first device. On one GPU the set repeats device 0 (the
     gather is then a peer copy; distinct devices use RCCL send/recv): the image, the f32 frame,
     the photon maps and every -v counter equal the single-device render's."""
     args = [scene(name), "/tmp/x.png", "-resolution", "40", "24", "-aa", "1", "-tt", "8",

@@ -576,7 +576,9 @@ __device__ __forceinline__ int scene_intersect_b(const SceneView &S, V org, V di
       if (!isZero(lv - 1.0)) scale *= lv;
     }
     if (!ok) continue;
-    const V linv = mk(1.0 / ldir.x, 1.0 / ldir.y, 1.0 / ldir.z);
+    // the pretest's slab reciprocals only when it runs (a wave-uniform flag: hard-light scenes
+    // skip three fp64 divisions per node and ray)
+    const V linv = S.elem_pretest ? mk(1.0 / ldir.x, 1.0 / ldir.y, 1.0 / ldir.z) : mk(0, 0, 0);
     for (int ei = 0; ei < nd.elem_count; ei++) {
       const int gei = nd.elem_first + ei;
       if (gei < 64 && !((emask >> gei) & 1ull)) continue;

@@ -1849,16 +1849,22 @@ void launch_path(const RenderArgs &a, hipStream_t st, hipStream_t st2, hipEvent_
                  hipEvent_t join) {
   const bool side = st2 && fork && join && a.total_mc > 0;
   hipStream_t ms = side ? st2 : st;
+  // the Monte Carlo queues' counters are zeroed on st before the fork: a fill on the side stream
+  // waits for a CU slot behind st's kernels (rocprof: single fills of 42 ms at C2 and 170 ms
+  // at C3 with the persistent kernel), and the side stream's kernels wait behind it
+  if (a.total_mc > 0 && a.mc_cont) {
+    (void)hipMemsetAsync(a.mc_ncont, 0, IND_QS * 32 * sizeof(uint32_t), st);
+    if (a.mc_next) (void)hipMemsetAsync(a.mc_next, 0, sizeof(uint32_t), st);
+    if (a.mc_cont2) (void)hipMemsetAsync(a.mc_ncont2, 0, IND_QS * 32 * sizeof(uint32_t), st);
+  }
   if (side) {
     (void)hipEventRecord(fork, st);
     (void)hipStreamWaitEvent(st2, fork, 0);
   }
   if (a.total_mc > 0) {
     unsigned g = nblk(a.total_mc, 128);
-    if (a.mc_cont) (void)hipMemsetAsync(a.mc_ncont, 0, IND_QS * 32 * sizeof(uint32_t), ms);
     if (a.mc_cont && a.mc_next) {
       // persistent: enough blocks to fill the chip at MC_WPE waves per SIMD, or one per 128 paths
-      (void)hipMemsetAsync(a.mc_next, 0, sizeof(uint32_t), ms);
       unsigned gp = std::min(g, (unsigned)(a.mc_persist_blocks > 0 ? a.mc_persist_blocks : 1024));
       if ((a.S.kinds & ~KINDS_TRI_SPHERE) == 0) {
         if (a.S.hard_lights) mc_persist_kernel<KINDS_TRI_SPHERE, true, true><<<gp, 128, 0, ms>>>(a);
@@ -1882,7 +1888,6 @@ void launch_path(const RenderArgs &a, hipStream_t st, hipStream_t st2, hipEvent_
     }
     if (a.mc_cont) {
       if (a.mc_cont2) {
-        (void)hipMemsetAsync(a.mc_ncont2, 0, IND_QS * 32 * sizeof(uint32_t), ms);
         launch_mc_sub(a, ms);
         launch_cont(a, a.mc_cont2, a.mc_ncont2, a.mc_cap_s, ms);
       } else {

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "gi_layout.h"
+#include "gi_math.h"  // sin / cos / tan / asin / acos / atan2 / pow shared with the oracle
 
 namespace gi {
 
@@ -651,8 +652,8 @@ __device__ __forceinline__ bool scene_intersect(const SceneView &S, V org, V dir
 // Optics and sampling (utils/graphics_utils.cpp)
 // ---------------------------------------------------------------------------------------
 GI_HD double reflection_coeff(double ir_air, double cos_theta, double ir_mat) {  // :95-101
-  double r0 = pow((ir_air - ir_mat) / (ir_air + ir_mat), 2.0);
-  return (r0 + (1.0 - r0) * pow((1.0 - fabs(cos_theta)), 5.0));
+  double r0 = gm::pow((ir_air - ir_mat) / (ir_air + ir_mat), 2.0);
+  return (r0 + (1.0 - r0) * gm::pow((1.0 - fabs(cos_theta)), 5.0));
 }
 GI_HD V reflective_bounce(V n, V view, double ct) {  // :104-117
   if (ct < 0) { n = -n; ct *= -1.0; }
@@ -669,42 +670,42 @@ GI_HD V transmissive_bounce(double ir_air, V n, V view, double ct, double ir_mat
   } else {
     eta = ir_air / ir_mat;
   }
-  double theta = acos(ct);
-  double sin_phi = eta * sin(theta);
+  double theta = gm::acos(ct);
+  double sin_phi = eta * gm::sin(theta);
   if (sin_phi < -1.0 || 1.0 < sin_phi) return reflective_bounce(n, view, ct);
-  double phi = asin(sin_phi);
+  double phi = gm::asin(sin_phi);
   V par = normalize(view + n * ct);
-  V refr = par * tan(phi) - n;
+  V refr = par * gm::tan(phi) - n;
   return normalize(refr);
 }
 GI_HD V rotate(V v, V axis, double theta) {  // R3Vector::Rotate, R3Vector.cpp:352-363
-  double ct = cos(theta);
+  double ct = gm::cos(theta);
   double d = dot(v, axis);
   V cr = cross(v, axis);
   v = v * ct;
   v = v + axis * d * (1.0 - ct);
-  v = v - cr * sin(theta);
+  v = v - cr * gm::sin(theta);
   return v;
 }
 GI_HD V diffuse_sample(V n, double ct, Rng &rng) {  // Diffuse_ImportanceSample :162-185
   if (ct < 0) n = -n;
-  double theta = acos(sqrt(rng.next()));
+  double theta = gm::acos(sqrt(rng.next()));
   double phi = 2 * kPi * rng.next();
   V perp = mk(n.y, -n.x, 0);
   if (1.0 - fabs(n.z) < 0.1) perp = mk(n.z, 0, -n.x);
   perp = normalize(perp);
-  V r = perp * sin(theta) + n * cos(theta);
+  V r = perp * gm::sin(theta) + n * gm::cos(theta);
   r = rotate(r, n, phi);
   return normalize(r);
 }
 GI_HD V specular_sample(V ex, double nsh, double ct, Rng &rng) {  // :189-216
-  double lim = (1.0 - acos(fabs(ct)) * 2.0 / kPi);
-  double alpha = acos(pow(rng.next(), 1.0 / (nsh + 1.0))) * lim;
+  double lim = (1.0 - gm::acos(fabs(ct)) * 2.0 / kPi);
+  double alpha = gm::acos(gm::pow(rng.next(), 1.0 / (nsh + 1.0))) * lim;
   double phi = 2.0 * kPi * rng.next();
   V perp = mk(ex.y, -ex.x, 0);
   if (1.0 - fabs(ex.z) < 0.1) perp = mk(ex.z, 0, -ex.x);
   perp = normalize(perp);
-  V r = perp * sin(alpha) + ex * cos(alpha);
+  V r = perp * gm::sin(alpha) + ex * gm::cos(alpha);
   r = rotate(r, ex, phi);
   return normalize(r);
 }
@@ -880,7 +881,7 @@ __device__ __noinline__ void soft_light(const SceneView &S, const DLight &L, C3 
         V R = (2.0 * NL) * nrm - Ld;
         double VR = dot(Vv, R);
         if (isNegOrZero(VR)) continue;
-        w += (I * pow(VR, m.n));
+        w += (I * gm::pow(VR, m.n));
       }
     }
     if (hits > 0) color += w * ldc(m.ks) * ldc(L.color) * L.area / (double)hits;
@@ -915,8 +916,8 @@ __device__ __forceinline__ C3 light_reflection_hard(const DLight &L, const DMate
     if (L.kind == LK_SPOT) {
       V ML = normalize(p - lp);
       double ca = dot(ML, ld3(L.dir));
-      if (cos(L.cutoff) > ca) I = 0.0;
-      else I = I * pow(ca, L.dropoff);
+      if (gm::cos(L.cutoff) > ca) I = 0.0;
+      else I = I * gm::pow(ca, L.dropoff);
     }
     V Ld = normalize(lp - p);
     double NL = dot(nrm, Ld);
@@ -924,7 +925,7 @@ __device__ __forceinline__ C3 light_reflection_hard(const DLight &L, const DMate
     V Vv = normalize(eye - p);
     double VR = dot(Vv, R);
     C3 o = I * Dc * Ic * fabs(NL);
-    if (isPos(VR)) o += (I * pow(VR, s)) * Sc * Ic;
+    if (isPos(VR)) o += (I * gm::pow(VR, s)) * Sc * Ic;
     return o;
   }
   if (L.kind == LK_DIR) {
@@ -935,7 +936,7 @@ __device__ __forceinline__ C3 light_reflection_hard(const DLight &L, const DMate
     V Vv = normalize(eye - p);
     double VR = dot(Vv, R);
     C3 o = (I * fabs(NL)) * Dc * Ic;
-    if (isPos(VR)) o += (I * pow(VR, s) * Sc * Ic);
+    if (isPos(VR)) o += (I * gm::pow(VR, s) * Sc * Ic);
     return o;
   }
   return rgb(0, 0, 0);
@@ -988,7 +989,7 @@ __device__ __noinline__ C3 light_reflection(const DLight &L, const DMaterial &m,
         V Vv = normalize(eye - p);
         double VR = dot(Vv, R);
         if (isNegOrZero(VR)) continue;
-        sum += (I * pow(VR, s) * Sc * Ic);
+        sum += (I * gm::pow(VR, s) * Sc * Ic);
       }
     }
     C3 mean = sum;

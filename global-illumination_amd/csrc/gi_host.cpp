@@ -2387,7 +2387,7 @@ int gi_knn_bench(gi_ctx *c, int map, int64_t n, const double *pts, const double 
 }
 
 int gi_math_probe(gi_ctx *c, int fn, int64_t n, const double *x, const double *y, double *out) {
-  if (!c || n < 0 || fn < 0 || fn > 5 || (n > 0 && (!x || !y || !out))) return GI_ERR_ARG;
+  if (!c || n < 0 || fn < 0 || fn > 7 || (n > 0 && (!x || !y || !out))) return GI_ERR_ARG;
   if (n == 0) return GI_OK;
   hipSetDevice(c->device);
   DBuf dx, dy, dout;

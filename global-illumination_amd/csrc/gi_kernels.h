@@ -201,7 +201,7 @@ __device__ __forceinline__ bool kd_next(const KdNode *nodes, int &node, float qx
 
 // pow behind a call: the estimates' specular and Gaussian-filter branches would otherwise inline
 // one fp64 pow per unrolled photon (code size, registers) for paths most scenes never take
-static __device__ __noinline__ double pow_call(double x, double y) { return pow(x, y); }
+static __device__ __noinline__ double pow_call(double x, double y) { return gm::pow(x, y); }
 
 // d-ary max-heap of u64 keys in LDS laid out [slot][lane] (stride 64): sift-down, Floyd build,
 // and accept (append unordered until K, heapify once, then replace the root)

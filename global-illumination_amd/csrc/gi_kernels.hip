@@ -1241,7 +1241,7 @@ __global__ __launch_bounds__(64) void knn_kernel(KnnArgs a) {
           double c1 = 1.0, c2 = 1.0, tot_w = 0;
           if (a.filter == 1) c1 = 1.0 / (a.fk * sqrt(maxd2));
           else if (a.filter == 2) {
-            c1 = pow(2.7182818284590452354, -a.fb);
+            c1 = gm::pow(2.7182818284590452354, -a.fb);
             c2 = 1.0 / (2.0 * maxd2);
           }
           for (int s = 0; s < num; s++) {
@@ -1259,7 +1259,7 @@ __global__ __launch_bounds__(64) void knn_kernel(KnnArgs a) {
             double ca = E0 * -ix + E1 * -iy + E2 * -iz;
             if (ca < 0) ca = 0;
             double ap = fabs(perp);
-            double pw = spec ? pow(ca, m.n) : 0.0;
+            double pw = spec ? gm::pow(ca, m.n) : 0.0;
             p0 *= ap * m.kd[0] + pw * m.ks[0];
             p1 *= ap * m.kd[1] + pw * m.ks[1];
             p2 *= ap * m.kd[2] + pw * m.ks[2];
@@ -1267,7 +1267,7 @@ __global__ __launch_bounds__(64) void knn_kernel(KnnArgs a) {
               double f = (1.0 - c1 * sqrt((double)h.d2[s * h.stride]));
               p0 *= f; p1 *= f; p2 *= f;
             } else if (a.filter == 2) {
-              double w = (1.0 - (1.0 - pow(c1, c2 * (double)h.d2[s * h.stride])) / (1.0 - c1));
+              double w = (1.0 - (1.0 - gm::pow(c1, c2 * (double)h.d2[s * h.stride])) / (1.0 - c1));
               p0 *= w; p1 *= w; p2 *= w;
               tot_w += w;
             }
@@ -1375,7 +1375,7 @@ __global__ __launch_bounds__(64) void cached_kernel(KnnArgs a) {
       double ca = sh.ex[0] * -ix + sh.ex[1] * -iy + sh.ex[2] * -iz;
       if (ca < 0) ca = 0;
       double ap = fabs(perp);
-      double pw = pow(ca, m.n);
+      double pw = gm::pow(ca, m.n);
       p0 *= ap * m.kd[0] + pw * m.ks[0];
       p1 *= ap * m.kd[1] + pw * m.ks[1];
       p2 *= ap * m.kd[2] + pw * m.ks[2];
@@ -1590,9 +1590,9 @@ __device__ __forceinline__ void store_photon(int mode, PhotonOut &o, C3 power, V
     ph.pos[1] = (float)p.y;
     ph.pos[2] = (float)p.z;
     ph.rgbe = rgbe_encode(power);
-    int phi = (uint8_t)(255.0 * (atan2(inc.y, inc.x) + kPi) / (2.0 * kPi));
+    int phi = (uint8_t)(255.0 * (gm::atan2(inc.y, inc.x) + kPi) / (2.0 * kPi));
     double z = inc.z < -1.0 ? -1.0 : (inc.z > 1.0 ? 1.0 : inc.z);
-    int theta = (uint8_t)(255.0 * acos(z) / kPi);
+    int theta = (uint8_t)(255.0 * gm::acos(z) / kPi);
     ph.dir = (uint16_t)(phi * 256 + theta);
     ph.flags = 0;
     if (mode == PM_EMIT) {
@@ -1700,7 +1700,7 @@ __global__ __launch_bounds__(128) void photon_kernel(PhotonArgs a) {
     dir = normalize(mk(x, y, z));
   } else if (L.kind == LK_SPOT) {
     V ln = ld3(L.dir);
-    double cutoff = fabs(cos(L.cutoff));
+    double cutoff = fabs(gm::cos(L.cutoff));
     int attempts_left = 20;
     V sd;
     do {
@@ -2000,18 +2000,21 @@ void launch_photon_gather(const gi_photon_dev *src, const uint32_t *slot, int64_
 void launch_photon_rescale(gi_photon_dev *ph, int64_t n, double pp, hipStream_t st) {
   if (n > 0) photon_rescale_kernel<<<nblk(n, 256), 256, 0, st>>>(ph, n, pp);
 }
-// gi_math_probe: the device's fp64 math as the path kernels call it (-ffp-contract=off build)
+// gi_math_probe: the device's fp64 math as the path kernels call it (gi_math.h; sqrt: the
+// correctly rounded hardware sequence)
 __global__ void math_probe_kernel(int fn, int64_t n, const double *x, const double *y,
                                   double *out) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   double a = x[i], b = y[i], r = 0.0;
   switch (fn) {
-    case 0: r = acos(a); break;
-    case 1: r = sin(a); break;
-    case 2: r = cos(a); break;
-    case 3: r = pow(a, b); break;
-    case 4: r = atan2(a, b); break;
+    case 0: r = gm::acos(a); break;
+    case 1: r = gm::sin(a); break;
+    case 2: r = gm::cos(a); break;
+    case 3: r = gm::pow(a, b); break;
+    case 4: r = gm::atan2(a, b); break;
+    case 6: r = gm::tan(a); break;
+    case 7: r = gm::asin(a); break;
     default: r = sqrt(a); break;
   }
   out[i] = r;

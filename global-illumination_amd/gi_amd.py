@@ -363,7 +363,7 @@ class Renderer:
         return hit, t, p, nr, m
 
 
-MATH_FNS = {"acos": 0, "sin": 1, "cos": 2, "pow": 3, "atan2": 4, "sqrt": 5}
+MATH_FNS = {"acos": 0, "sin": 1, "cos": 2, "pow": 3, "atan2": 4, "sqrt": 5, "tan": 6, "asin": 7}
 
 
 def math_probe(renderer, fn, x, y=None):

@@ -253,9 +253,10 @@ int gi_knn_bench(gi_ctx *ctx, int map, int64_t n, const double *points, const do
 int gi_intersect_batch(gi_ctx *ctx, int64_t n, const double *org, const double *dir,
                        int32_t *hit, double *t, double *point, double *normal, int32_t *material);
 /* Test seam: the device's fp64 math on host inputs, fn = 0 acos(x), 1 sin(x), 2 cos(x),
- * 3 pow(x, y), 4 atan2(x, y), 5 sqrt(x) (y ignored except by 3 and 4): the functions the photon
- * tracer and samplers call (graphics_utils.cpp:95-216, photon_utils.cpp:56-60), for comparing
- * the device's results with the host C library's one for one. */
+ * 3 pow(x, y), 4 atan2(x, y), 5 sqrt(x), 6 tan(x), 7 asin(x) (y ignored except by 3 and 4): the
+ * functions the photon tracer, samplers and Phong terms call (graphics_utils.cpp:95-216,
+ * photon_utils.cpp:56-60), gi_math.h's sequences, for comparing the device's results with the
+ * oracle's (the same sequences on the host) and the host C library's one for one. */
 int gi_math_probe(gi_ctx *ctx, int fn, int64_t n, const double *x, const double *y, double *out);
 
 /* Free the context's render and photon-tracing device scratch (all devices of a device set),

@@ -9,9 +9,15 @@
 //   - photon emission runs as ONE emitter (the reference splits quotas per CPU thread,
 //     photonmap.cpp:294-329); photons are stored in emission order;
 //   - kd-tree pivots are deterministic (reference: random quickselect R3Kdtree.cpp:1563);
-//   - Q8 (EstimateCachedRadiance null dereference) is guarded: no photon -> no contribution.
+//   - Q8 (EstimateCachedRadiance null dereference) is guarded: no photon -> no contribution;
+//   - the transcendentals the device evaluates (samplers, Fresnel / Phong pow, photon direction
+//     codes) are gi_math.h's fp64 sequences, shared with the device, not the C library's: within
+//     1-2 ulp of glibc (tests/test_cpu_math.py), as the reference built on another C library
+//     would be; host-side setup (light power, camera, direction LUT) keeps the C library.
 #include "oracle_scene.h"
 #include "../include/gi.h"
+// the fp64 transcendentals the device evaluates (shared operation sequence: same bits as the GPU)
+#include "../global-illumination_amd/csrc/gi_math.h"
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -251,8 +257,8 @@ static bool intersect(const Ctx &c, V3 org, V3 dir, Hit &h);
 
 // Schlick, :95-101
 static double reflection_coeff(double ir_air, double cos_theta, double ir_mat) {
-  double r0 = pow((ir_air - ir_mat) / (ir_air + ir_mat), 2);
-  return (r0 + (1.0 - r0) * pow((1.0 - fabs(cos_theta)), 5));
+  double r0 = gm::pow((ir_air - ir_mat) / (ir_air + ir_mat), 2);
+  return (r0 + (1.0 - r0) * gm::pow((1.0 - fabs(cos_theta)), 5));
 }
 // ReflectiveBounce, :104-117
 static V3 reflective_bounce(V3 normal, V3 view, double cos_theta) {
@@ -271,45 +277,45 @@ static V3 transmissive_bounce(double ir_air, V3 normal, V3 view, double cos_thet
   } else {
     eta = ir_air / ir_mat;
   }
-  double theta = acos(cos_theta);
-  double sin_phi = eta * sin(theta);
+  double theta = gm::acos(cos_theta);
+  double sin_phi = eta * gm::sin(theta);
   if (sin_phi < -1.0 || 1.0 < sin_phi) return reflective_bounce(normal, view, cos_theta);
-  double phi = asin(sin_phi);
+  double phi = gm::asin(sin_phi);
   V3 par = normalize(view + normal * cos_theta);
-  V3 refr = par * tan(phi) - normal;
+  V3 refr = par * gm::tan(phi) - normal;
   return normalize(refr);
 }
 // R3Vector::Rotate (Goldstein), R3Vector.cpp:352-363
 static V3 rotate(V3 v, V3 axis, double theta) {
-  double ct = cos(theta);
+  double ct = gm::cos(theta);
   double d = dot(v, axis);
   V3 cr = cross(v, axis);
   v = v * ct;
   v = v + axis * d * (1.0 - ct);
-  v = v - cr * sin(theta);
+  v = v - cr * gm::sin(theta);
   return v;
 }
 // Diffuse_ImportanceSample, :162-185
 static V3 diffuse_sample(V3 normal, double cos_theta, Rng &rng) {
   if (cos_theta < 0) normal = -normal;
-  double theta = acos(sqrt(rng.next()));
+  double theta = gm::acos(sqrt(rng.next()));
   double phi = 2 * PI * rng.next();
   V3 perp(normal.y, -normal.x, 0);
   if (1.0 - fabs(normal.z) < 0.1) perp = V3(normal.z, 0, -normal.x);
   perp = normalize(perp);
-  V3 r = perp * sin(theta) + normal * cos(theta);
+  V3 r = perp * gm::sin(theta) + normal * gm::cos(theta);
   r = rotate(r, normal, phi);
   return normalize(r);
 }
 // Specular_ImportanceSample, :189-216
 static V3 specular_sample(V3 exact, double n, double cos_theta, Rng &rng) {
-  double angle_limit = (1.0 - acos(fabs(cos_theta)) * 2.0 / PI);
-  double alpha = acos(pow(rng.next(), 1.0 / (n + 1.0))) * angle_limit;
+  double angle_limit = (1.0 - gm::acos(fabs(cos_theta)) * 2.0 / PI);
+  double alpha = gm::acos(gm::pow(rng.next(), 1.0 / (n + 1.0))) * angle_limit;
   double phi = 2.0 * PI * rng.next();
   V3 perp(exact.y, -exact.x, 0);
   if (1.0 - fabs(exact.z) < 0.1) perp = V3(exact.z, 0, -exact.x);
   perp = normalize(perp);
-  V3 r = perp * sin(alpha) + exact * cos(alpha);
+  V3 r = perp * gm::sin(alpha) + exact * gm::cos(alpha);
   r = rotate(r, exact, phi);
   return normalize(r);
 }
@@ -460,7 +466,7 @@ static void soft_light(const Ctx &c, const Light &L, Rgb &color, const Brdf &brd
         V3 R = (2.0 * NL) * normal - Ld;
         double VR = dot(V, R);
         if (isNegOrZero(VR)) continue;
-        weight += (I * pow(VR, brdf.n));
+        weight += (I * gm::pow(VR, brdf.n));
       }
     }
     if (hits > 0) color += weight * brdf.ks * L.color * areasz / (double)hits;
@@ -495,8 +501,8 @@ static Rgb light_reflection(const Light &L, const Brdf &brdf, V3 eye, V3 p, V3 n
     if (L.type == L_SPOT) {
       V3 ML = normalize(p - L.pos);
       double ca = dot(ML, L.dir);
-      if (cos(L.cutoff) > ca) I = 0.0;
-      else I = I * pow(ca, L.dropoff);
+      if (gm::cos(L.cutoff) > ca) I = 0.0;
+      else I = I * gm::pow(ca, L.dropoff);
     }
     V3 Ld = normalize(L.pos - p);
     double NL = dot(normal, Ld);
@@ -504,7 +510,7 @@ static Rgb light_reflection(const Light &L, const Brdf &brdf, V3 eye, V3 p, V3 n
     V3 V = normalize(eye - p);
     double VR = dot(V, R);
     Rgb rgb = I * Dc * L.color * fabs(NL);
-    if (isPos(VR)) rgb += (I * pow(VR, s)) * Sc * L.color;
+    if (isPos(VR)) rgb += (I * gm::pow(VR, s)) * Sc * L.color;
     return rgb;
   }
   if (L.type == L_DIR) {
@@ -515,7 +521,7 @@ static Rgb light_reflection(const Light &L, const Brdf &brdf, V3 eye, V3 p, V3 n
     V3 V = normalize(eye - p);
     double VR = dot(V, R);
     Rgb rgb = (I * fabs(NL)) * Dc * L.color;
-    if (isPos(VR)) rgb += (I * pow(VR, s) * Sc * L.color);
+    if (isPos(VR)) rgb += (I * gm::pow(VR, s) * Sc * L.color);
     return rgb;
   }
   // area / rect without shadow tests
@@ -573,7 +579,7 @@ static Rgb light_reflection(const Light &L, const Brdf &brdf, V3 eye, V3 p, V3 n
         V3 V = normalize(eye - p);
         double VR = dot(V, R);
         if (isNegOrZero(VR)) continue;
-        sum += (I * pow(VR, s) * Sc * L.color);
+        sum += (I * gm::pow(VR, s) * Sc * L.color);
       }
     }
     Rgb mean = sum;
@@ -661,7 +667,7 @@ static void estimate_radiance(const Ctx &c, V3 p, V3 normal, Rgb &color, const B
   double c1 = 1.0, c2 = 1.0, total_w = 0;
   if (filter == GI_FILTER_CONE) c1 = 1.0 / (P.filter_const_k * sqrt(maxd2));
   else if (filter == GI_FILTER_GAUSS) {
-    c1 = pow(2.7182818284590452354, -P.filter_const_b);
+    c1 = gm::pow(2.7182818284590452354, -P.filter_const_b);
     c2 = 1.0 / (2.0 * maxd2);
   }
   for (int i = 0; i < num; i++) {
@@ -686,11 +692,11 @@ static void estimate_radiance(const Ctx &c, V3 p, V3 normal, Rgb &color, const B
     Rgb pc = rgbe_to_rgb(ph.rgbe);
     double ca = dot(exact, -inc);
     if (ca < 0) ca = 0;
-    pc *= fabs(perp) * brdf.kd + pow(ca, brdf.n) * brdf.ks;
+    pc *= fabs(perp) * brdf.kd + gm::pow(ca, brdf.n) * brdf.ks;
     if (filter == GI_FILTER_CONE) {
       pc *= (1.0 - c1 * sqrt((double)near[i].d2));
     } else if (filter == GI_FILTER_GAUSS) {
-      double w = (1.0 - (1.0 - pow(c1, c2 * (double)near[i].d2)) / (1.0 - c1));
+      double w = (1.0 - (1.0 - gm::pow(c1, c2 * (double)near[i].d2)) / (1.0 - c1));
       pc *= w;
       total_w += w;
     }
@@ -732,7 +738,7 @@ static void estimate_cached(const Ctx &c, V3 p, V3 normal, Rgb &color, const Brd
   Rgb pc = rgbe_to_rgb(map.ph[best].rgbe);
   double ca = dot(exact, -inc);
   if (ca < 0) ca = 0;
-  pc *= fabs(perp) * brdf.kd + pow(ca, brdf.n) * brdf.ks;
+  pc *= fabs(perp) * brdf.kd + gm::pow(ca, brdf.n) * brdf.ks;
   color += pc;
 }
 
@@ -1018,9 +1024,9 @@ static void store_photon(const Rgb &power, V3 inc, V3 p, std::vector<Photon> &ou
   Photon ph;
   ph.pos[0] = (float)p.x; ph.pos[1] = (float)p.y; ph.pos[2] = (float)p.z;
   rgb_to_rgbe(power, ph.rgbe);
-  int phi = (uint8_t)(255.0 * (atan2(inc.y, inc.x) + PI) / (2.0 * PI));
+  int phi = (uint8_t)(255.0 * (gm::atan2(inc.y, inc.x) + PI) / (2.0 * PI));
   double z = inc.z < -1.0 ? -1.0 : (inc.z > 1.0 ? 1.0 : inc.z);
-  int theta = (uint8_t)(255.0 * acos(z) / PI);
+  int theta = (uint8_t)(255.0 * gm::acos(z) / PI);
   ph.dir = (uint16_t)(phi * 256 + theta);
   ph.flags = (uint16_t)(g_tagging ? tag : 0);
   out.push_back(ph);
@@ -1120,7 +1126,7 @@ static void emit_one(const Ctx &c, const Light &L, bool caustic, Rng &rng,
     dir = normalize(V3(x, y, z));
   } else if (L.type == L_SPOT) {
     V3 ln = L.dir;
-    double cutoff = fabs(cos(L.cutoff));
+    double cutoff = fabs(gm::cos(L.cutoff));
     int attempts_left = 20;
     V3 sd;
     do {
@@ -1752,6 +1758,25 @@ int oracle_parse_args(int argc, char **argv, gi_params *P, int *w, int *h, int *
   std::string scene, out, err;
   *w = 1024; *h = 1024; *aa = 2; *real = 0;
   return parse_args(argc, argv, *P, scene, out, *w, *h, *aa, *real, err);
+}
+
+// gi_math.h on the host (tests/test_cpu_math.py): fn as gi_math_probe (include/gi.h)
+int oracle_math(int fn, int64_t n, const double *x, const double *y, double *out) {
+  for (int64_t i = 0; i < n; i++) {
+    const double a = x[i], b = y[i];
+    switch (fn) {
+      case 0: out[i] = gm::acos(a); break;
+      case 1: out[i] = gm::sin(a); break;
+      case 2: out[i] = gm::cos(a); break;
+      case 3: out[i] = gm::pow(a, b); break;
+      case 4: out[i] = gm::atan2(a, b); break;
+      case 5: out[i] = sqrt(a); break;
+      case 6: out[i] = gm::tan(a); break;
+      case 7: out[i] = gm::asin(a); break;
+      default: return 1;
+    }
+  }
+  return 0;
 }
 
 }  // extern "C"

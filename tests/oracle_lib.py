@@ -32,6 +32,7 @@ def lib():
         L.oracle_rgbe_encode.argtypes = [C.c_void_p, C.c_void_p]
         L.oracle_rgbe_decode.argtypes = [C.c_void_p, C.c_void_p]
         L.oracle_direction_lut.argtypes = [C.c_void_p]
+        L.oracle_math.argtypes = [C.c_int, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
         L.oracle_parse_args.argtypes = [C.c_int, C.POINTER(C.c_char_p), C.c_void_p,
                                         C.POINTER(C.c_int), C.POINTER(C.c_int),
                                         C.POINTER(C.c_int), C.POINTER(C.c_int)]
@@ -137,4 +138,17 @@ def rgbe_decode(b):
 def direction_lut():
     out = np.zeros((65536, 3))
     lib().oracle_direction_lut(out.ctypes.data)
+    return out
+
+
+MATH_FNS = {"acos": 0, "sin": 1, "cos": 2, "pow": 3, "atan2": 4, "sqrt": 5, "tan": 6, "asin": 7}
+
+
+def math(fn, x, y=None):
+    """gi_math.h's fp64 function `fn` on the host (the oracle's, and the device's, sequence)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.zeros_like(x) if y is None else np.ascontiguousarray(y, dtype=np.float64)
+    out = np.empty_like(x)
+    rc = lib().oracle_math(MATH_FNS[fn], len(x), x.ctypes.data, y.ctypes.data, out.ctypes.data)
+    assert rc == 0
     return out

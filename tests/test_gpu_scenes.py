@@ -13,6 +13,7 @@ import os
 import numpy as np
 import pytest
 
+import libm_ref
 import oracle_lib
 from gpu_util import compare, run_gpu, INP
 
@@ -101,47 +102,20 @@ def test_circle_intersections_match_oracle(renderer):
     np.testing.assert_array_equal(gm[both], om[both])
 
 
-def _glibc(fn, x, y):
-    """The host C library's fp64 function (the oracle's <cmath> calls), one call per element."""
-    import ctypes as C
-    libm = C.CDLL("libm.so.6")
-    f = getattr(libm, fn)
-    two = fn in ("pow", "atan2")
-    f.argtypes = [C.c_double, C.c_double] if two else [C.c_double]
-    f.restype = C.c_double
-    if two:
-        return np.array([f(float(a), float(b)) for a, b in zip(x, y)])
-    return np.array([f(float(a)) for a in x])
-
-
-def test_device_math_differs_from_host_libm_by_one_ulp(renderer):
-    """The fork source that the small-map scene tests above allow for (their 1 % stored-count
-    and L2 tolerances): the device's fp64 acos / sin / cos / pow / atan2 (ROCm's math library)
-    and the host C library the oracle calls agree to within one ulp, but not bit for bit, on the
-    argument ranges the samplers and StorePhoton use (graphics_utils.cpp:162-216,
-    photon_utils.cpp:56-60); sqrt is correctly rounded on both sides."""
+def test_device_math_equals_oracle_math(renderer):
+    """The device evaluates gi_math.h's fp64 sin / cos / tan / asin / acos / atan2 / pow (the
+    functions the samplers, Fresnel / Phong terms and StorePhoton call: graphics_utils.cpp:
+    95-216, photon_utils.cpp:56-60) with the same operation sequence as the oracle, so the two
+    agree bit for bit on every input; both stay within libm_ref.ULP_BOUND of glibc. (Before
+    r04 the device called ROCm's math library, within one ulp of glibc but not equal to it, and
+    that ulp forked the long bounce chains of cylinder.scn.)"""
     import gi_amd
-    rng = np.random.default_rng(11)
-    n = 20000
-    u = rng.random(n)
-    cases = {
-        "acos": (2.0 * u - 1.0, None),                    # acos(cos theta), acos(z)
-        "sin": (u * np.pi, None),                          # sin(theta), sin(alpha)
-        "cos": (u * 2.0 * np.pi, None),                    # cos(phi) of the samplers' rotation
-        "pow": (u, 1.0 / (rng.integers(1, 10000, n) + 1.0)),  # pow(r, 1 / (n + 1))
-        "atan2": (2.0 * u - 1.0, 2.0 * rng.random(n) - 1.0),  # atan2(y, x) of the direction code
-        "sqrt": (u, None),
-    }
-    differ = {}
-    for fn, (x, y) in cases.items():
-        dev = gi_amd.math_probe(renderer, fn, x, y)
-        host = _glibc(fn, x, np.zeros_like(x) if y is None else y)
-        ulp = np.abs(dev - host) / np.spacing(np.abs(host))
-        assert ulp.max() <= 1.0, (fn, float(ulp.max()))
-        differ[fn] = float((dev != host).mean())
-    print("\nfraction of inputs where device != host libm:", differ)
-    assert differ["sqrt"] == 0.0
-    assert max(v for k, v in differ.items() if k != "sqrt") > 0.0
+    for fn, (x, y) in libm_ref.cases().items():
+        yy = np.zeros_like(x) if y is None else y
+        dev = gi_amd.math_probe(renderer, fn, x, yy)
+        np.testing.assert_array_equal(dev, oracle_lib.math(fn, x, yy), err_msg=fn)
+        u = libm_ref.ulps(dev, libm_ref.glibc(fn, x, yy))
+        assert u.max() <= libm_ref.ULP_BOUND[fn], (fn, float(u.max()))
 
 
 def test_cylinder_scene_is_exact_without_bounce_chains(renderer):

@@ -679,12 +679,13 @@ GI_HD V transmissive_bounce(double ir_air, V n, V view, double ct, double ir_mat
   return normalize(refr);
 }
 GI_HD V rotate(V v, V axis, double theta) {  // R3Vector::Rotate, R3Vector.cpp:352-363
-  double ct = gm::cos(theta);
+  double st, ct;
+  gm::sincos(theta, st, ct);  // = gm::sin(theta), gm::cos(theta), one range reduction
   double d = dot(v, axis);
   V cr = cross(v, axis);
   v = v * ct;
   v = v + axis * d * (1.0 - ct);
-  v = v - cr * gm::sin(theta);
+  v = v - cr * st;
   return v;
 }
 GI_HD V diffuse_sample(V n, double ct, Rng &rng) {  // Diffuse_ImportanceSample :162-185
@@ -694,7 +695,9 @@ GI_HD V diffuse_sample(V n, double ct, Rng &rng) {  // Diffuse_ImportanceSample 
   V perp = mk(n.y, -n.x, 0);
   if (1.0 - fabs(n.z) < 0.1) perp = mk(n.z, 0, -n.x);
   perp = normalize(perp);
-  V r = perp * gm::sin(theta) + n * gm::cos(theta);
+  double st, ctt;
+  gm::sincos(theta, st, ctt);
+  V r = perp * st + n * ctt;
   r = rotate(r, n, phi);
   return normalize(r);
 }
@@ -705,7 +708,9 @@ GI_HD V specular_sample(V ex, double nsh, double ct, Rng &rng) {  // :189-216
   V perp = mk(ex.y, -ex.x, 0);
   if (1.0 - fabs(ex.z) < 0.1) perp = mk(ex.z, 0, -ex.x);
   perp = normalize(perp);
-  V r = perp * gm::sin(alpha) + ex * gm::cos(alpha);
+  double sa, ca;
+  gm::sincos(alpha, sa, ca);
+  V r = perp * sa + ex * ca;
   r = rotate(r, ex, phi);
   return normalize(r);
 }

@@ -9,8 +9,9 @@ one ulp forks the chains. Both sides now evaluate the same operation sequence bu
 operations that are correctly rounded on x86-64 and on gfx950 (+, -, *, /, sqrt, fma, rint, exact
 scaling), so they get the same bits.
 
-The polynomial coefficients are Taylor coefficients (exact rationals, rounded once to double);
-the constants (pi/2, pi, ln 2 in two or three parts) come from 60-digit decimal arithmetic here.
+The polynomial coefficients are Chebyshev fits (near minimax, truncation error below 2^-56
+relative to each function) computed in 70-digit decimal arithmetic and rounded once to double; the
+ln(m / c) series keeps its Taylor coefficients; the constants (pi/2, pi, ln 2 in two or three parts) come from 60-digit decimal arithmetic here.
 Accuracy against glibc is measured by tests/test_cpu_math.py.
 
 usage: python3 tools/gen_gi_math.py   (rewrites the header)
@@ -20,7 +21,7 @@ from decimal import Decimal, getcontext
 from fractions import Fraction
 from math import factorial
 
-getcontext().prec = 80
+getcontext().prec = 70
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "global-illumination_amd", "csrc", "gi_math.h")
 
@@ -65,6 +66,82 @@ def split(d, n, zero_bits=0):
     return out
 
 
+def dcos(x):
+    s = Decimal(0); t = Decimal(1); k = 0
+    while abs(t) > Decimal(10) ** -68:
+        s += t; k += 2; t = -t * x * x / (k * (k - 1))
+    return s
+
+def cheb_fit(f, a, b, deg, PI, N=None):
+    """near-minimax polynomial (monomial coeffs in t, as Fractions) of degree deg for f on [a,b]"""
+    N = N or deg + 1
+    a, b = Decimal(a), Decimal(b)
+    xs = [dcos(PI * (Decimal(k) + Decimal('0.5')) / N) for k in range(N)]
+    ts = [(b - a) / 2 * x + (b + a) / 2 for x in xs]
+    fs = [f(t) for t in ts]
+    c = []
+    for j in range(deg + 1):
+        s = Decimal(0)
+        for k in range(N):
+            s += fs[k] * dcos(PI * j * (Decimal(k) + Decimal('0.5')) / N)
+        c.append(s * 2 / N)
+    c[0] /= 2
+    # sum c_j T_j(s), s = (2t - (a+b))/(b-a)  -> monomials in t (Fractions)
+    A = Fraction(2) / Fraction(b - a); B = -Fraction(b + a) / Fraction(b - a)   # s = A t + B
+    # T_0 = 1, T_1 = s, T_{j+1} = 2 s T_j - T_{j-1}; polys as lists of Fractions in t
+    T = [[Fraction(1)], [B, A]]
+    for j in range(2, deg + 1):
+        p = [Fraction(0)] * (j + 1)
+        for i, ci in enumerate(T[j - 1]):
+            p[i] += 2 * B * ci; p[i + 1] += 2 * A * ci
+        for i, ci in enumerate(T[j - 2]):
+            p[i] -= ci
+        T.append(p)
+    out = [Fraction(0)] * (deg + 1)
+    for j in range(deg + 1):
+        cj = Fraction(c[j])
+        for i, ti in enumerate(T[j]):
+            out[i] += cj * ti
+    return out, float(abs(c[-1]))
+
+def dasin_series(x):
+    # asin x = sum (2n)!/(4^n n!^2 (2n+1)) x^(2n+1)
+    s = Decimal(0); term = x; n = 0; x2 = x * x; coef = Decimal(1)
+    while True:
+        t = coef * term / (2 * n + 1)
+        if abs(t) < Decimal(10) ** -66: break
+        s += t
+        n += 1; coef = coef * (2 * n - 1) / (2 * n); term *= x2
+    return s
+
+def datan_series(x):
+    s = Decimal(0); t = x; k = 0; x2 = x * x
+    while abs(t) > Decimal(10) ** -66:
+        s += t / (2 * k + 1) * (1 if k % 2 == 0 else -1); t *= x2; k += 1
+    return s
+
+def A_f(t):  # (asin(sqrt t)/sqrt t - 1)/t
+    if t == 0: return Decimal(1) / 6
+    r = t.sqrt(); return (dasin_series(r) / r - 1) / t
+def T_f(w):
+    if w == 0: return Decimal(-1) / 3
+    r = w.sqrt(); return (datan_series(r) / r - 1) / w
+def S_f(z):  # (sin r - r)/(r z), z = r^2 -> sum (-1)^k z^(k-1)/(2k+1)!
+    s = Decimal(0); t = Decimal(-1) / 6; k = 1
+    while abs(t) > Decimal(10) ** -66:
+        s += t; k += 1; t = -t * z / ((2 * k) * (2 * k + 1))
+    return s
+def C_f(z):  # (cos r - 1 + z/2)/z^2
+    s = Decimal(0); t = Decimal(1) / 24; k = 2
+    while abs(t) > Decimal(10) ** -66:
+        s += t; k += 1; t = -t * z / ((2 * k - 1) * (2 * k))
+    return s
+def E_f(r):  # (exp r - 1 - r)/r^2
+    if abs(r) < Decimal(10) ** -12:
+        return Decimal(1) / 2 + r / 6 + r * r / 24
+    return (r.exp() - 1 - r) / (r * r)
+
+
 def lit(v):
     r = repr(float(v))
     return r if ("e" in r or "." in r or "inf" in r or "nan" in r) else r + ".0"
@@ -81,21 +158,21 @@ def main():
     pio4_lo = dbl(PI / 4 - Decimal(Fraction(pio4).numerator) / Decimal(Fraction(pio4).denominator))
     tan_pi8 = dbl((Decimal(2).sqrt() - 1))
     inv_ln2 = dbl(1 / LN2)
-    # sin(r) = r + r z S(z), S = sum_{k=1..10} (-1)^k z^(k-1) / (2k+1)!
-    S = [Fraction((-1) ** k, factorial(2 * k + 1)) for k in range(1, 11)]
-    # cos(r) = 1 - z/2 + z^2 C(z), C = sum_{k=2..10} (-1)^k z^(k-2) / (2k)!
-    Cc = [Fraction((-1) ** k, factorial(2 * k)) for k in range(2, 11)]
-    # asin(x) = x + x t A(t), t = x^2, |x| <= 1/2: A = sum_{n=1..24} c_n t^(n-1)
-    A = [Fraction(factorial(2 * n), 4 ** n * factorial(n) ** 2 * (2 * n + 1)) for n in range(1, 25)]
-    # atan(v) = v + v w T(w), w = v^2, |v| <= tan(pi/8): T = sum_{k=1..21} (-1)^k w^(k-1)/(2k+1)
-    T = [Fraction((-1) ** k, 2 * k + 1) for k in range(1, 22)]
+    # sin(r) = r + r z S(z), S: degree-7 Chebyshev fit of (sin r - r) / (r z) on z in [0, (pi/4)^2]
+    S = cheb_fit(S_f, 0, 0.6169, 7, PI)[0]
+    # cos(r) = 1 - z/2 + z^2 C(z), C: degree-6 fit of (cos r - 1 + z/2) / z^2
+    Cc = cheb_fit(C_f, 0, 0.6169, 6, PI)[0]
+    # asin(x) = x + x t A(t), t = x^2, |x| <= 1/2: A: degree-13 fit on t in [0, 1/4]
+    A = cheb_fit(A_f, 0, 0.25, 13, PI)[0]
+    # atan(v) = v + v w T(w), w = v^2, |v| <= tan(pi/8): T: degree-12 fit on w in [0, tan(pi/8)^2]
+    T = cheb_fit(T_f, 0, 0.1716, 12, PI)[0]
     # ln(m / c) = 2 s + s u L(u), s = (m-c)/(m+c), u = s^2, |s| <= 0.0056:
     #   L = sum_{k=1..5} 2 u^(k-1) / (2k+1)
     L = [Fraction(2, 2 * k + 1) for k in range(1, 6)]
     # ln(c_j), c_j = 1 + j/64, j = -19..27 (covers m in [sqrt(1/2), sqrt(2))), as hi + lo
     LNC = [split((1 + Decimal(j) / 64).ln(), 2) for j in range(-19, 28)]
-    # exp(r) = 1 + r + r^2 E(r), |r| <= ln2/2 (+ tail): E = sum_{k=2..14} r^(k-2)/k!
-    E = [Fraction(1, factorial(k)) for k in range(2, 15)]
+    # exp(r) = 1 + r + r^2 E(r), |r| <= ln2/2 (+ tail): E: degree-11 fit of (e^r - 1 - r) / r^2
+    E = cheb_fit(E_f, -0.3466, 0.3466, 11, PI)[0]
 
     def horner(name, coeffs, var):
         # returns C++ expression evaluating sum coeffs[i] var^i with fma (highest first)
@@ -118,7 +195,7 @@ def main():
 // -ffp-contract=off), so the device and the host restatement get the same bits. (The device's
 // ROCm math library and glibc agree only to within one ulp, and that ulp forks long bounce
 // chains: tests/test_gpu_scenes.py.) Accuracy against glibc: tests/test_cpu_math.py.
-// Polynomials: Taylor coefficients rounded once to double; constants from 60-digit arithmetic.
+// Polynomials: Chebyshev fits rounded once to double; constants from 70-digit arithmetic.
 #ifndef GI_MATH_H
 #define GI_MATH_H
 #include <stdint.h>
@@ -190,6 +267,17 @@ GM_HD double cos(double x) {{
   const double v = (q & 1) ? sin_k(r) : cos_k(r);
   return (q == 1 || q == 2) ? -v : v;
 }}
+// sin(x) and cos(x) with one reduction (bit-identical to sin(x), cos(x))
+GM_HD void sincos(double x, double &sn, double &cs) {{
+  if (x == 0.0) {{ sn = x; cs = 1.0; return; }}
+  double k;
+  const double r = reduce(x, k);
+  const int q = (int)((int64_t)k & 3);
+  const double s0 = sin_k(r), c0 = cos_k(r);
+  const double vs = (q & 1) ? c0 : s0, vc = (q & 1) ? s0 : c0;
+  sn = (q & 2) ? -vs : vs;
+  cs = (q == 1 || q == 2) ? -vc : vc;
+}}
 GM_HD double tan(double x) {{
   if (x == 0.0) return x;
   double k;
@@ -204,20 +292,26 @@ GM_HD double asin_k(double x) {{
   const double a = {horner("A", A, "t")};
   return fma(x * t, a, x);
 }}
+// asin / acos: one polynomial evaluation per call (|x| <= 1/2: asin_k(x); else the half-angle
+// argument sqrt((1 - |x|) / 2)), so divergent lanes do not run both
 GM_HD double asin(double x) {{
   const double ax = fabs(x);
   if (!(ax <= 1.0)) return (x - x) / (x - x);  // NaN (|x| > 1 or NaN)
-  if (ax <= 0.5) return asin_k(x);
-  const double s = sqrt((1.0 - ax) * 0.5);
-  const double v = (PIO2_HI - 2.0 * asin_k(s)) + PIO2_MID;
+  const bool small = ax <= 0.5;
+  const double z = small ? x : sqrt((1.0 - ax) * 0.5);
+  const double p = asin_k(z);
+  if (small) return p;
+  const double v = (PIO2_HI - 2.0 * p) + PIO2_MID;
   return x < 0 ? -v : v;
 }}
 GM_HD double acos(double x) {{
   const double ax = fabs(x);
   if (!(ax <= 1.0)) return (x - x) / (x - x);
-  if (ax <= 0.5) return PIO2_HI - (asin_k(x) - PIO2_MID);
-  const double s = sqrt((1.0 - ax) * 0.5);
-  const double a = 2.0 * asin_k(s);
+  const bool small = ax <= 0.5;
+  const double z = small ? x : sqrt((1.0 - ax) * 0.5);
+  const double p = asin_k(z);
+  if (small) return PIO2_HI - (p - PIO2_MID);
+  const double a = 2.0 * p;
   return x > 0 ? a : (PI_HI - a) + PI_LO;
 }}
 

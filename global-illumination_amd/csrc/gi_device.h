@@ -652,8 +652,8 @@ __device__ __forceinline__ bool scene_intersect(const SceneView &S, V org, V dir
 // Optics and sampling (utils/graphics_utils.cpp)
 // ---------------------------------------------------------------------------------------
 GI_HD double reflection_coeff(double ir_air, double cos_theta, double ir_mat) {  // :95-101
-  double r0 = gm::pow((ir_air - ir_mat) / (ir_air + ir_mat), 2.0);
-  return (r0 + (1.0 - r0) * gm::pow((1.0 - fabs(cos_theta)), 5.0));
+  double r0 = gm::pow2((ir_air - ir_mat) / (ir_air + ir_mat));
+  return (r0 + (1.0 - r0) * gm::pow5((1.0 - fabs(cos_theta))));
 }
 GI_HD V reflective_bounce(V n, V view, double ct) {  // :104-117
   if (ct < 0) { n = -n; ct *= -1.0; }

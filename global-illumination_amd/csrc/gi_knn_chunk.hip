@@ -633,13 +633,16 @@ __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, flo
         }
         o0 *= kd0; o1 *= kd1; o2 *= kd2;
       } else {
+      // one photon per step here: this path calls pow (specular term, Gauss filter), and a
+      // group of photons held across those calls would cost the whole kernel registers
+      constexpr int EB1 = 1;
       const double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
-      for (int s0 = 0; s0 < num; s0 += EB) {
-      float4 pg[EB];
-      uint32_t eg[EB];
-      double lg[EB][3];
+      for (int s0 = 0; s0 < num; s0 += EB1) {
+      float4 pg[EB1];
+      uint32_t eg[EB1];
+      double lg[EB1][3];
 #pragma unroll
-      for (int u = 0; u < EB; u++) {
+      for (int u = 0; u < EB1; u++) {
         uint32_t slot = slot_at(s0 + u < num ? s0 + u : s0);
         pg[u] = cpos.get(slot);
         eg[u] = crgbe[slot];
@@ -649,7 +652,7 @@ __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, flo
         lg[u][2] = a.lut[3 * dc + 2];
       }
 #pragma unroll
-      for (int u = 0; u < EB; u++) {
+      for (int u = 0; u < EB1; u++) {
         if (s0 + u >= num) break;
         float4 p = pg[u];
         double d2 = (double)metric(qp.x, qp.y, qp.z, p);

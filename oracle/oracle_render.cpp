@@ -257,8 +257,8 @@ static bool intersect(const Ctx &c, V3 org, V3 dir, Hit &h);
 
 // Schlick, :95-101
 static double reflection_coeff(double ir_air, double cos_theta, double ir_mat) {
-  double r0 = gm::pow((ir_air - ir_mat) / (ir_air + ir_mat), 2);
-  return (r0 + (1.0 - r0) * gm::pow((1.0 - fabs(cos_theta)), 5));
+  double r0 = gm::pow2((ir_air - ir_mat) / (ir_air + ir_mat));
+  return (r0 + (1.0 - r0) * gm::pow5((1.0 - fabs(cos_theta))));
 }
 // ReflectiveBounce, :104-117
 static V3 reflective_bounce(V3 normal, V3 view, double cos_theta) {

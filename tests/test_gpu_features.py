@@ -121,8 +121,9 @@ def test_emission_per_light_type(renderer, name, extra):
     """EmitPhotons per light type (photontracer.cpp:198-360): spot (Phong lobe + cutoff
     rejection), directional (disk at 3 R_scene), circular area (disk point + cosine direction),
     point, rect -- the device map equals the restatement's photon for photon."""
-    args = [scene(name), "/tmp/x.png", "-global", "20000", "-caustic", "20000", "-seed",
-            "13"] + extra
+    # global map only: the caustic map is not compared here, and spotlight1.scn's Ks = 0.2
+    # walls store one caustic photon per ~47,000 emitted (the restatement traced 942 M of them)
+    args = [scene(name), "/tmp/x.png", "-global", "20000", "-no_caustic", "-seed", "13"] + extra
     p, sc, *_ = gi_amd.ParseArgs(args)
     renderer.set_params(p)
     renderer.ReadScene(sc)

@@ -4,9 +4,10 @@ same RNG streams (f3 of SURVEY.md 8(f); .scn grammar R3Scene.cpp:1462-1953, .off
 
 Each scene renders a small direct-only image and a small full-GI image (own photon maps, every
 estimator on), so every loader command, light type, primitive and material combination the
-reference's inputs use runs at least once on the GPU. Thresholds are those of the other image
-tests (test_gpu_render.py): a one-ulp difference in a device transcendental may fork a Monte
-Carlo path, nothing more."""
+reference's inputs use runs at least once on the GPU. Both must be bit-identical to the oracle's,
+with equal stored photon counts: the device and the oracle share gi_math.h's transcendentals
+(before r04 a one-ulp difference between ROCm's math library and glibc forked the long bounce
+chains of cylinder.scn, and the stack / violin maps by a few photons)."""
 import glob
 import os
 
@@ -22,7 +23,6 @@ pytestmark = pytest.mark.gpu
 EXTRA = os.path.join(os.path.dirname(INP), "scenes_extra")
 SCENES = sorted(os.path.basename(p) for p in glob.glob(os.path.join(INP, "*.scn")))
 ALL = [os.path.join(INP, s) for s in SCENES] + [os.path.join(EXTRA, "circles.scn")]
-CYLINDER_SCENES = {"cylinder.scn", "lines.scn"}
 FAST = ["-lt", "4", "-ss", "4", "-tt", "4", "-st", "4", "-md", "32"]
 
 
@@ -37,7 +37,7 @@ def test_scene_direct_only_matches_oracle(renderer, path):
     g, gst, _ = run_gpu(renderer, args)
     o, ost = oracle_lib.render(args, 32, 24)
     assert gst["screen_rays"] == ost["screen_rays"]
-    compare(g, o, 0.99, 0.995, 0.5)
+    compare(g, o, 1.0, 1.0, 0.0, l2_rms_tol=0.0)
 
 
 @pytest.mark.parametrize("path", ALL, ids=os.path.basename)
@@ -47,23 +47,12 @@ def test_scene_full_gi_matches_oracle(renderer, path):
     g, gst, gp = run_gpu(renderer, args)
     o, ost = oracle_lib.render(args, 24, 16)
     if gp is not None:
-        # equal in practice; a photon path can fork on a one-ulp difference between the
-        # device's and glibc's acos/sin/cos where a bounce grazes its own surface (measured on
-        # cylinder.scn: rays leaving the side next to a cap re-enter the infinite cylinder at
-        # t ~ 0, R3Isect.cpp:1049-1095), and the emission rounds then re-plan the counts
         for k in ("global_stored", "caustic_stored"):
-            assert abs(gp[k] - ost[k]) <= max(2, 0.01 * ost[k]), (k, gp[k], ost[k])
+            assert gp[k] == ost[k], (k, gp[k], ost[k])
     assert gst["screen_rays"] == ost["screen_rays"]
-    if os.path.basename(path) in CYLINDER_SCENES:
-        # a photon that bounces off the reference's cylinder re-hits it at t ~ 0 (1,747 of the
-        # 3,012 photons stored here are such repeats), so these chains fork often on one-ulp
-        # transcendental differences (and so do the render's own indirect paths leaving the
-        # cylinder): the maps are the same distribution, not the same photons
-        compare(g, o, 0.90, 0.97, 1.0, l2_rms_tol=3.0)
-    else:
-        # a map that differs by a few forked photons moves some estimates by 1-3 LSB (measured:
-        # stack.scn 97.4 % exact, all within 1 LSB; violin.scn 94.5 % exact, L2 RMS 0.44)
-        compare(g, o, 0.93, 0.98, 0.5)
+    for k in ("shadow_rays", "monte_carlo_rays", "indirect_samples", "caustic_samples"):
+        assert gst[k] == ost[k], (k, gst[k], ost[k])
+    compare(g, o, 1.0, 1.0, 0.0, l2_rms_tol=0.0)
 
 
 def test_circle_intersections_match_oracle(renderer):
@@ -116,22 +105,3 @@ def test_device_math_equals_oracle_math(renderer):
         np.testing.assert_array_equal(dev, oracle_lib.math(fn, x, yy), err_msg=fn)
         u = libm_ref.ulps(dev, libm_ref.glibc(fn, x, yy))
         assert u.max() <= libm_ref.ULP_BOUND[fn], (fn, float(u.max()))
-
-
-def test_cylinder_scene_is_exact_without_bounce_chains(renderer):
-    """cylinder.scn's full-GI comparison above needs its own loose bound (L2 RMS 3.0) because a
-    photon or indirect path leaving the infinite cylinder re-hits it at t ~ 0 (R3Isect.cpp:
-    1049-1095), so its chains run many bounces on the surface and a one-ulp libm difference
-    (test above) forks them. With the chains cut to one bounce (-pd 1: photons store at their
-    first hit and stop; -md 1: Monte Carlo paths one bounce) the same scene meets the other
-    scenes' full-GI tolerance: the stored counts are equal, and on MI355X 382 of the 384 pixels
-    are exact with per-pixel L2 RMS 0.87 (1.95 with the chains; bound 1.0 here, 3.0 there)."""
-    path = os.path.join(INP, "cylinder.scn")
-    args = [path, "/tmp/s.png", "-resolution", "24", "16", "-aa", "0", "-global", "3000",
-            "-caustic", "3000", "-it", "4", "-seed", "4", "-pd", "1", "-lt", "4", "-ss", "4",
-            "-tt", "4", "-st", "4", "-md", "1"]
-    g, gst, gp = run_gpu(renderer, args)
-    o, ost = oracle_lib.render(args, 24, 16)
-    assert gp["global_stored"] == ost["global_stored"]
-    assert gp["caustic_stored"] == ost["caustic_stored"]
-    compare(g, o, 0.93, 0.98, 0.5, l2_rms_tol=1.0)

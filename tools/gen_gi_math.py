@@ -387,6 +387,11 @@ GM_HD double exp_dd(double hi, double lo) {{
   return scale2(p, (int)k);
 }}
 
+// pow(x, 2) and pow(x, 5) of Schlick's formula (graphics_utils.cpp:95-101): x * x is the
+// correctly rounded square (what glibc's pow(x, 2) returns); x^5 = (x^2)^2 x, within 2 ulp
+GM_HD double pow2(double x) {{ return x * x; }}
+GM_HD double pow5(double x) {{ const double x2 = x * x; return (x2 * x2) * x; }}
+
 GM_HD double pow(double x, double y) {{
   if (y == 0.0 || x == 1.0) return 1.0;
   if (x != x || y != y) return x + y;

@@ -45,6 +45,12 @@ def l2_stats(a, b):
     return float(np.sqrt((l2 * l2).mean())), float(l2.max())
 
 
+def compare_exact(a, b):
+    """The device image equals the oracle's bit for bit (every pixel, every channel): the two
+    share the RNG streams, the operation order and, since r04, gi_math.h's transcendentals."""
+    compare(a, b, 1.0, 1.0, 0.0, l2_rms_tol=0.0)
+
+
 def compare(a, b, exact_frac, le1_frac, mean_tol, l2_rms_tol=None):
     """8-bit image parity: fraction of pixels exact / within 1 LSB (max over channels), the
     mean level and the RMS of the per-pixel L2 distance."""

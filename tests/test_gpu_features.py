@@ -9,7 +9,7 @@ import pytest
 import gallery
 import gi_amd
 import oracle_lib
-from gpu_util import compare, run_gpu, scene
+from gpu_util import compare_exact, run_gpu, scene
 
 pytestmark = pytest.mark.gpu
 
@@ -27,7 +27,7 @@ def test_gallery_figure_pins_device(renderer, fig, tmp_path):
     assert s["exact_unsat"] >= 0.85, s
     assert s["zero_agree"] >= 0.999, s
     o, _ = oracle_lib.render(args + ["-threads", "16"], 512, 512)
-    compare(g, o, 0.999, 0.9999, 0.01)
+    compare_exact(g, o)
 
 
 @pytest.mark.parametrize("scn,light", [
@@ -51,7 +51,7 @@ def test_c1_exact_command(renderer):
             "-no_indirect", "-no_caustic", "-seed", "1"]
     g, gst, _ = run_gpu(renderer, args)
     o, ost = oracle_lib.render(args + ["-threads", "16"], 256, 256)
-    compare(g, o, 0.999, 0.9995, 0.02)
+    compare_exact(g, o)
     for k in ("screen_rays", "shadow_rays", "transmissive_samples", "specular_samples"):
         assert gst[k] == ost[k], k
 
@@ -67,7 +67,7 @@ def test_c4_with_caustic_map(renderer):
     assert gp["caustic_stored"] == ost["caustic_stored"] > 30000
     assert gp["global_stored"] == ost["global_stored"]
     assert gst["knn_map_queries"][1] > 0
-    compare(g, o, 0.99, 0.99, 0.5)
+    compare_exact(g, o)
 
 
 # --- render features -----------------------------------------------------------------------
@@ -111,7 +111,7 @@ def test_feature_matches_oracle(renderer, name, extra):
     assert gst["screen_rays"] == ost["screen_rays"]
     assert gst["shadow_rays"] == ost["shadow_rays"]
     assert g.max() > 0
-    compare(g, o, 0.99, 0.995, 0.5)
+    compare_exact(g, o)
 
 
 @pytest.mark.parametrize("name,extra", [
@@ -131,9 +131,9 @@ def test_emission_per_light_type(renderer, name, extra):
     gg = renderer.photon_map(gi_amd.GLOBAL)
     og, oc, _em = oracle_lib.map_photons(args)
     assert len(gg) == len(og) > 10000
-    np.testing.assert_allclose(gg["pos"], og["pos"], atol=1e-5)
-    assert (gg["rgbe"] == og["rgbe"]).all(axis=1).mean() > 0.999
-    assert (gg["dir"] == og["dir"]).mean() > 0.999
+    np.testing.assert_array_equal(gg["pos"], og["pos"])
+    np.testing.assert_array_equal(gg["rgbe"], og["rgbe"])
+    np.testing.assert_array_equal(gg["dir"], og["dir"])
     gc = renderer.photon_map(gi_amd.CAUSTIC)
     assert len(gc) == len(oc)
 
@@ -189,7 +189,7 @@ def test_large_map_render_matches_oracle(renderer, name, extra, res):
     assert gp["caustic_stored"] == ost["caustic_stored"] >= 4000000
     assert gp["global_stored"] == ost["global_stored"]
     assert gst["knn_map_queries"][1] > 0
-    compare(g, o, 0.99, 0.99, 0.5)
+    compare_exact(g, o)
 
 
 @pytest.mark.parametrize("name,extra,goal_g,goal_c", [

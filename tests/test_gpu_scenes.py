@@ -16,7 +16,7 @@ import pytest
 
 import libm_ref
 import oracle_lib
-from gpu_util import compare, run_gpu, INP
+from gpu_util import compare_exact, run_gpu, INP
 
 pytestmark = pytest.mark.gpu
 
@@ -37,7 +37,7 @@ def test_scene_direct_only_matches_oracle(renderer, path):
     g, gst, _ = run_gpu(renderer, args)
     o, ost = oracle_lib.render(args, 32, 24)
     assert gst["screen_rays"] == ost["screen_rays"]
-    compare(g, o, 1.0, 1.0, 0.0, l2_rms_tol=0.0)
+    compare_exact(g, o)
 
 
 @pytest.mark.parametrize("path", ALL, ids=os.path.basename)
@@ -52,7 +52,7 @@ def test_scene_full_gi_matches_oracle(renderer, path):
     assert gst["screen_rays"] == ost["screen_rays"]
     for k in ("shadow_rays", "monte_carlo_rays", "indirect_samples", "caustic_samples"):
         assert gst[k] == ost[k], (k, gst[k], ost[k])
-    compare(g, o, 1.0, 1.0, 0.0, l2_rms_tol=0.0)
+    compare_exact(g, o)
 
 
 def test_circle_intersections_match_oracle(renderer):

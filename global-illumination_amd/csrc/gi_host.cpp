@@ -329,6 +329,7 @@ struct gi_ctx {
   int chunk_minsub_big2 = 64;        // ... its overflowing chunks retried down to this group size
   bool chunk_dk = true;            // chunk kernel (K <= 64): centre bound from the dk bounds (measured: fewer fallbacks)
   bool chunk_fb_all = false;       // test knob: the lane-select chunk kernel hands every query to its fallback
+  bool knn_all_general = false;    // GI_KNN_GENERAL=1: k-NN instances with the general estimate form only
   bool use_dk = true;              // wave k-NN kernel starts from per-photon K-th bounds
   DBuf qseg[2];  // K-best lists of the query-per-wave k-NN path
   size_t qcap_hint[2] = {0, 0};
@@ -815,6 +816,22 @@ hipError_t read_stats(gi_ctx *c, unsigned long long *out) {
   return e;
 }
 
+// KnnArgs::general: 0 when the map's filter is the disk and no material a query can carry (kd or
+// the diffuse flag: queries sit on diffuse hits) has a specular term -- the device's test for the
+// estimate's common form (photon_utils.cpp:98-158; gi_knn.hip wave_estimate) -- so the k-NN
+// kernels can run their instances without pow
+// (every_material: also those no render query can carry -- the estimate seam's per-query ones)
+static int knn_general(const std::vector<DMaterial> &mats, int filter, bool every_material = false) {
+  if (filter != 0) return 1;
+  for (const DMaterial &m : mats) {
+    if (!every_material && !(m.flags & MF_DIFFUSE) && m.max_kd == 0.0) continue;
+    const bool spec = (m.flags & MF_SPECULAR) || (m.n < 0);
+    if (spec || !std::isfinite(m.ks[0]) || !std::isfinite(m.ks[1]) || !std::isfinite(m.ks[2]))
+      return 1;
+  }
+  return 0;
+}
+
 KnnArgs knn_args(gi_ctx *c, int mi) {
   KnnArgs k;
   memset(&k, 0, sizeof k);
@@ -835,6 +852,7 @@ KnnArgs knn_args(gi_ctx *c, int mi) {
   k.sel_slack = c->sel_slack;
   k.chunk_minsub = c->chunk_minsub;
   k.qpl = c->knn_qpl;
+  k.general = c->knn_all_general ? 1 : knn_general(c->scene.mats, k.filter);
   if (const char *s = getenv("GI_KNN_DBG")) k.dbg = atoi(s);
   return k;
 }
@@ -1576,6 +1594,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_CHUNK_MINSUB_BIG")) c->chunk_minsub_big = std::min(64, std::max(1, atoi(s)));
   if (const char *s = getenv("GI_CHUNK_MINSUB")) c->chunk_minsub = std::min(64, std::max(1, atoi(s)));
   if (const char *s = getenv("GI_SPLIT_IND")) c->split_ind = atoi(s) != 0;
+  if (const char *s = getenv("GI_KNN_GENERAL")) c->knn_all_general = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_DK")) c->use_dk = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_DK")) c->chunk_dk = atoi(s) != 0;
   if (const char *s = getenv("GI_MC_SUB")) c->mc_sub = atoi(s) != 0;
@@ -2261,6 +2280,7 @@ int gi_estimate_radiance_batch(gi_ctx *c, int map, int64_t n, const gi_radiance_
   k.mats = dm.as<DMaterial>();
   k.K = q[0].k;
   k.filter = q[0].filter;
+  k.general = c->knn_all_general ? 1 : knn_general(mats, k.filter, true);  // the batch's own materials
   k.r2f = (float)(q[0].max_dist * q[0].max_dist);
   k.rmax = q[0].max_dist;
   k.qpos = dq.as<float4>();

@@ -289,7 +289,10 @@ struct KnnArgs {
   int32_t chunk_minsub;    // chunk kernel: smallest query group an overflowing chunk is split to
   int32_t qpl;             // per-lane kernel: consecutive (sorted) queries per lane
   int32_t dbg;             // diagnostics: chunk kernel phase skips (timing only)
-  int32_t pad4;
+  int32_t general;         // 1: a query may need EstimateRadiance's general form (pow: specular
+                           // term, cone / Gauss filter); 0: host-checked that the disk filter and
+                           // diffuse-only materials serve every query (knn_general), and the
+                           // kernels run instances without the general form (fewer registers)
   float r2f;               // (float)(r*r) accept radius
   double rmax;
   double fa, fb, fk;       // FILTER_CONST_A/B/K

@@ -163,7 +163,7 @@ __device__ __forceinline__ void select_k(uint64_t *buf, uint32_t *hist, int lane
 // num K-best photons (fetch_id(s), fetch_d2(s) for s < num), one wave per query: photons spread
 // over the lanes, fp64 partial sums reduced across the wave (butterfly). Shared by the
 // list-estimate kernel and the wave kernel's fused estimate, so both sum in the same order.
-template <typename FetchId, typename FetchD2>
+template <bool GEN = true, typename FetchId, typename FetchD2>
 __device__ __forceinline__ void wave_estimate(const KnnArgs &a, int64_t qi, float4 qp, int num,
                                               FetchId fetch_id, FetchD2 fetch_d2) {
   const int lane = threadIdx.x;
@@ -255,6 +255,8 @@ __device__ __forceinline__ void wave_estimate(const KnnArgs &a, int64_t qi, floa
             o0 += p0; o1 += p1; o2 += p2;
           }
         }
+      } else if constexpr (!GEN) {
+        o0 = o1 = o2 = __builtin_nan("");  // see chunk_estimate: the host's check failed
       } else
       for (int s = lane; s < num; s += 64) {
         uint32_t id = fetch_id(s);
@@ -332,7 +334,7 @@ __device__ __forceinline__ void wave_estimate(const KnnArgs &a, int64_t qi, floa
 #ifndef SWEEP_H
 #define SWEEP_H 6
 #endif
-template <int CAP, int LB, bool PROF, bool FUSE, bool SWEEP>
+template <int CAP, int LB, bool PROF, bool FUSE, bool SWEEP, bool GEN = true>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FUSE ? WAVE_WPE : 1)))
 void knn_wave_kernel(KnnArgs a) {
   __shared__ uint64_t buf[CAP];
@@ -680,7 +682,7 @@ void knn_wave_kernel(KnnArgs a) {
         a.out_dk[qi] = (num < K) ? INFINITY : __double2float_ru(sqrt((double)km * (1.0 + 1e-5)));
     } else if (FUSE) {
       // the estimate straight from the K best keys in LDS (no list round trip through HBM)
-      wave_estimate(a, qi, qp, num, [&](int s) { return (uint32_t)buf[s]; },
+      wave_estimate<GEN>(a, qi, qp, num, [&](int s) { return (uint32_t)buf[s]; },
                     [&](int s) { return __uint_as_float((uint32_t)(buf[s] >> 32)); });
     } else {
       for (int s = lane; s < K; s += 64) {
@@ -1036,6 +1038,14 @@ void launch_list_estimate(const KnnArgs &a, hipStream_t st) {
 #endif
 template <bool PROF, bool FUSE, bool SWEEP>
 bool wave_launch(const KnnArgs &a, int need, unsigned grid, hipStream_t st) {
+  if (!PROF && FUSE && SWEEP && !a.general) {  // without the estimate's general form
+    if (need <= 128) knn_wave_kernel<128, 1, false, true, true, false><<<grid, 64, 0, st>>>(a);
+    else if (need <= 256) knn_wave_kernel<256, 1, false, true, true, false><<<grid, 64, 0, st>>>(a);
+    else if (need <= 512) knn_wave_kernel<512, WAVE_LB, false, true, true, false><<<grid, 64, 0, st>>>(a);
+    else if (need <= 1024) knn_wave_kernel<1024, WAVE_LB, false, true, true, false><<<grid, 64, 0, st>>>(a);
+    else return false;
+    return true;
+  }
   if (need <= 128) knn_wave_kernel<128, 1, PROF, FUSE, SWEEP><<<grid, 64, 0, st>>>(a);
   else if (need <= 256) knn_wave_kernel<256, 1, PROF, FUSE, SWEEP><<<grid, 64, 0, st>>>(a);
   else if (need <= 512) knn_wave_kernel<512, WAVE_LB, PROF, FUSE, SWEEP><<<grid, 64, 0, st>>>(a);

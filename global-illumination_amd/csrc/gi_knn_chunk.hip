@@ -552,7 +552,7 @@ __device__ __forceinline__ void to_fallback(const KnnArgs &a, uint64_t vmask, bo
 
 // ---- 4. the estimate of one query from LDS-staged photons (slot_at(s) = s-th kept slot).
 //         EstimateRadiance photon_utils.cpp:72-162 / irradiance :209-246
-template <int CAPC, typename SlotAt>
+template <bool GEN, int CAPC, typename SlotAt>
 __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, float4 qp, int num,
                                                float km, const Cands<CAPC> &cpos, const uint32_t *crgbe,
                                                SlotAt slot_at) {
@@ -632,6 +632,10 @@ __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, flo
           }
         }
         o0 *= kd0; o1 *= kd1; o2 *= kd2;
+      } else if constexpr (!GEN) {
+        // an instance without the general form (KnnArgs::general == 0) met a query that needs
+        // it: the host's check failed; make the result unmistakable
+        o0 = o1 = o2 = __builtin_nan("");
       } else {
       // one photon per step here: this path calls pow (specular term, Gauss filter), and a
       // group of photons held across those calls would cost the whole kernel registers
@@ -941,7 +945,7 @@ __device__ __forceinline__ float next_down(float x) { return __uint_as_float(__f
 // CAPC = 240 (first pass): 10,112 B of LDS per wave, so 16 waves (4 per SIMD, the VGPR limit)
 // fit in a CU's 160 KiB (256 candidates took 10,752 B: 14 waves); u8 slots and u8 counters.
 // CAPC = 480 (second pass over the first's overflowing chunks): u16 slots and counters, 19.8 KB.
-template <int WPE, bool PROF, int CAPC = 240>
+template <int WPE, bool PROF, int CAPC = 240, bool GEN = true>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE)))
 void knn_chunk_lane_kernel(KnnArgs a) {
   using SlotT = typename std::conditional<(CAPC < 256), uint8_t, uint16_t>::type;
@@ -1165,7 +1169,7 @@ void knn_chunk_lane_kernel(KnnArgs a) {
     if (!(a.dbg & 2)) {
       auto slot_at = [&](int s) { return (uint32_t)sel[s * 64 + lane]; };
       chunk_estimate_shared<CAPC>(a, lane, col, qi, qp, n, km, count, cpos, crgbe, cand_lds, slot_at,
-                                  [&]() { chunk_estimate(a, qi, qp, n, km, cpos, crgbe, slot_at); });
+                                  [&]() { chunk_estimate<GEN>(a, qi, qp, n, km, cpos, crgbe, slot_at); });
     }
     if (col) {
       st_q += 1;
@@ -1190,7 +1194,7 @@ void knn_chunk_lane_kernel(KnnArgs a) {
 // comes from the per-photon K-th distance bounds (KdView::dk), which the host requires here.
 // Overflowing chunks and unresolved queries go to the one-query-per-wave kernel.
 // ---------------------------------------------------------------------------------------------
-template <int CAPC, bool PROF>
+template <int CAPC, bool PROF, bool GEN = true>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
 void knn_chunk_big_kernel(KnnArgs a) {
   constexpr int NW = CAPC / 32;
@@ -1391,7 +1395,7 @@ void knn_chunk_big_kernel(KnnArgs a) {
         return wi * 32u + b;
       };
       chunk_estimate_shared<CAPC>(a, lane, col, qi, qp, n, km, count, cpos, crgbe, cand_lds, slot_at,
-                                  [&]() { chunk_estimate(a, qi, qp, n, km, cpos, crgbe, slot_at); });
+                                  [&]() { chunk_estimate<GEN>(a, qi, qp, n, km, cpos, crgbe, slot_at); });
     }
     if (col) {
       st_q += 1;
@@ -1443,10 +1447,12 @@ bool launch_knn_chunk_big(const KnnArgs &a, int cap, hipStream_t st) {
     else knn_chunk_big_kernel<384, false><<<grid, 64, 0, st>>>(a);
   } else if (cap <= 512) {
     if (prof) knn_chunk_big_kernel<512, true><<<grid, 64, 0, st>>>(a);
-    else knn_chunk_big_kernel<512, false><<<grid, 64, 0, st>>>(a);
+    else if (a.general) knn_chunk_big_kernel<512, false><<<grid, 64, 0, st>>>(a);
+    else knn_chunk_big_kernel<512, false, false><<<grid, 64, 0, st>>>(a);
   } else {
     // second pass over the first pass's overflowing chunks: 32 KiB of LDS per wave
-    knn_chunk_big_kernel<1024, false><<<grid, 64, 0, st>>>(a);
+    if (a.general) knn_chunk_big_kernel<1024, false><<<grid, 64, 0, st>>>(a);
+    else knn_chunk_big_kernel<1024, false, false><<<grid, 64, 0, st>>>(a);
   }
   return true;
 }
@@ -1456,7 +1462,8 @@ bool launch_knn_chunk_big(const KnnArgs &a, int cap, hipStream_t st) {
 bool launch_knn_chunk2(const KnnArgs &a, hipStream_t st) {
   if (a.nq == 0) return true;
   if (a.mode == KNN_MODE_LIST || a.K > 64) return false;
-  knn_chunk_lane_kernel<2, false, 480><<<knn_chunk_grid(a.nq), 64, 0, st>>>(a);
+  if (a.general) knn_chunk_lane_kernel<2, false, 480><<<knn_chunk_grid(a.nq), 64, 0, st>>>(a);
+  else knn_chunk_lane_kernel<2, false, 480, false><<<knn_chunk_grid(a.nq), 64, 0, st>>>(a);
   return true;
 }
 
@@ -1470,7 +1477,8 @@ bool launch_knn_chunk(const KnnArgs &a, hipStream_t st) {
   unsigned grid = knn_chunk_grid(a.nq);
   // GI_KNN_DBG & 128: phase counters from the large-K kernel only
   if ((a.dbg & 16) && !(a.dbg & 128)) knn_chunk_lane_kernel<3, true><<<grid, 64, 0, st>>>(a);
-  else knn_chunk_lane_kernel<LANE_WPE, false><<<grid, 64, 0, st>>>(a);
+  else if (a.general) knn_chunk_lane_kernel<LANE_WPE, false><<<grid, 64, 0, st>>>(a);
+  else knn_chunk_lane_kernel<LANE_WPE, false, 240, false><<<grid, 64, 0, st>>>(a);
   return true;
 }
 

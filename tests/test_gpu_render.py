@@ -315,3 +315,30 @@ def test_batch_rerun_on_slot_guard_is_exact(monkeypatch):
         assert out[0][1][k] == out[1][1][k], k
     o, _ = oracle_lib.render(args, w, h)
     compare_exact(out[1][2], o)
+
+
+def test_knn_instances_without_general_form_are_exact(monkeypatch):
+    """The k-NN kernels run instances compiled without EstimateRadiance's general form (pow:
+    specular term, cone / Gauss filters; KnnArgs::general == 0) when the host finds the disk
+    filter and diffuse-only query materials (cornell.scn: the walls; the glass sphere takes no
+    queries). Forcing the general instances (GI_KNN_GENERAL=1) gives the same f32 image and
+    counters."""
+    args = [scene("cornell.scn"), "/tmp/x.png", "-resolution", "40", "30", "-aa", "1",
+            "-global", "50000", "-caustic", "100000", "-it", "16", "-tt", "8", "-st", "8",
+            "-seed", "4"]
+    p, sc, _o, w, h, aa, real = gi_amd.ParseArgs(args)
+    out = []
+    for gen in ("0", "1"):
+        monkeypatch.setenv("GI_KNN_GENERAL", gen)
+        r = gi_amd.Renderer(0, p)
+        try:
+            r.ReadScene(sc, real)
+            r.MapPhotons()
+            _rgb, f, st = r.RenderImage(aa, w, h, want_float=True)
+            out.append((f, st))
+        finally:
+            r.close()
+    assert np.isfinite(out[0][0]).all()
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    for k in ("knn_queries", "knn_photons", "caustic_samples", "indirect_samples"):
+        assert out[0][1][k] == out[1][1][k], k

@@ -6,7 +6,8 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 R=${ROUND:-r01}
 mkdir -p gpurun_out/full
-GI_PARITY_LOG=$GRAFT_REPO_ROOT/gpurun_out/full/parity_l2.jsonl timeout -k 10 900 python -u -m pytest ${PYTEST_TARGET:-tests} -x -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/full/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/full/pytest_gpu.log; exit 1; }
+rm -f gpurun_out/full/parity_l2.jsonl
+GI_PARITY_LOG=$GRAFT_REPO_ROOT/gpurun_out/full/parity_l2.jsonl timeout -k 10 900 python -u -m pytest ${PYTEST_TARGET:-tests} -x -v --durations=10 -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/full/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/full/pytest_gpu.log; exit 1; }
 tail -2 gpurun_out/full/pytest_gpu.log
 # FETCH_SIZE pass first, so the bench line below carries roofline.traffic from it
 timeout -k 10 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/full/pmc -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/full/pmc.log 2>&1 || { tail -20 gpurun_out/full/pmc.log; exit 1; }

@@ -13,6 +13,11 @@
 namespace gi {
 
 #define GI_HD __host__ __device__ __forceinline__
+// pow out of line: the Phong / spot terms call it from the path megakernels, where gi_math.h's
+// inlined pow (log and exp in double-double) made the 256-VGPR kernels spill
+__host__ __device__ __attribute__((noinline)) static double pow_ool(double x, double y) {
+  return gm::pow(x, y);
+}
 
 constexpr double kEps = 1.0e-6;     // RN_EPSILON, RNScalar.cpp:21
 constexpr double kInf = 1.0e6;      // RN_INFINITY, RNScalar.cpp:22
@@ -886,7 +891,7 @@ __device__ __noinline__ void soft_light(const SceneView &S, const DLight &L, C3 
         V R = (2.0 * NL) * nrm - Ld;
         double VR = dot(Vv, R);
         if (isNegOrZero(VR)) continue;
-        w += (I * gm::pow(VR, m.n));
+        w += (I * pow_ool(VR, m.n));
       }
     }
     if (hits > 0) color += w * ldc(m.ks) * ldc(L.color) * L.area / (double)hits;
@@ -922,7 +927,7 @@ __device__ __forceinline__ C3 light_reflection_hard(const DLight &L, const DMate
       V ML = normalize(p - lp);
       double ca = dot(ML, ld3(L.dir));
       if (gm::cos(L.cutoff) > ca) I = 0.0;
-      else I = I * gm::pow(ca, L.dropoff);
+      else I = I * pow_ool(ca, L.dropoff);
     }
     V Ld = normalize(lp - p);
     double NL = dot(nrm, Ld);
@@ -930,7 +935,7 @@ __device__ __forceinline__ C3 light_reflection_hard(const DLight &L, const DMate
     V Vv = normalize(eye - p);
     double VR = dot(Vv, R);
     C3 o = I * Dc * Ic * fabs(NL);
-    if (isPos(VR)) o += (I * gm::pow(VR, s)) * Sc * Ic;
+    if (isPos(VR)) o += (I * pow_ool(VR, s)) * Sc * Ic;
     return o;
   }
   if (L.kind == LK_DIR) {
@@ -941,7 +946,7 @@ __device__ __forceinline__ C3 light_reflection_hard(const DLight &L, const DMate
     V Vv = normalize(eye - p);
     double VR = dot(Vv, R);
     C3 o = (I * fabs(NL)) * Dc * Ic;
-    if (isPos(VR)) o += (I * gm::pow(VR, s) * Sc * Ic);
+    if (isPos(VR)) o += (I * pow_ool(VR, s) * Sc * Ic);
     return o;
   }
   return rgb(0, 0, 0);
@@ -994,7 +999,7 @@ __device__ __noinline__ C3 light_reflection(const DLight &L, const DMaterial &m,
         V Vv = normalize(eye - p);
         double VR = dot(Vv, R);
         if (isNegOrZero(VR)) continue;
-        sum += (I * gm::pow(VR, s) * Sc * Ic);
+        sum += (I * pow_ool(VR, s) * Sc * Ic);
       }
     }
     C3 mean = sum;

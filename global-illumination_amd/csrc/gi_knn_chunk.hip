@@ -1194,8 +1194,11 @@ void knn_chunk_lane_kernel(KnnArgs a) {
 // comes from the per-photon K-th distance bounds (KdView::dk), which the host requires here.
 // Overflowing chunks and unresolved queries go to the one-query-per-wave kernel.
 // ---------------------------------------------------------------------------------------------
+#ifndef BIG_WPE
+#define BIG_WPE 3  // large-K chunk kernel occupancy target (waves per SIMD)
+#endif
 template <int CAPC, bool PROF, bool GEN = true>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BIG_WPE)))
 void knn_chunk_big_kernel(KnnArgs a) {
   constexpr int NW = CAPC / 32;
   // bracket list length: 8 keeps the 512-candidate kernel at 17.6 KB of LDS (9 waves per CU)

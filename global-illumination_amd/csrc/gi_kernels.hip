@@ -733,8 +733,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(W))) void i
 // fill (the fills are known only on the device). At-hit entries (mat >= 0): shading of the
 // first hit, then MonteCarlo_IndirectSample's loop from iteration 1 on; ray entries
 // (mat == -1): the whole loop, its contribution added to the Monte Carlo path's base.
+// occupancy: 3 waves per SIMD; scenes with meshes / boxes (C4: 148 VGPRs spilled at 3) get 2
 template <uint32_t KINDS>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3)))
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu((KINDS & ~KINDS_TRI_SPHERE) ? 2 : 3)))
 void ind_cont_kernel(RenderArgs a, const IndCont *queue, const uint32_t *fill, uint32_t cap_s) {
   const uint32_t stripe = blockIdx.x % IND_QS, part = blockIdx.x / IND_QS;
   const uint32_t parts = gridDim.x / IND_QS;

@@ -127,10 +127,13 @@ KNN_KINDS = {
 }
 
 # CPU-baseline calibration: the restatement vs the reference binary on the
-# survey's C2 sample (cornell 64x64 aa=0, 1M + 1M photons, 8 threads) in the build container:
-# restatement render 52.70 s (this repo, tests/oracle_lib.py), reference 72.62 s (SURVEY.md
-# section 6). ratio = restatement time / reference time; DESIGN.md section 7 explains the gap.
-CPU_CALIBRATION = {"ratio": round(52.70 / 72.62, 3), "restatement_s": 52.70, "reference_s": 72.62,
+# survey's C2 sample (cornell 64x64 aa=0, 1M + 1M photons, 8 threads) in the build container.
+# Round-5 measurement (tools/cpu_calibration.py -> profiles/r05_cpu_calibration.json): restatement
+# render 81.42 s (best of two), reference 72.62 s. ratio = restatement time /
+# reference time, inside BASELINE.md's 0.8-1.25 band; DESIGN.md section 7 explains the drift from
+# round 2's 52.70 s. reference_equivalent_value = value x ratio (the reference's rate).
+CPU_CALIBRATION = {"ratio": round(81.417 / 72.62, 3), "restatement_s": 81.417, "reference_s": 72.62,
+                   "measured": "r05, profiles/r05_cpu_calibration.json",
                    "sample": "cornell 64x64 aa=0 1M+1M photons, 8 threads, build container"}
 
 

@@ -265,8 +265,9 @@ struct MapExec {
 struct gi_ctx {
   int device = 0;
   // Device set (gi_create_devices): this context drives the first device and forwards every
-  // call to one context per further device. Output tiles t go to device t % ndev; photon
-  // emission ranges are split across the devices; the maps are built once and replicated.
+  // call to one context per further device. Output tile (tx, ty) goes to device (tx + ty) % ndev
+  // (shard_pixels' diagonal deal); photon emission ranges are split across the devices; the maps
+  // are built once and replicated.
   std::vector<gi_ctx *> peers;
   std::vector<ncclComm_t> comms;     // [ndev] RCCL communicators (distinct devices), else empty
   DBuf pack;                         // this device's shard pixels, packed for the gather
@@ -329,7 +330,10 @@ struct gi_ctx {
   int chunk_minsub_big2 = 64;        // ... its overflowing chunks retried down to this group size
   bool chunk_dk = true;            // chunk kernel (K <= 64): centre bound from the dk bounds (measured: fewer fallbacks)
   bool chunk_fb_all = false;       // test knob: the lane-select chunk kernel hands every query to its fallback
-  bool knn_all_general = false;    // GI_KNN_GENERAL=1: k-NN instances with the general estimate form only
+  // k-NN instances: 0 auto (knn_general), 1 the general estimate form only (GI_KNN_GENERAL=1,
+  // and after an instance without it met a query that needed it), -1 test knob: claim that no
+  // render query needs it (GI_KNN_GENERAL=-1; exercises render_common's re-run)
+  int knn_general_mode = 0;
   bool use_dk = true;              // wave k-NN kernel starts from per-photon K-th bounds
   DBuf qseg[2];  // K-best lists of the query-per-wave k-NN path
   size_t qcap_hint[2] = {0, 0};
@@ -852,7 +856,7 @@ KnnArgs knn_args(gi_ctx *c, int mi) {
   k.sel_slack = c->sel_slack;
   k.chunk_minsub = c->chunk_minsub;
   k.qpl = c->knn_qpl;
-  k.general = c->knn_all_general ? 1 : knn_general(c->scene.mats, k.filter);
+  k.general = c->knn_general_mode > 0 ? 1 : c->knn_general_mode < 0 ? 0 : knn_general(c->scene.mats, k.filter);
   if (const char *s = getenv("GI_KNN_DBG")) k.dbg = atoi(s);
   return k;
 }
@@ -1594,7 +1598,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_CHUNK_MINSUB_BIG")) c->chunk_minsub_big = std::min(64, std::max(1, atoi(s)));
   if (const char *s = getenv("GI_CHUNK_MINSUB")) c->chunk_minsub = std::min(64, std::max(1, atoi(s)));
   if (const char *s = getenv("GI_SPLIT_IND")) c->split_ind = atoi(s) != 0;
-  if (const char *s = getenv("GI_KNN_GENERAL")) c->knn_all_general = atoi(s) != 0;
+  if (const char *s = getenv("GI_KNN_GENERAL")) c->knn_general_mode = std::max(-1, std::min(1, atoi(s)));
   if (const char *s = getenv("GI_KNN_DK")) c->use_dk = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_DK")) c->chunk_dk = atoi(s) != 0;
   if (const char *s = getenv("GI_MC_SUB")) c->mc_sub = atoi(s) != 0;
@@ -1645,6 +1649,19 @@ int gi_create_devices(gi_ctx **out, const gi_device_set *set) {
   return GI_OK;
 }
 
+// the calling thread's current HIP device, restored on scope exit (the packed entry points run
+// inside processes whose torch shares that device setting)
+struct DeviceScope {
+  int prev = -1;
+  explicit DeviceScope(int d) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    hipSetDevice(d);
+  }
+  ~DeviceScope() {
+    if (prev >= 0) hipSetDevice(prev);
+  }
+};
+
 // the render's and the photon tracer's device scratch (everything but the scene, the maps, the
 // counters and the streams); the next call re-allocates what it needs
 static void release_scratch(gi_ctx *c) {
@@ -1677,6 +1694,7 @@ static void release_scratch(gi_ctx *c) {
 
 int gi_release_scratch(gi_ctx *c) {
   if (!c) return GI_ERR_ARG;
+  DeviceScope scope(c->device);  // the caller's current device is restored on return
   for (gi_ctx *d : c->peers) {
     hipSetDevice(d->device);
     hipDeviceSynchronize();
@@ -1987,13 +2005,36 @@ static int render_common(gi_ctx *c, int aa, int w, int h, const std::vector<int3
   c->p2_q[0] = c->p2_q[1] = 0;
   c->last_kind[0] = c->last_kind[1] = -1;
   gi_render_stats local;
-  memset(&local, 0, sizeof local);
-  rc = render_pixels(c, aa, w, h, pix, &local);
-  if (rc) return rc;
+  unsigned long long s[ST_COUNT];
+  for (int pass = 0;; pass++) {
+    memset(&local, 0, sizeof local);
+    rc = render_pixels(c, aa, w, h, pix, &local);
+    if (rc) return rc;
+    HIPCHK(c, read_stats(c, s));
+    if (s[ST_GEN_MISS] == 0) break;
+    // a k-NN instance without the general estimate form (KnnArgs::general == 0, knn_general)
+    // met a query that needed it and wrote NaN: the host's material check missed a query site.
+    // Render again with the general instances only (kept for this context), never return NaN.
+    if (pass > 0 || c->knn_general_mode > 0)
+      return fail(c, GI_ERR_STATE, "k-NN estimate: general-form query in a general instance");
+    fprintf(stderr, "[gi] %llu k-NN queries needed the general estimate form; re-rendering with "
+            "the general k-NN instances\n", s[ST_GEN_MISS]);
+    c->knn_general_mode = 1;
+    if (keep_rgbf && rgbf) {
+      HIPCHK(c, hipMemcpyAsync(c->rgbf.p, rgbf, npx * 4, hipMemcpyHostToDevice, c->stream));
+    } else {
+      HIPCHK(c, hipMemsetAsync(c->rgbf.p, 0, npx * 4, c->stream));
+    }
+    HIPCHK(c, hipMemsetAsync(c->rgb8.p, 0, npx, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_stats.p, 0, ST_BYTES, c->stream));
+    c->fb_ms[0] = c->fb_ms[1] = 0;
+    c->fb_q[0] = c->fb_q[1] = 0;
+    c->p2_ms[0] = c->p2_ms[1] = 0;
+    c->p2_q[0] = c->p2_q[1] = 0;
+  }
   if (rgbf) HIPCHK(c, hipMemcpyAsync(rgbf, c->rgbf.p, npx * 4, hipMemcpyDeviceToHost, c->stream));
   if (rgb8) HIPCHK(c, hipMemcpyAsync(rgb8, c->rgb8.p, npx, hipMemcpyDeviceToHost, c->stream));
-  unsigned long long s[ST_COUNT];
-  HIPCHK(c, read_stats(c, s));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   if (const char *kd = getenv("GI_KNN_DBG"); kd && (atoi(kd) & 16)) {
     fprintf(stderr, "[gi] k-NN phase cycles (sum over waves):");
     for (int i = 0; i < 16; i++) fprintf(stderr, " %llu", s[ST_PHASE + i]);
@@ -2175,19 +2216,6 @@ int gi_render_tiles(gi_ctx *c, int aa, int w, int h, int tile, int shard, int ns
 
 // One rank's shard, left on the device and packed (torchrun: each rank gathers these buffers to
 // rank 0 over RCCL and rank 0 composes them with gi_compose_tiles; nothing else crosses).
-// the calling thread's current HIP device, restored on scope exit (the packed entry points run
-// inside processes whose torch shares that device setting)
-struct DeviceScope {
-  int prev = -1;
-  explicit DeviceScope(int d) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    hipSetDevice(d);
-  }
-  ~DeviceScope() {
-    if (prev >= 0) hipSetDevice(prev);
-  }
-};
-
 int gi_render_tiles_packed(gi_ctx *c, int aa, int w, int h, int tile, int shard, int nshards,
                            void *packed, int64_t cap, int64_t *npix, gi_render_stats *st) {
   if (!c || !npix || tile <= 0 || nshards <= 0 || shard < 0 || shard >= nshards || w <= 0 || h <= 0)
@@ -2280,7 +2308,7 @@ int gi_estimate_radiance_batch(gi_ctx *c, int map, int64_t n, const gi_radiance_
   k.mats = dm.as<DMaterial>();
   k.K = q[0].k;
   k.filter = q[0].filter;
-  k.general = c->knn_all_general ? 1 : knn_general(mats, k.filter, true);  // the batch's own materials
+  k.general = c->knn_general_mode > 0 ? 1 : knn_general(mats, k.filter, true);  // the batch's own materials
   k.r2f = (float)(q[0].max_dist * q[0].max_dist);
   k.rmax = q[0].max_dist;
   k.qpos = dq.as<float4>();
@@ -2409,7 +2437,7 @@ int gi_knn_bench(gi_ctx *c, int map, int64_t n, const double *pts, const double 
 int gi_math_probe(gi_ctx *c, int fn, int64_t n, const double *x, const double *y, double *out) {
   if (!c || n < 0 || fn < 0 || fn > 7 || (n > 0 && (!x || !y || !out))) return GI_ERR_ARG;
   if (n == 0) return GI_OK;
-  hipSetDevice(c->device);
+  DeviceScope scope(c->device);
   DBuf dx, dy, dout;
   HIPCHK(c, upload(dx, x, (size_t)n * 8, c->stream));
   HIPCHK(c, upload(dy, y, (size_t)n * 8, c->stream));

@@ -67,6 +67,7 @@ enum {
   ST_RAY = 0, ST_SHADOW, ST_MONTE, ST_TRANS, ST_SPEC, ST_INDIRECT, ST_CAUSTIC,
   ST_KNN, ST_KNN_PHOTONS, ST_KNN_VISITED,        // global map (caustic map: + ST_KNN_MAP)
   ST_KNN_C, ST_KNN_C_PHOTONS, ST_KNN_C_VISITED,
+  ST_GEN_MISS,   // queries an instance without the general estimate form met (host re-runs)
   ST_PHASE = 16,                                 // 16 diagnostic counters (GI_KNN_DBG & 16)
   ST_COUNT = 32
 };

@@ -1858,6 +1858,12 @@ void launch_path(const RenderArgs &a, hipStream_t st, hipStream_t st2, hipEvent_
     if (a.mc_next) (void)hipMemsetAsync(a.mc_next, 0, sizeof(uint32_t), st);
     if (a.mc_cont2) (void)hipMemsetAsync(a.mc_ncont2, 0, IND_QS * 32 * sizeof(uint32_t), st);
   }
+  // the same for the indirect continuation queue's counters: cleared before the fork, not after
+  // it on st, where the fill waited for the persistent Monte Carlo kernel (whose 1,024 blocks of
+  // 256-VGPR waves take every SIMD's registers) to release a CU -- C3's 40-162 ms single fills,
+  // 725 ms over two frames
+  if (a.total_ind > 0 && a.split_ind)
+    (void)hipMemsetAsync(a.ind_ncont, 0, IND_QS * 32 * sizeof(uint32_t), st);
   if (side) {
     (void)hipEventRecord(fork, st);
     (void)hipStreamWaitEvent(st2, fork, 0);
@@ -1901,7 +1907,6 @@ void launch_path(const RenderArgs &a, hipStream_t st, hipStream_t st2, hipEvent_
   if (a.nprim > 0) slot0_kernel<<<nblk(a.nprim, 256), 256, 0, st>>>(a);
   if (a.total_ind > 0) {
     unsigned g = nblk(a.tind, 128);
-    if (a.split_ind) (void)hipMemsetAsync(a.ind_ncont, 0, IND_QS * 32 * sizeof(uint32_t), st);
     if (!a.split_ind) ind_kernel<2, false, KINDS_ALL><<<g, 128, 0, st>>>(a);
     else if ((a.S.kinds & ~KINDS_TRI_SPHERE) == 0) launch_ind<KINDS_TRI_SPHERE>(a, g, st);
     else if ((a.S.kinds & ~KINDS_POLY) == 0) launch_ind<KINDS_POLY>(a, g, st);

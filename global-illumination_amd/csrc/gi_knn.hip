@@ -257,6 +257,7 @@ __device__ __forceinline__ void wave_estimate(const KnnArgs &a, int64_t qi, floa
         }
       } else if constexpr (!GEN) {
         o0 = o1 = o2 = __builtin_nan("");  // see chunk_estimate: the host's check failed
+        if (a.stats) atomicAdd(a.stats + ST_GEN_MISS, 1ull);
       } else
       for (int s = lane; s < num; s += 64) {
         uint32_t id = fetch_id(s);

@@ -634,8 +634,10 @@ __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, flo
         o0 *= kd0; o1 *= kd1; o2 *= kd2;
       } else if constexpr (!GEN) {
         // an instance without the general form (KnnArgs::general == 0) met a query that needs
-        // it: the host's check failed; make the result unmistakable
+        // it: the host's check failed. Count it (the host re-runs the render with the general
+        // instances, gi_host.cpp render_common) and make the result unmistakable meanwhile
         o0 = o1 = o2 = __builtin_nan("");
+        if (a.stats) atomicAdd(a.stats + ST_GEN_MISS, 1ull);
       } else {
       // one photon per step here: this path calls pow (specular term, Gauss filter), and a
       // group of photons held across those calls would cost the whole kernel registers

@@ -51,8 +51,9 @@ def shard_sizes(width, height, tile, world):
 
 def gather_tiles_to_rank0(img, owner, dist, device=None):
     """Host path: gather every rank's own pixels of its partial f32 image [h, w, 3] (zeros
-    elsewhere) onto rank 0. Each rank sends a [max_count, 3] buffer (its pixels first, padding
-    after: the shard sizes differ by at most one tile). Returns the full image on rank 0, None
+    elsewhere) onto rank 0. Each rank sends a [max_count, 3] buffer (its pixels first, then
+    padding to the largest shard: with the diagonal deal, tile (tx, ty) on rank (tx + ty) % N,
+    shard sizes can differ by more than one tile). Returns the full image on rank 0, None
     elsewhere."""
     import torch
     rank, world = dist.get_rank(), dist.get_world_size()

@@ -37,5 +37,13 @@ def test_gi_math_special_values():
     assert p[:6].tolist() == [0.0, 1.0, 1.0, -8.0, 4.0, -0.03125]
     assert p[6] == 0.0 and abs(p[7] / 0.0067211119598655882 - 1) < 1e-15
     assert np.isnan(m("pow", [-2.0], [0.5])[0])
+    # signed zero and infinite operands, as glibc's pow (C99 F.9.4.4): -0.0 reaches
+    # pow through EstimateRadiance's clamp `if (ca < 0) ca = 0`
+    xs = [-0.0, -0.0, -0.0, -0.0, 0.0, -np.inf, -np.inf, -np.inf, -1.0, -1.0, 0.5, 2.0, -0.5]
+    ys = [3.0, -3.0, 2.0, 0.5, -2.0, 3.0, 0.5, -3.0, np.inf, -np.inf, np.inf, -np.inf, -np.inf]
+    got = m("pow", xs, ys)
+    with np.errstate(divide="ignore"):
+        want = np.power(np.array(xs), np.array(ys))
+    assert got.tolist() == want.tolist() and (np.signbit(got) == np.signbit(want)).all(), got
     assert m("sin", [0.0, -0.0]).tolist() == [0.0, -0.0] and np.signbit(m("sin", [-0.0])[0])
     assert m("cos", [0.0]).tolist() == [1.0] and m("tan", [0.0]).tolist() == [0.0]

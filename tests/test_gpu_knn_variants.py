@@ -221,3 +221,30 @@ def test_caustic_focus_rim(env, filt, k, r):
     tied = (onn == k + 1) & (od[:, k - 1] == od[:, k])
     assert tied.mean() < 0.01
     np.testing.assert_allclose(g[~tied], o[~tied], rtol=1e-10, atol=1e-300)
+
+
+@pytest.mark.parametrize("name,extra", [
+    ("stilllife.scn", ["-global", "20000", "-caustic", "40000"]),                 # Ks = 1, n = 100
+    ("jensen.scn", ["-global", "5000", "-caustic", "20000", "-cf", "cone", "1.25"]),  # cone filter
+])
+def test_general_form_miss_rerenders(name, extra):
+    """ADVICE r04: an instance without the general estimate form (KnnArgs::general == 0) that
+    meets a query needing it (specular term, cone / Gauss filter) writes NaN and counts it
+    (ST_GEN_MISS); render_common then re-renders with the general instances. GI_KNN_GENERAL=-1
+    makes the host claim that no query needs the general form, so every such query misses: the
+    image must still equal the normal context's, bit for bit, with no NaN."""
+    from gpu_util import run_gpu, scene
+    args = [scene(name), "/tmp/x.png", "-resolution", "24", "24", "-aa", "0", "-it", "8",
+            "-tt", "4", "-st", "4", "-lt", "4", "-ss", "4", "-seed", "2"] + extra
+    outs = []
+    for env in ({}, {"GI_KNN_GENERAL": "-1"}):
+        r = make_renderer(env)
+        try:
+            g, f, st, _ = run_gpu(r, args, want_float=True)
+            assert np.isfinite(f).all()
+            outs.append((g, st))
+        finally:
+            r.close()
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    for key in ("knn_queries", "knn_photons", "shadow_rays", "monte_carlo_rays"):
+        assert outs[0][1][key] == outs[1][1][key], key

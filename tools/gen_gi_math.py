@@ -395,15 +395,20 @@ GM_HD double pow5(double x) {{ const double x2 = x * x; return (x2 * x2) * x; }}
 GM_HD double pow(double x, double y) {{
   if (y == 0.0 || x == 1.0) return 1.0;
   if (x != x || y != y) return x + y;
-  double sign = 1.0;
-  if (x < 0.0) {{
-    if (rint(y) != y) return (x - x) / (x - x);  // negative base, non-integer exponent: NaN
-    const double h = 0.5 * y;
-    if (rint(h) != h) sign = -1.0;                  // odd integer exponent
-    x = -x;
+  const double ax = fabs(x);
+  if (y == (double)INFINITY || y == -(double)INFINITY) {{  // C99 F.9.4.4, as glibc
+    if (ax == 1.0) return 1.0;
+    return (ax < 1.0) == (y < 0.0) ? (double)INFINITY : 0.0;
   }}
-  if (x == 0.0) return y > 0.0 ? 0.0 * sign : sign / 0.0;
-  if (x == (double)INFINITY) return y > 0.0 ? sign * x : 0.0 * sign;
+  // an odd integer exponent keeps the sign of the base, -0.0 included (signbit, not x < 0:
+  // EstimateRadiance's clamp `if (ca < 0) ca = 0` leaves ca = -0.0 in place)
+  const bool yint = rint(y) == y;
+  const bool odd = yint && rint(0.5 * y) != 0.5 * y;
+  const double sign = (odd && __builtin_signbit(x)) ? -1.0 : 1.0;
+  if (ax == 0.0) return y > 0.0 ? 0.0 * sign : sign / 0.0;
+  if (ax == (double)INFINITY) return y > 0.0 ? sign * ax : 0.0 * sign;
+  if (x < 0.0 && !yint) return (x - x) / (x - x);  // negative base, non-integer exponent: NaN
+  x = ax;
   double lh, ll;
   log_dd(x, lh, ll);
   const double zh = y * lh;

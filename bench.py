@@ -308,8 +308,17 @@ def main():
         except ImportError:
             pass
 
-    for _ in range(a.warmup):
+    # the first frame (the drop-in CLI renders exactly one): its device buffers are sized
+    # before the first batch (gi_host.cpp presize_batches), reported as first_frame_ms
+    first_ms = None
+    for i in range(a.warmup):
+        if i == 0:
+            barrier()
+            tf = time.perf_counter()
         step()
+        if i == 0:
+            barrier()
+            first_ms = round((time.perf_counter() - tf) * 1e3, 1)
     barrier()
     t0 = time.perf_counter()
     keys = ("q0", "q1", "ph0", "ph1", "vis0", "vis1", "ms0", "ms1", "n0", "n1", "fb0", "fb1",
@@ -420,6 +429,8 @@ def main():
                             if rgb is not None else None),
             "roofline": roofline, "cpu_baseline": cpu,
             "step_ms": step_ms,
+            # the first (cold) frame, what the drop-in CLI renders: first warmup step
+            "first_frame_ms": first_ms,
         }
         if shard is not None:
             line["shard"] = {"shard": shard[0], "nshards": shard[1], "pixels": npix_shard,

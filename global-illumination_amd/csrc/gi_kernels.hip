@@ -373,6 +373,9 @@ __device__ __forceinline__ void mc_begin(McLoop &L, V org, V dir, const Rng &rng
   L.iter = 0;
 }
 
+#ifndef MC_ISECT_OOL
+#define MC_ISECT_OOL 0
+#endif
 // One iteration of MonteCarlo_PathTrace's loop (DEFER: indirect sub-paths go to the mc_cont
 // queue). Returns false when the path has ended.
 template <uint32_t KINDS = KINDS_ALL, bool DEFER = false, bool HARD = false>
@@ -385,7 +388,12 @@ __device__ __forceinline__ bool mc_step(PathCtx &P, McLoop &L) {
   Rng &rng = L.rng;
   C3 &tw = L.tw;
   Hit h;
-  if (!scene_intersect<KINDS>(S, L.org, L.dir, h, P.hint)) {
+  bool hit;
+  if constexpr (MC_ISECT_OOL && (KINDS & ~KINDS_TRI_SPHERE) != 0)
+    hit = scene_intersect_ool<KINDS>(S, L.org, L.dir, h, P.hint);
+  else
+    hit = scene_intersect<KINDS>(S, L.org, L.dir, h, P.hint);
+  if (!hit) {
     P.base += W * (tw * ldc(S.background));
     return false;
   }

@@ -110,9 +110,15 @@ def test_full_tile_shard_properties(renderer, cid, res, shard):
         rgb = b[:, :3]
         assert np.isfinite(rgb).all() and rgb.min() >= 0.0 and rgb.max() <= 1.0
         u8 = b[:, 3].view(np.uint32)
-        want = (rgb * 255.0).astype(np.uint32)    # R2Image::SetPixelRGB truncation
-        got = np.stack([u8 & 255, (u8 >> 8) & 255, (u8 >> 16) & 255], -1)
-        assert (got == want).mean() > 0.999
+        got = np.stack([u8 & 255, (u8 >> 8) & 255, (u8 >> 16) & 255], -1).astype(np.int64)
+        # the u8 word is trunc(255 r) of the fp64 pixel value r (R2Image::SetPixelRGB), the f32
+        # words r rounded to fp32: equal truncations except where 255 r lies within fp32
+        # rounding of an integer
+        x = rgb.astype(np.float64) * 255.0
+        want = np.floor(x).astype(np.int64)
+        edge = np.abs(x - np.rint(x)) < 1e-4
+        assert (np.abs(got - want) <= 1).all()
+        assert (got == want)[~edge].all()
         assert st["screen_rays"] > 0
         if cid == "c5":
             assert p.dof_test == 4

@@ -1069,7 +1069,7 @@ __device__ __noinline__ void direct_illumination(const SceneView &S, const Flags
 // spilled around them. Same operations as direct_illumination -> compute_illumination ->
 // illum_test / light_reflection for those light kinds (TestLightIntersection is 0 for them).
 #ifndef HARD_ILLUM_OOL
-#define HARD_ILLUM_OOL 1
+#define HARD_ILLUM_OOL 0  // measured r05: C4 shard 0/8 5,862 -> 6,271 ms with it on (spills 48 -> 20)
 #endif
 template <uint32_t KINDS = KINDS_ALL>
 __device__ __forceinline__ void direct_illumination_hard(const SceneView &S, const Flags &F, V p,
@@ -1086,9 +1086,9 @@ __device__ __forceinline__ void direct_illumination_hard(const SceneView &S, con
     V pol = (L.kind == LK_DIR) ? p - ld3(L.dir) * S.radius * 3.0 : ld3(L.pos);
     double side = dot(nrm, pol - p);
     if ((side > 0 && ct < 0) || (side < 0 && ct > 0)) continue;
-    // the shadow ray's scene walk out of line where the scene has boxes or meshes: inlined next
-    // to the caller's own walk (mc_step), it set mc_kernel<boxes|meshes, hard lights>'s register
-    // footprint (256 VGPRs + 48 spilled at 2 waves per SIMD)
+    // HARD_ILLUM_OOL: the shadow ray's scene walk out of line where the scene has boxes or
+    // meshes (mc_kernel<boxes|meshes, hard lights>: 48 -> 20 spilled VGPRs), measured slower
+    // than the spills it removes (C4 shard 0/8 +7 %), so off
     bool lit;
     if constexpr (HARD_ILLUM_OOL && (KINDS & ~KINDS_TRI_SPHERE) != 0) lit = illum_test<KINDS>(S, p, pol, cnt);
     else lit = illum_test_inl<KINDS>(S, p, pol, cnt);

@@ -44,13 +44,14 @@ static bool alloc_log() {
 struct DBuf {
   void *p = nullptr;
   size_t cap = 0;
-  hipError_t ensure(size_t bytes) {
+  hipError_t ensure(size_t bytes, int line = __builtin_LINE()) {
     if (bytes <= cap && p) return hipSuccess;
     if (alloc_log() && bytes >= ((size_t)64 << 20)) {
       auto t0 = std::chrono::steady_clock::now();
       size_t old = cap;
       hipError_t e = grow(bytes);
-      fprintf(stderr, "[gi] alloc %.2f GB (was %.2f GB): %.1f ms\n", cap / 1e9, old / 1e9,
+      fprintf(stderr, "[gi] alloc %.2f GB (was %.2f GB) at gi_host.cpp:%d: %.1f ms\n", cap / 1e9,
+              old / 1e9, line,
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
       return e;
     }
@@ -310,10 +311,6 @@ struct gi_ctx {
   KdBuildScratch kdb;            // its scratch
   DBuf kd_ph;                    // emission-ordered photons uploaded for the device build
   int wave_cap_mul = 1;
-  // large-K fallback: G queries per wave on one walk (knn_group_kernel, GI_KNN_GROUP; 1 = the
-  // query-per-wave kernel) with GI_GROUP_CAP LDS candidates per query
-  int knn_group = 1;
-  int group_cap = 512;
   int chunk_cap_big = 512;        // large-K chunk kernel: LDS candidates of the first pass
   int chunk_minsub_big = 64;      // large-K chunk kernel: overflowing chunks retried down to this (64: none, measured best)
   int chunk_minsub = 32;          // chunk kernel: overflowing chunks retried as halves (measured best with the dk bound)
@@ -378,7 +375,7 @@ struct gi_ctx {
   bool batch_log = false;            // GI_BATCH_LOG: per-batch sizes and times on stderr
   int64_t query_budget = 400000000;  // photon-map queries per batch (~120 B each: ~48 GB)
   double q_per_prim = 0.0;           // largest queries per primary sample seen so far
-  double qrate[2] = {0.0, 0.0};      // per list: largest queries per primary sample seen so far
+  double mc_app_rate[2] = {0.0, 0.0};  // per list: largest appends per Monte Carlo path seen
   float sbmin[3] = {0, 0, 0}, sbmax[3] = {1, 1, 1};
 };
 
@@ -1025,8 +1022,7 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
       f.perm = dense;
       f.nq = nfb2;
       f.q0 = 0;
-      const bool grouped = c->knn_group > 1 && launch_knn_group(f, c->knn_group, c->group_cap, X.st);
-      if (!grouped && !launch_knn_wave(f, c->wave_cap_mul, X.st))
+      if (!launch_knn_wave(f, c->wave_cap_mul, X.st))
         return fail(c, GI_ERR_ARG, "k-NN launch: unsupported estimate size for this kernel");
       HIPCHK(c, hipGetLastError());
     }
@@ -1413,9 +1409,11 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
         // deterministic slots plus 8 appends per primary
         size_t cap = std::max<size_t>(c->qcap_hint[l], (size_t)qbase[l] + 1024);
         if (attempt == 0) {
-          const double rate = c->qrate[l] > 0.0 ? 1.25 * c->qrate[l] : 0.0;
-          size_t pred = c->qrate[l] > 0.0 ? (size_t)(rate * (double)nprim) + 1024
-                                          : (size_t)qbase[l] + 8 * (size_t)nprim + 1024;
+          // the deterministic slots are known (qbase); the appends come from the batch's
+          // Monte Carlo paths, whose count is known too (total_mc): at the largest appends per
+          // Monte Carlo path seen so far (at least 2), +25 %
+          const double per_mc = std::max(2.0, c->mc_app_rate[l]);
+          size_t pred = (size_t)qbase[l] + (size_t)(1.25 * per_mc * (double)a.total_mc) + 1024;
           cap = std::max(cap, std::min<size_t>(pred, 0xFFFFFFF0u));
         }
         HIPCHK(c, c->qpos[l].ensure(cap * 16));
@@ -1454,7 +1452,9 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
       for (int l = 0; l < 2; l++)
         c->qcap_hint[l] = std::max<size_t>(c->qcap_hint[l], (size_t)(nq[l] * 1.25) + 1024);
       c->q_per_prim = std::max(c->q_per_prim, (double)((uint64_t)nq[0] + nq[1]) / (double)nprim);
-      for (int l = 0; l < 2; l++) c->qrate[l] = std::max(c->qrate[l], (double)nq[l] / (double)nprim);
+      if (a.total_mc > 0)
+        for (int l = 0; l < 2; l++)
+          c->mc_app_rate[l] = std::max(c->mc_app_rate[l], (double)(nq[l] - qbase[l]) / (double)a.total_mc);
       if (ok) break;
       if (attempt == 2) return fail(c, GI_ERR_ALLOC, "query list overflow");
       HIPCHK(c, hipMemcpyAsync(c->d_stats.p, c->stats_bak.p, ST_BYTES,
@@ -1555,7 +1555,7 @@ int upload_scene(gi_ctx *c) {
   c->have_scene = true;
   c->map_valid[0] = c->map_valid[1] = false;
   c->q_per_prim = 0.0;  // the batch size is re-measured on the new scene
-  c->qrate[0] = c->qrate[1] = 0.0;
+  c->mc_app_rate[0] = c->mc_app_rate[1] = 0.0;
   for (int i = 0; i < 3; i++) {
     c->sbmin[i] = (float)H.bmin[i];
     c->sbmax[i] = (float)H.bmax[i];
@@ -1645,8 +1645,6 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_CHUNK_FB_ALL")) c->chunk_fb_all = atoi(s) != 0;
   if (const char *s = getenv("GI_IND_FRAC")) c->ind_frac = std::min(1.0, std::max(1e-6, atof(s)));
   if (const char *s = getenv("GI_KNN_KERNEL")) c->knn_kernel_kind = atoi(s);
-  if (const char *s = getenv("GI_KNN_GROUP")) c->knn_group = std::max(1, atoi(s));
-  if (const char *s = getenv("GI_GROUP_CAP")) c->group_cap = atoi(s);
   *out = c;
   return GI_OK;
 }

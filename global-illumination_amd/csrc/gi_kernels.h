@@ -362,7 +362,6 @@ void launch_segments(const uint64_t *skeys, uint32_t n, uint32_t nprim, uint32_t
 // generic per-lane kernel with its heaps in global scratch (any K; used beyond the LDS kernels)
 void launch_knn(const KnnArgs &a, hipStream_t st);
 bool launch_knn_wave(const KnnArgs &a, int cap_mul, hipStream_t st);
-bool launch_knn_group(const KnnArgs &a, int G, int cap, hipStream_t st);
 bool launch_knn_lane(const KnnArgs &a, hipStream_t st);
 bool launch_knn_chunk(const KnnArgs &a, hipStream_t st);  // K <= 64, lane select
 bool launch_knn_chunk2(const KnnArgs &a, hipStream_t st);  // its 480-candidate second pass

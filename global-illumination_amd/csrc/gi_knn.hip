@@ -706,270 +706,6 @@ void knn_wave_kernel(KnnArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// G queries per wave on one shared walk: the large-K chunk kernel's fallback (the caustic map's
-// focus-rim queries). Those queries come in Morton order (the compacted
-// fallback list keeps each chunk's queries together) and adjacent ones are ~0.002 apart against
-// d_K ~ 0.04, so their K-neighbourhoods nearly coincide, while one query per wave pays the whole
-// dependent chain of node and leaf loads alone. Here a wave takes G consecutive queries and walks
-// the tree once for all of them: a subtree / leaf is entered when it lies within the current
-// bound of ANY of the G queries; each leaf's photons are loaded once and tested against every
-// query (each with its own LDS candidate buffer, threshold and selects). A query's set is still
-// exactly its own K best: every photon of a skipped leaf / subtree lies beyond that query's bound
-// (the box test is the same monotone fp32 sequence as knn_wave_kernel's), the bounds only
-// shrink, and the start bound from the per-photon dk (d_K(q) <= |q - p| + d_K(p)) holds for any
-// photon p. Same walk structure as knn_wave_kernel's SWEEP form (near child first above the sweep
-// height, leaf boxes of a <= 2^SWEEP_H-leaf subtree read one per lane).
-// ---------------------------------------------------------------------------------------------
-#ifndef GROUP_WPE
-#define GROUP_WPE 4
-#endif
-template <int CAP, int G, bool GEN>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GROUP_WPE)))
-void knn_group_kernel(KnnArgs a) {
-  __shared__ uint64_t buf[G][CAP];
-  __shared__ uint32_t hist[256];
-  __shared__ uint32_t stk[64];
-  __shared__ float sdist[G][64];
-  const int lane = threadIdx.x;
-  const float4 *pos = reinterpret_cast<const float4 *>(a.map.pos4);
-  const int L = a.map.nleaves;
-  const int64_t N = a.map.n;
-  const int K = a.K;
-  const int levels = a.map.levels;
-  const KdNode *nodesv = reinterpret_cast<const KdNode *>(a.map.nodes);
-  uint64_t st_q = 0, st_found = 0, st_vis = 0;
-  const int64_t ngroups = (a.nq + G - 1) / G;
-  for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
-    float qx[G], qy[G], qz[G];
-    float4 qpv[G];
-    int64_t qiv[G];
-    uint64_t thr[G];
-    uint32_t count[G];
-    bool live[G], tight[G];
-    bool any = false;
-#pragma unroll
-    for (int g = 0; g < G; g++) {
-      const int64_t qq = grp * G + g;
-      live[g] = qq < a.nq;
-      count[g] = 0;
-      tight[g] = false;
-      thr[g] = 0;  // a dead slot accepts nothing (key < 0) and wants no node (bound NaN)
-      qiv[g] = 0;
-      qpv[g] = make_float4(0.f, 0.f, 0.f, 0.f);
-      qx[g] = qy[g] = qz[g] = 0.0f;
-      if (live[g]) {
-        const int64_t qg = a.q0 + qq;
-        const int64_t qi = a.perm ? (int64_t)a.perm[qg] : qg;
-        const float4 qp = a.qpos[qi];
-        qiv[g] = qi;
-        qpv[g] = qp;
-        if (__float_as_uint(qp.w) == QMETA_NONE) {  // empty deterministic slot
-          if (lane == 0) {
-            a.out[3 * qi] = a.out[3 * qi + 1] = a.out[3 * qi + 2] = 0.0;
-            if (a.out_n) a.out_n[qi] = 0;
-            if (a.out_maxd2) a.out_maxd2[qi] = 0.0f;
-          }
-          live[g] = false;
-        } else {
-          qx[g] = ffirst(qp.x);
-          qy[g] = ffirst(qp.y);
-          qz[g] = ffirst(qp.z);
-          thr[g] = ((uint64_t)__float_as_uint(a.r2f) << 32) + 0x100000000ull;
-          any = true;
-        }
-      }
-    }
-    // largest accepted d2 of query g (NaN for a dead slot: every `d <= bound` test is false)
-    auto bound = [&](int g) { return __uint_as_float((uint32_t)((thr[g] - 1ull) >> 32)); };
-    if (N > 0 && any) {
-      bool need_dk = (a.map.dk != nullptr) && K > 0;
-      int sp = 0;
-      int node = 0;
-      {
-        KdNode r = ld_node(a.map.nodes, 1);
-#pragma unroll
-        for (int g = 0; g < G; g++)
-          if (kd_box_d2(r.lo, r.hi, qx[g], qy[g], qz[g]) <= bound(g)) node = 1;
-      }
-      while (true) {
-        if (!node) {
-          while (sp > 0) {
-            sp--;
-            bool want = false;
-#pragma unroll
-            for (int g = 0; g < G; g++) want = want || (ffirst(sdist[g][sp]) <= bound(g));
-            if (want) {
-              node = (int)ufirst(stk[sp]);
-              break;
-            }
-          }
-          if (!node) break;
-        }
-        node = __builtin_amdgcn_readfirstlane(node);
-        const int h = levels - (31 - __clz(node));
-        if (h > SWEEP_H) {
-          KdNode c0 = ld_node(a.map.nodes, 2 * node), c1 = ld_node(a.map.nodes, 2 * node + 1);
-          float d0[G], d1[G];
-          float m0 = INFINITY, m1 = INFINITY;
-          bool w0 = false, w1 = false;
-#pragma unroll
-          for (int g = 0; g < G; g++) {
-            d0[g] = kd_box_d2(c0.lo, c0.hi, qx[g], qy[g], qz[g]);
-            d1[g] = kd_box_d2(c1.lo, c1.hi, qx[g], qy[g], qz[g]);
-            const float b = bound(g);
-            w0 = w0 || d0[g] <= b;
-            w1 = w1 || d1[g] <= b;
-            if (live[g]) {
-              m0 = fminf(m0, d0[g]);
-              m1 = fminf(m1, d1[g]);
-            }
-          }
-          // near child first: the smaller distance to any of the group's queries
-          const bool swap01 = m1 < m0;
-          const int nn = swap01 ? 2 * node + 1 : 2 * node;
-          const int fn = swap01 ? 2 * node : 2 * node + 1;
-          const bool wn = swap01 ? w1 : w0, wf = swap01 ? w0 : w1;
-          if (wf) {
-            stk[sp] = (uint32_t)fn;  // every lane stores the same values
-#pragma unroll
-            for (int g = 0; g < G; g++) sdist[g][sp] = swap01 ? d0[g] : d1[g];
-            sp++;
-          }
-          node = wn ? nn : 0;
-          continue;
-        }
-        // sweep: leaf boxes of the 2^h leaves under node, lane i holding leaf i
-        const int nl = 1 << h;
-        const int lf0 = node << h;
-        float ld[G];
-        float lmin = INFINITY;
-#pragma unroll
-        for (int g = 0; g < G; g++) ld[g] = INFINITY;
-        if (lane < nl) {
-          KdNode b = nodesv[lf0 + lane];
-#pragma unroll
-          for (int g = 0; g < G; g++) {
-            ld[g] = kd_box_d2(b.lo, b.hi, qx[g], qy[g], qz[g]);
-            if (live[g]) lmin = fminf(lmin, ld[g]);
-          }
-        }
-        uint64_t lm = 0;
-#pragma unroll
-        for (int g = 0; g < G; g++) lm |= __ballot(ld[g] <= bound(g));
-        while (lm) {
-          // the nearest pending leaf (to any query of the group), still within some bound
-          const uint32_t cb = ((lm >> lane) & 1ull) ? __float_as_uint(lmin) : 0xffffffffu;
-          const uint32_t mn = wave_min_u32(cb);
-          const int li = __ffsll((long long)__ballot(cb == mn)) - 1;
-          lm &= ~(1ull << li);
-          bool want = false;
-#pragma unroll
-          for (int g = 0; g < G; g++) want = want || (__shfl(ld[g], li, 64) <= bound(g));
-          if (!want) continue;
-          const int leaf = lf0 + li - L;
-          const int64_t s0 = ((int64_t)leaf * N) / L, s1 = ((int64_t)(leaf + 1) * N) / L;
-          if (need_dk) {
-            // start bounds from the first leaf scanned: for each query, min over its photons p
-            // of |q - p| + d_K(p) (the same bound and margins as knn_wave_kernel)
-            need_dk = false;
-            double best[G];
-#pragma unroll
-            for (int g = 0; g < G; g++) best[g] = INFINITY;
-            for (int64_t b = s0; b < s1; b += 64) {
-              const int64_t ii = b + lane;
-              if (ii < s1) {
-                const float4 p = pos[ii];
-                const float dkp = a.map.dk[ii];
-                if (dkp < INFINITY) {
-#pragma unroll
-                  for (int g = 0; g < G; g++) {
-                    float dx = qx[g] - p.x, dy = qy[g] - p.y, dz = qz[g] - p.z;
-                    float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
-                    best[g] = fmin(best[g], sqrt((double)d2 * (1.0 + 1e-5)) + (double)dkp);
-                  }
-                }
-              }
-            }
-#pragma unroll
-            for (int g = 0; g < G; g++) {
-#pragma unroll
-              for (int o = 32; o > 0; o >>= 1) best[g] = fmin(best[g], __shfl_xor(best[g], o, 64));
-              if (live[g] && best[g] < INFINITY) {
-                double U = best[g] * (1.0 + 1e-6) + 1e-12;
-                float U2 = __double2float_ru(U * U * (1.0 + 1e-5));
-                if (U2 < a.r2f) thr[g] = ((uint64_t)__float_as_uint(U2) << 32) + 0x100000000ull;
-                tight[g] = true;
-              }
-            }
-          }
-#pragma unroll
-          for (int g = 0; g < G; g++)
-            if (live[g]) st_vis += (uint64_t)(s1 - s0);
-          for (int64_t base = s0; base < s1; base += 64) {
-            const int64_t ii = base + lane;
-            const float4 p = pos[ii < s1 ? ii : s0];
-#pragma unroll
-            for (int g = 0; g < G; g++) {
-              if (!live[g]) continue;
-              uint64_t key = ~0ull;
-              if (ii < s1) {
-                float dx = qx[g] - p.x, dy = qy[g] - p.y, dz = qz[g] - p.z;
-                float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
-                key = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)(uint32_t)ii;
-              }
-              bool pass = key < thr[g];
-              uint64_t m = __ballot(pass);
-              uint32_t nnew = (uint32_t)__popcll(m);
-              if (nnew == 0) continue;
-              if (count[g] + nnew > (uint32_t)CAP) {
-                select_k<CAP>(buf[g], hist, lane, count[g], K, thr[g]);
-                tight[g] = true;
-                pass = key < thr[g];
-                m = __ballot(pass);
-                nnew = (uint32_t)__popcll(m);
-                if (nnew == 0) continue;
-              }
-              if (pass) buf[g][count[g] + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = key;
-              count[g] += nnew;
-              __syncthreads();
-            }
-          }
-          // a query that holds K candidates for the first time: select now, so its bound
-          // tightens from r^2 (or the dk bound) to its K-th distance early
-#pragma unroll
-          for (int g = 0; g < G; g++) {
-            if (live[g] && K > 0 && count[g] >= (uint32_t)K + (tight[g] ? (uint32_t)a.sel_slack : 0u)) {
-              select_k<CAP>(buf[g], hist, lane, count[g], K, thr[g]);
-              tight[g] = true;
-            }
-          }
-        }
-        node = 0;
-      }
-    }
-    // exact K best and the estimate, query by query
-#pragma unroll
-    for (int g = 0; g < G; g++) {
-      if (!live[g]) continue;
-      if (count[g] > (uint32_t)K) select_k<CAP>(buf[g], hist, lane, count[g], K, thr[g]);
-      const int num = (int)count[g];
-      st_q += 1;
-      st_found += (uint64_t)num;
-      uint64_t *bg = buf[g];
-      wave_estimate<GEN>(a, qiv[g], qpv[g], num, [&](int s) { return (uint32_t)bg[s]; },
-                         [&](int s) { return __uint_as_float((uint32_t)(bg[s] >> 32)); });
-    }
-    __syncthreads();
-  }
-  if (a.stats && lane == 0) {
-    unsigned long long *sd = stat_stripe(a.stats);
-    if (st_q) atomicAdd(&sd[ST_KNN + a.stat_off], (unsigned long long)st_q);
-    if (st_found) atomicAdd(&sd[ST_KNN_PHOTONS + a.stat_off], (unsigned long long)st_found);
-    if (st_vis) atomicAdd(&sd[ST_KNN_VISITED + a.stat_off], (unsigned long long)st_vis);
-  }
-}
-
 // the estimate over the K-best lists written by knn_wave_kernel in list mode (kept for
 // the group kernel); split from the search so the search kernel keeps a
 // small register footprint
@@ -1341,26 +1077,6 @@ bool launch_knn_wave(const KnnArgs &a, int cap_mul, hipStream_t st) {
                       : wave_launch<false, false>(a, need, (unsigned)grid, st);
   }
   if (!ok) return false;
-  return true;
-}
-
-// the group kernel (estimate mode only): G queries per wave, CAP candidates per query
-bool launch_knn_group(const KnnArgs &a, int G, int cap, hipStream_t st) {
-  if (a.nq == 0) return true;
-  if (a.mode == KNN_MODE_LIST || a.mode == KNN_MODE_DK || a.K + 64 > cap) return false;
-  const int64_t groups = (a.nq + G - 1) / G;
-  const unsigned grid = (unsigned)(groups < (1 << 16) ? groups : (1 << 16));
-#define GI_GROUP_LAUNCH(C_, G_)                                                          \
-  do {                                                                                   \
-    if (a.general) knn_group_kernel<C_, G_, true><<<grid, 64, 0, st>>>(a);               \
-    else knn_group_kernel<C_, G_, false><<<grid, 64, 0, st>>>(a);                        \
-  } while (0)
-  if (G == 2 && cap <= 320) GI_GROUP_LAUNCH(320, 2);
-  else if (G == 2 && cap <= 512) GI_GROUP_LAUNCH(512, 2);
-  else if (G == 4 && cap <= 320) GI_GROUP_LAUNCH(320, 4);
-  else if (G == 4 && cap <= 512) GI_GROUP_LAUNCH(512, 4);
-  else return false;
-#undef GI_GROUP_LAUNCH
   return true;
 }
 

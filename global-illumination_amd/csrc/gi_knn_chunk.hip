@@ -944,6 +944,9 @@ __device__ __forceinline__ bool in_bracket(float d2, uint32_t ab, uint32_t span)
 __device__ __forceinline__ float next_up(float x) { return __uint_as_float(__float_as_uint(x) + 1u); }
 __device__ __forceinline__ float next_down(float x) { return __uint_as_float(__float_as_uint(x) - 1u); }
 
+#ifndef LS_ONE_STORE
+#define LS_ONE_STORE 1  // lane select: one LDS store per collected candidate (r05)
+#endif
 // CAPC = 240 (first pass): 10,112 B of LDS per wave, so 16 waves (4 per SIMD, the VGPR limit)
 // fit in a CU's 160 KiB (256 candidates took 10,752 B: 14 waves); u8 slots and u8 counters.
 // CAPC = 480 (second pass over the first's overflowing chunks): u16 slots and counters, 19.8 KB.
@@ -960,15 +963,22 @@ void knn_chunk_lane_kernel(KnnArgs a) {
   const Cands<CAPC> cpos{cbase};
   uint32_t *const cidx = reinterpret_cast<uint32_t *>(cbase + 4 * CAPC);
   uint32_t *const crgbe = cidx + CAPC;
-  __shared__ uint32_t stk[64];  // kd walk stack (walk_within)
   // kept LDS slots [s][lane] (K <= 64, u8) during the collect and the estimate; during the
   // counting passes the lanes' bin counters [w][lane] (u32, four u8 bins each), and during the
   // bound phase the centre select's 256-bin histogram. One spare slot row (row 64): a lane that
   // keeps exactly K = 64 photons without a bracket stores its later, unkept candidates there
   // (the collect's branch-free store always writes entry n).
-  __shared__ uint32_t selh[16 * SB * 64 + 16 * SB];
+  // counting-pass layout (LS_ONE_STORE): lane-major with a stride of NWC + 1 words (coprime with
+  // the banks: conflict-free), so a counter's address is base + (b & ~(PERW - 1)) / PERW words
+  // -- one and + add instead of the word-major layout's shift, and, add
+  constexpr int CST = LS_ONE_STORE ? NWC + 1 : 64;   // counter row stride (words)
+  __shared__ uint32_t selh[(16 * SB * 64 + 16 * SB) > 64 * (NWC + 1) ? (16 * SB * 64 + 16 * SB) : 64 * (NWC + 1)];
   SlotT *sel = reinterpret_cast<SlotT *>(selh);
   uint32_t *hist = selh;
+  // kd walk stack (walk_within): the last 64 words of selh, live only during the gather walk,
+  // when neither the counters nor the slot lists are (the bound phase's histogram is words
+  // 0-255)
+  uint32_t *const stk = selh + (sizeof(selh) / sizeof(uint32_t) - 64);
   const int lane = threadIdx.x;
   const int K = a.K;
   uint64_t st_q = 0, st_found = 0, st_vis = 0;
@@ -1033,7 +1043,7 @@ void knn_chunk_lane_kernel(KnnArgs a) {
         // LS_NB = 64 bins per lane: u8 counters packed four per LDS word [w][lane] (w = bin / 4;
         // conflict-free, one ds_add per candidate; at most 255 members, so no byte carries)
 #pragma unroll
-        for (int w = 0; w < NWC; w++) selh[w * 64 + lane] = 0u;
+        for (int w = 0; w < NWC; w++) selh[LS_ONE_STORE ? lane * CST + w : w * 64 + lane] = 0u;
         // groups of 8 candidates: the group's (broadcast) LDS reads are issued together and the
         // loop body has no branches (non-members, and the +inf padding past `count`, add 0)
         constexpr uint32_t PERW = 4 / SB;  // counters per word
@@ -1044,7 +1054,11 @@ void knn_chunk_lane_kernel(KnnArgs a) {
           for (int u = 0; u < 8; u++) {
             const uint32_t b = binN<LS_NB>(dg[u], sc, off);
             const uint32_t inc = in_bracket(dg[u], ab, span) ? (1u << ((b & (PERW - 1u)) * 8u * SB)) : 0u;
+#if LS_ONE_STORE
+            atomicAdd(&selh[lane * CST + b / PERW], inc);
+#else
             atomicAdd(&selh[(b / PERW) * 64 + lane], inc);
+#endif
           }
         }
         if (on) {
@@ -1053,7 +1067,7 @@ void knn_chunk_lane_kernel(KnnArgs a) {
           constexpr uint32_t CM = SB == 1 ? 255u : 65535u;
 #pragma unroll
           for (int w = 0; w < NWC; w++) {
-            const uint32_t c4 = selh[w * 64 + lane];
+            const uint32_t c4 = selh[LS_ONE_STORE ? lane * CST + w : w * 64 + lane];
             const uint32_t ws = SB == 1 ? __builtin_amdgcn_sad_u8(c4, 0u, 0u) : (c4 & 65535u) + (c4 >> 16);
             if (bs == LS_NB) {
               if (before + ws >= (uint32_t)need) {
@@ -1126,10 +1140,17 @@ void knn_chunk_lane_kernel(KnnArgs a) {
         const float d2 = dg[u];
         const bool kf = d2 < acol;
         const bool kb = in_bracket(d2, ab, span);
+#if LS_ONE_STORE
+        // one store per candidate: a bracket member to the back entry bm, anything else to the
+        // front entry n (a kept one stays there, an unkept one is overwritten by the next kept
+        // one or never read; a lane without a bracket may fill all 64 entries, row 64 spare)
+        sel[(kb ? bm : n) * 64 + lane] = (SlotT)s;
+#else
         // (a lane without a bracket may fill all 64 entries: its bracket store goes to n too,
         // before the front store of the same value)
         sel[(inb_on ? bm : n) * 64 + lane] = (SlotT)s;
         sel[n * 64 + lane] = (SlotT)s;
+#endif
         n += kf ? 1 : 0;
         bm -= kb ? 1 : 0;
         km = fmaxf(km, kf ? d2 : 0.0f);

@@ -112,3 +112,12 @@ def test_figures_show_the_named_scene(name):
     assert core.sum() > 0.02 * res * res
     assert (fig[core] <= 8).mean() > 0.97, (fig[core] <= 8).mean()
     assert fig[diffuse].mean() > 10
+
+
+def test_calibration_figures_are_named():
+    """The figures the unstated settings were fitted on are marked (photon_figs.CALIBRATION),
+    and the held-out pins outnumber them."""
+    assert set(pf.CALIBRATION) <= set(pf.FIGS)
+    held = [n for n in pf.FIGS if pf.role(n) == "held-out"]
+    assert len(held) >= 30 and len(pf.CALIBRATION) == 3
+

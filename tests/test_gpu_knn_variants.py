@@ -36,11 +36,8 @@ VARIANTS = [
     {"GI_KNN_KERNEL": "8"},
     {"GI_KNN_KERNEL": "8", "GI_LEAF_SIZE": "128"},
     {"GI_KNN_KERNEL": "8", "GI_CHUNK_MINSUB_BIG": "1"},
-    # the large-K fallback as G queries per wave on one walk (knn_group_kernel), with every
-    # overflowing chunk handed to it whole (MINSUB_BIG 64) so that it sees many queries
-    {"GI_KNN_KERNEL": "8", "GI_KNN_GROUP": "2", "GI_CHUNK_MINSUB_BIG": "64"},
-    {"GI_KNN_KERNEL": "8", "GI_KNN_GROUP": "4", "GI_GROUP_CAP": "320", "GI_CHUNK_MINSUB_BIG": "64"},
-    {"GI_KNN_KERNEL": "8", "GI_KNN_GROUP": "4", "GI_LEAF_SIZE": "64"},
+    # every overflowing large-K chunk handed to the query-per-wave fallback whole
+    {"GI_KNN_KERNEL": "8", "GI_CHUNK_MINSUB_BIG": "64"},
 ]
 
 

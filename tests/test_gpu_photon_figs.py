@@ -44,7 +44,7 @@ def test_device_figure_pin(renderer, name, tmp_path):
     log = os.environ.get("GI_FIG_LOG")
     if log:
         with open(log, "a") as f:
-            f.write(json.dumps(dict(r, figure=name)) + "\n")
+            f.write(json.dumps(dict(r, figure=name, role=pf.role(name))) + "\n")
     if name in KNOWN_MISSES:
         pytest.xfail(KNOWN_MISSES[name] + f" ({r})")
     assert r["ok"], r

@@ -343,7 +343,12 @@ struct gi_ctx {
   // render scratch
   DBuf spawn, npaths, path_off, nmc, mc_off, nind, ind_off, base, pixels, rgbf, rgb8, qcount, stats_bak;
   DBuf qpos[2], qshade[2], qkey[2], qout[2];
-  bool chunk_big2 = true;            // large-K chunk k-NN: second chunk pass (1024 candidates)
+  bool chunk_big2 = true;            // large-K chunk k-NN: further chunk passes
+  // ... the second pass's LDS candidates (GI_CHUNK_CAP_BIG2; kernel instances: 384, 512, 1024)
+  // and a third pass's (GI_CHUNK_CAP_BIG3; 0: none). r05: a 576-candidate pass at two waves per
+  // SIMD, alone or before the 1024 one, was not faster (profiles/r05_chunk_pass_chain_ab.txt)
+  int chunk_cap_big2 = 1024;
+  int chunk_cap_big3 = 0;
   bool chunk_lane2 = true;           // lane-select chunk k-NN: second pass (480, GI_CHUNK_LANE2)
   int chunk_minsub_big2 = 64;        // ... its overflowing chunks retried down to this group size
   bool chunk_dk = true;            // chunk kernel (K <= 64): centre bound from the dk bounds (measured: fewer fallbacks)
@@ -966,34 +971,41 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
     X.fb_total += nfb;
     uint32_t nfb2 = nfb;
     bool ran2 = false;
-    if (nfb && c->chunk_big2) {
+    // further chunk passes over the overflowing chunks' queries, with more LDS candidates each
+    // (chunk_cap_big2: 1024 by default; chunk_cap_big3 > 0 adds a third); the compacted lists
+    // keep each chunk's queries together, in Morton order. What overflows the last one goes to
+    // the query-per-wave kernel. Pass i reads `dense` and writes the other list (ping-pong:
+    // the first pass's list is free once the second has read it).
+    const int caps2[2] = {c->chunk_cap_big2, c->chunk_cap_big3};
+    for (int pi = 0; pi < 2 && nfb2 && c->chunk_big2 && caps2[pi] > 0; pi++) {
       ran2 = true;
-      // second chunk pass with 1024 LDS candidates over the overflowing chunks' queries (the
-      // compacted list keeps each chunk's queries together, in Morton order); what overflows
-      // again goes to the query-per-wave kernel
-      int64_t chunks2 = ((int64_t)nfb + 63) / 64;
-      int64_t grid2 = knn_chunk_grid(nfb);
+      const uint32_t nin = nfb2;
+      DBuf &L = pi == 0 ? X.fb_list2 : X.fb_list;
+      DBuf &Dn = pi == 0 ? X.fb_dense2 : X.fb_dense;
+      DBuf &Cn = pi == 0 ? X.fb_count2 : X.fb_count;
+      int64_t chunks2 = ((int64_t)nin + 63) / 64;
+      int64_t grid2 = knn_chunk_grid(nin);
       uint32_t cap2 = (uint32_t)(64 * ((chunks2 + grid2 - 1) / grid2) * ((grid2 + FB_QS - 1) / FB_QS));
-      HIPCHK(c, X.fb_list2.ensure((size_t)FB_QS * cap2 * 4));
-      HIPCHK(c, X.fb_dense2.ensure((size_t)nfb * 4 + 4));
-      HIPCHK(c, X.fb_count2.ensure(FB_QS * 32 * 4));
-      HIPCHK(c, hipMemsetAsync(X.fb_count2.p, 0, FB_QS * 32 * 4, X.st));
+      HIPCHK(c, L.ensure((size_t)FB_QS * cap2 * 4));
+      HIPCHK(c, Dn.ensure((size_t)nin * 4 + 4));
+      HIPCHK(c, Cn.ensure(FB_QS * 32 * 4));
+      HIPCHK(c, hipMemsetAsync(Cn.p, 0, FB_QS * 32 * 4, X.st));
       KnnArgs s2 = k;
       s2.perm = dense;
-      s2.nq = nfb;
+      s2.nq = nin;
       s2.q0 = 0;
-      s2.fb_list = X.fb_list2.as<uint32_t>();
-      s2.fb_count = X.fb_count2.as<uint32_t>();
+      s2.fb_list = L.as<uint32_t>();
+      s2.fb_count = Cn.as<uint32_t>();
       s2.fb_cap_s = cap2;
       s2.dbg &= ~16;
       s2.chunk_minsub = c->chunk_minsub_big2;
-      if (!launch_knn_chunk_big(s2, 1024, X.st))
+      if (!launch_knn_chunk_big(s2, caps2[pi], X.st))
         return fail(c, GI_ERR_ARG, "k-NN launch: large-K chunk kernel unavailable");
       HIPCHK(c, hipGetLastError());
-      dense = X.fb_dense2.as<uint32_t>();
-      launch_fb_compact(s2.fb_list, s2.fb_count, cap2, dense, dense + nfb, X.st);
+      dense = Dn.as<uint32_t>();
+      launch_fb_compact(s2.fb_list, s2.fb_count, cap2, dense, dense + nin, X.st);
       HIPCHK(c, hipGetLastError());
-      HIPCHK(c, hipMemcpyAsync(&nfb2, dense + nfb, 4, hipMemcpyDeviceToHost, X.st));
+      HIPCHK(c, hipMemcpyAsync(&nfb2, dense + nin, 4, hipMemcpyDeviceToHost, X.st));
       HIPCHK(c, hipStreamSynchronize(X.st));
     }
     bool dumped = false;
@@ -1632,6 +1644,8 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_PHOTON_RATE0"))  // test knob: first launch's slots per photon
     c->prate[0] = c->prate[1] = std::max(0.0, atof(s));
   if (const char *s = getenv("GI_CHUNK_MINSUB_BIG")) c->chunk_minsub_big = std::min(64, std::max(1, atoi(s)));
+  if (const char *s = getenv("GI_CHUNK_CAP_BIG2")) c->chunk_cap_big2 = atoi(s);
+  if (const char *s = getenv("GI_CHUNK_CAP_BIG3")) c->chunk_cap_big3 = atoi(s);
   if (const char *s = getenv("GI_CHUNK_MINSUB")) c->chunk_minsub = std::min(64, std::max(1, atoi(s)));
   if (const char *s = getenv("GI_SPLIT_IND")) c->split_ind = atoi(s) != 0;
   if (const char *s = getenv("GI_KNN_GENERAL")) c->knn_general_mode = std::max(-1, std::min(1, atoi(s)));

@@ -38,6 +38,8 @@ VARIANTS = [
     {"GI_KNN_KERNEL": "8", "GI_CHUNK_MINSUB_BIG": "1"},
     # every overflowing large-K chunk handed to the query-per-wave fallback whole
     {"GI_KNN_KERNEL": "8", "GI_CHUNK_MINSUB_BIG": "64"},
+    # a third large-K chunk pass (512 -> 1024 -> 1024 candidates: the pass chain's ping-pong)
+    {"GI_KNN_KERNEL": "8", "GI_CHUNK_CAP_BIG3": "1024", "GI_LEAF_SIZE": "128"},
 ]
 
 

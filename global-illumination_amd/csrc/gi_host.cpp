@@ -357,6 +357,7 @@ struct gi_ctx {
   // and after an instance without it met a query that needed it), -1 test knob: claim that no
   // render query needs it (GI_KNN_GENERAL=-1; exercises render_common's re-run)
   int knn_general_mode = 0;
+  bool sort_all = false;  // GI_SORT_ALL=1: sort / search every list slot, empty ones included
   bool use_dk = true;              // wave k-NN kernel starts from per-photon K-th bounds
   DBuf qseg[2];  // K-best lists of the query-per-wave k-NN path
   size_t qcap_hint[2] = {0, 0};
@@ -1239,16 +1240,30 @@ int knn_list(gi_ctx *c, int mi, const float4 *qpos, const QShade *qshade, int64_
   k.qshade = qshade;
   k.out = out;
   k.nq = nq;
-  {
-    uint32_t *perm = nullptr;
-    HIPCHK(c, morton_order(qpos, nq, c->sbmin, c->sbmax, X.sorter, &perm, X.st));
-    k.perm = perm;
-  }
   if (c->P.irradiance_cache && mi == GI_MAP_GLOBAL) {
+    // the cached-radiance lookup runs thread per list slot (it reads no permutation)
     c->last_kind[mi] = 9;
     launch_cached(k, X.st);
     HIPCHK(c, hipGetLastError());
     return GI_OK;
+  }
+  {
+    // only the valid queries are sorted and searched: the empty deterministic slots (indirect
+    // paths absorbed, escaped, or whose continuation left no query; primaries without their own
+    // query; Monte Carlo paths that deferred none) are ~46 % of C2's global list, and the
+    // reduction never reads their outputs (their keys / row-mask bits mark them). GI_SORT_ALL=1:
+    // the r04 behaviour (every slot sorted, empties skipped inside the k-NN kernels).
+    uint32_t *perm = nullptr;
+    if (c->sort_all) {
+      HIPCHK(c, morton_order(qpos, nq, c->sbmin, c->sbmax, X.sorter, &perm, X.st));
+    } else {
+      int64_t nv = 0;
+      HIPCHK(c, morton_order_valid(qpos, nq, c->sbmin, c->sbmax, X.sorter, &perm, &nv, X.st));
+      nq = nv;
+      k.nq = nv;
+      if (nv == 0) return GI_OK;
+    }
+    k.perm = perm;
   }
   return run_knn(c, k, nq, ms);
 }
@@ -1659,6 +1674,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_CHUNK_FB_ALL")) c->chunk_fb_all = atoi(s) != 0;
   if (const char *s = getenv("GI_IND_FRAC")) c->ind_frac = std::min(1.0, std::max(1e-6, atof(s)));
   if (const char *s = getenv("GI_KNN_KERNEL")) c->knn_kernel_kind = atoi(s);
+  if (const char *s = getenv("GI_SORT_ALL")) c->sort_all = atoi(s) != 0;
   *out = c;
   return GI_OK;
 }

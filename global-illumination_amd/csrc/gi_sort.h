@@ -11,6 +11,11 @@ struct SortScratch {
 // returns a device permutation (sorted position -> query index) valid until the next call
 hipError_t morton_order(const float4 *q, int64_t n, const float bmin[3], const float bmax[3],
                         SortScratch &s, uint32_t **perm_out, hipStream_t st);
+// the same with the empty slots (meta == QMETA_NONE) sorted after every valid query: the first
+// *nvalid entries of the permutation are the valid queries in morton_order's order, so the k-NN
+// launch takes only those (synchronises st for the count)
+hipError_t morton_order_valid(const float4 *q, int64_t n, const float bmin[3], const float bmax[3],
+                              SortScratch &s, uint32_t **perm_out, int64_t *nvalid, hipStream_t st);
 void sort_scratch_release(SortScratch &s);
 
 struct KeySortScratch {

@@ -87,6 +87,110 @@ hipError_t morton_order(const float4 *q, int64_t n, const float bmin[3], const f
   return hipSuccess;
 }
 
+// Morton keys of the valid queries (meta != QMETA_NONE) and, for the empty slots, the key 2^30
+// (above every 30-bit code): the stable sort puts the valid queries first, in the order
+// morton_order gives them, and the empty ones after them
+__global__ void morton_valid_kernel(const float4 *q, int64_t n, float ox, float oy, float oz,
+                                    float sx, float sy, float sz, float cmax, uint32_t *keys,
+                                    uint32_t *vals) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float4 p = q[i];
+  const bool valid = __float_as_uint(p.w) != 0xffffffffu;  // QMETA_NONE (gi_kernels.h)
+  float fx = fminf(fmaxf((p.x - ox) * sx, 0.0f), cmax);
+  float fy = fminf(fmaxf((p.y - oy) * sy, 0.0f), cmax);
+  float fz = fminf(fmaxf((p.z - oz) * sz, 0.0f), cmax);
+  keys[i] = valid ? ((spread10((uint32_t)fx) << 2) | (spread10((uint32_t)fy) << 1) |
+                     spread10((uint32_t)fz))
+                  : (1u << 30);
+  vals[i] = (uint32_t)i;
+}
+
+// the number of valid queries = the first sorted key >= 2^30, by a 64-way search in one wave
+// (a per-wave atomic count in morton_valid_kernel serialised 6M same-address atomics: r05i,
+// +32 ms per list)
+__global__ void __launch_bounds__(64) first_empty_kernel(const uint32_t *k, int64_t n,
+                                                         unsigned long long *out) {
+  int64_t lo = 0, hi = n;  // the answer lies in [lo, hi]
+  const int lane = threadIdx.x;
+  while (lo < hi) {
+    const int64_t step = (hi - lo + 63) / 64;
+    const int64_t p = lo + lane * step;
+    const uint64_t m = __ballot(p >= hi || k[p] >= (1u << 30));
+    if (m == 0) {  // every probe valid: past lane 63's
+      lo += 63 * step + 1;
+      continue;
+    }
+    const int f = __ffsll((unsigned long long)m) - 1;
+    const int64_t nhi = lo + f * step;
+    lo = f ? lo + (f - 1) * step + 1 : lo;
+    hi = nhi < hi ? nhi : hi;
+  }
+  if (lane == 0) *out = (unsigned long long)lo;
+}
+
+hipError_t morton_order_valid(const float4 *q, int64_t n, const float bmin[3], const float bmax[3],
+                              SortScratch &s, uint32_t **perm_out, int64_t *nvalid, hipStream_t st) {
+  *perm_out = nullptr;
+  *nvalid = 0;
+  if (n <= 0) return hipSuccess;
+  hipError_t e;
+  auto grow = [&](void *&p, size_t &cap, size_t bytes) -> hipError_t {
+    if (bytes <= cap && p) return hipSuccess;
+    size_t want = cap ? std::max(bytes, cap + cap / 2) : bytes;  // headroom (gi_host.cpp DBuf)
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (want > bytes) {
+      size_t fr = 0, tot = 0;
+      if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < want + tot / 4) want = bytes;
+    }
+    hipError_t r = hipMalloc(&p, want);
+    if (r != hipSuccess && want > bytes) {
+      (void)hipGetLastError();
+      want = bytes;
+      r = hipMalloc(&p, want);
+    }
+    if (r == hipSuccess) cap = want;
+    return r;
+  };
+  size_t b4 = (size_t)n * 4;
+  if ((e = grow(s.k0, s.k0_cap, b4 + 16)) != hipSuccess) return e;
+  if ((e = grow(s.k1, s.k1_cap, b4)) != hipSuccess) return e;
+  if ((e = grow(s.v0, s.v0_cap, b4)) != hipSuccess) return e;
+  if ((e = grow(s.v1, s.v1_cap, b4)) != hipSuccess) return e;
+  // the valid count lives past the keys (8 B, aligned)
+  auto *d_cnt = reinterpret_cast<unsigned long long *>((char *)s.k0 + ((b4 + 7) & ~(size_t)7));
+  constexpr int bits = 10;
+  const float cmax = (float)((1 << bits) - 1);
+  float sc[3];
+  for (int i = 0; i < 3; i++) {
+    float ext = bmax[i] - bmin[i];
+    sc[i] = ext > 0 ? cmax / ext : 0.0f;
+  }
+  morton_valid_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(
+      q, n, bmin[0], bmin[1], bmin[2], sc[0], sc[1], sc[2], cmax, (uint32_t *)s.k0,
+      (uint32_t *)s.v0);
+  size_t tb = 0;
+  // 31 key bits: the 30-bit code and the empty slots' 2^30 (four 8-bit passes, as for 30 bits)
+  e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t *)s.k0, (uint32_t *)s.k1,
+                                         (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0,
+                                         3 * bits + 1, st);
+  if (e != hipSuccess) return e;
+  if ((e = grow(s.tmp, s.tmp_cap, tb + 256)) != hipSuccess) return e;
+  e = hipcub::DeviceRadixSort::SortPairs(s.tmp, tb, (const uint32_t *)s.k0, (uint32_t *)s.k1,
+                                         (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0,
+                                         3 * bits + 1, st);
+  if (e != hipSuccess) return e;
+  first_empty_kernel<<<1, 64, 0, st>>>((const uint32_t *)s.k1, n, d_cnt);
+  unsigned long long nv = 0;
+  if ((e = hipMemcpyAsync(&nv, d_cnt, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+  if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+  *nvalid = (int64_t)nv;
+  *perm_out = (uint32_t *)s.v1;
+  return hipSuccess;
+}
+
 __global__ void iota_kernel(uint32_t *v, int64_t n) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) v[i] = (uint32_t)i;

@@ -220,6 +220,31 @@ def test_element_pretest_is_exact(scene, monkeypatch):
     np.testing.assert_array_equal(out[0], out[1])
 
 
+@pytest.mark.parametrize("scene", ["cornell.scn", "jensen.scn"])
+def test_valid_first_query_order_is_exact(scene, monkeypatch):
+    """The k-NN launches take only the valid query slots, sorted ahead of the empty ones
+    (gi_sort.hip morton_order_valid; the photon lookups of PhotonMap_EstimateRadiance,
+    photonmap.cpp): the f32 image and the -v counters equal those of the r04 order that sorts and
+    walks every slot (GI_SORT_ALL=1), here with many empty slots (it 16, short paths)."""
+    import gi_amd
+    import gpu_util
+    args = [gpu_util.scene(scene), "/tmp/so.png", "-resolution", "40", "32", "-aa", "1",
+            "-global", "30000", "-caustic", "30000", "-it", "16", "-tt", "4", "-st", "4",
+            "-seed", "5"]
+    out = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("GI_SORT_ALL", v)
+        r = gi_amd.Renderer(0)
+        try:
+            _, f, st, _ = gpu_util.run_gpu(r, args, want_float=True)
+        finally:
+            r.close()
+        out.append((f, st))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    for k in ("indirect_samples", "caustic_samples", "knn_queries"):
+        assert out[0][1][k] == out[1][1][k], k
+
+
 def test_c5_settings_match_oracle(renderer):
     """C5's sampling settings at an oracle-sized resolution: teapot.scn, aa 3 (64 subsamples per
     pixel, render.cpp:174-178), depth of field with 4 aperture samples at the C5 focus and

@@ -358,6 +358,11 @@ struct gi_ctx {
   // render query needs it (GI_KNN_GENERAL=-1; exercises render_common's re-run)
   int knn_general_mode = 0;
   bool sort_all = false;  // GI_SORT_ALL=1: sort / search every list slot, empty ones included
+  // GI_EARLY_KNN=1: in a batch with Monte Carlo paths on the side stream, the k-NN of the
+  // deterministic query slots runs before the join, beside the side stream's tail (off by
+  // default: C2 -0.4 % per frame, but the global k-NN launches that share the GPU with the
+  // Monte Carlo kernel then take 45.3 -> 47.0 ms on average; render_pixels)
+  bool early_knn = false;
   bool use_dk = true;              // wave k-NN kernel starts from per-photon K-th bounds
   DBuf qseg[2];  // K-best lists of the query-per-wave k-NN path
   size_t qcap_hint[2] = {0, 0};
@@ -1427,6 +1432,18 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     // paths' tiled slots; Monte Carlo paths append after qbase[l]
     uint32_t qbase[2] = {(uint32_t)(nprim + tind), (uint32_t)nprim};
     a.qind_base = nprim;
+    // Early k-NN (batches with Monte Carlo paths on the side stream): the deterministic slots
+    // [0, qbase[l]) are written only by the main stream's kernels (slot0, ind, ind_cont; the
+    // Monte Carlo paths only append, PathCtx::fixed = -1), so their estimates run on the main
+    // stream as soon as its path kernels end, while the side stream's Monte Carlo tail is still
+    // running; the appends [qbase[l], nq[l]) are estimated after the join. Each query's result
+    // is independent of the launch it is in, so the image is the same. Not beside the
+    // persistent Monte Carlo kernel (mc_next: soft-light scenes), whose waves hold every SIMD's
+    // registers until its last path ends: there the k-NN only waits for CUs (C3 2,485 -> 2,513
+    // ms with it; C2, plain mc_kernel, 1,460.7 -> 1,455.5 ms; profiles/r05_early_knn_ab.txt:
+    // the plain kernel fills the chip too, so there is little tail to hide).
+    const bool early = c->early_knn && a.total_mc > 0 && !a.mc_next && c->stream2 && c->ev_fork &&
+                       c->ev_join;
     for (int attempt = 0; attempt < 3; attempt++) {
       for (int l = 0; l < 2; l++) {
         // capacity: the largest list seen so far (+25 %), or this batch's primaries at the
@@ -1461,8 +1478,20 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
       a.qcount = c->qcount.as<uint32_t>();
       HIPCHK(c, hipMemcpyAsync(c->qcount.p, qbase, 8, hipMemcpyHostToDevice, c->stream));
       if (tind > (uint64_t)a.total_ind) launch_ind_pad(a, c->stream);  // (never when tind = 0)
-      launch_path(a, c->stream, c->stream2, c->ev_fork, c->ev_join);
+      if (early)  // outputs for the whole capacity: the appends' part is written after the join
+        for (int l = 0; l < 2; l++)
+          if (c->map_valid[l]) HIPCHK(c, c->qout[l].ensure((size_t)a.qcap[l] * 24));
+      launch_path(a, c->stream, c->stream2, c->ev_fork, c->ev_join, !early);
       HIPCHK(c, hipGetLastError());
+      if (early) {
+        for (int l = 0; l < 2; l++) {
+          if (!c->map_valid[l] || qbase[l] == 0) continue;
+          int rc = knn_list(c, l, a.qpos[l], a.qshade[l], qbase[l], c->qout[l].as<double>(),
+                            rs ? &knn_ms[l] : nullptr);
+          if (rc) return rc;
+        }
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+      }
       HIPCHK(c, hipMemcpyAsync(nq, c->qcount.p, 8, hipMemcpyDeviceToHost, c->stream));
       uint32_t fills[IND_QS * 32];
       if (a.split_ind && a.total_ind > 0)
@@ -1497,7 +1526,7 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
       a.qapp[l] = qbase[l];
       a.qout[l] = nullptr;
       if (nq[l]) {
-        HIPCHK(c, c->qout[l].ensure((size_t)nq[l] * 24));
+        if (!early || !c->map_valid[l]) HIPCHK(c, c->qout[l].ensure((size_t)nq[l] * 24));
         a.qout[l] = c->qout[l].as<double>();
         if (!c->map_valid[l])
           HIPCHK(c, hipMemsetAsync(c->qout[l].p, 0, (size_t)nq[l] * 24, c->stream));
@@ -1510,8 +1539,10 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     int rcm[2] = {GI_OK, GI_OK};
     for (int l = 0; l < 2; l++) {
       if (!run[l]) continue;
-      rcm[l] = knn_list(c, l, a.qpos[l], a.qshade[l], nq[l], c->qout[l].as<double>(),
-                        rs ? &knn_ms[l] : nullptr);
+      const uint32_t q0 = early ? qbase[l] : 0u;  // early: the deterministic part is done
+      if (nq[l] > q0)
+        rcm[l] = knn_list(c, l, a.qpos[l] + q0, a.qshade[l] + q0, nq[l] - q0,
+                          c->qout[l].as<double>() + 3 * (size_t)q0, rs ? &knn_ms[l] : nullptr);
       if (rcm[l]) break;
     }
     for (int l = 0; l < 2; l++) {
@@ -1675,6 +1706,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_IND_FRAC")) c->ind_frac = std::min(1.0, std::max(1e-6, atof(s)));
   if (const char *s = getenv("GI_KNN_KERNEL")) c->knn_kernel_kind = atoi(s);
   if (const char *s = getenv("GI_SORT_ALL")) c->sort_all = atoi(s) != 0;
+  if (const char *s = getenv("GI_EARLY_KNN")) c->early_knn = atoi(s) != 0;
   *out = c;
   return GI_OK;
 }

@@ -340,8 +340,10 @@ struct ScanTemp {
 hipError_t launch_scan(const uint32_t *in, uint32_t *out, int64_t n, ScanTemp &tmp,
                        hipStream_t st);
 void launch_primary(const RenderArgs &a, hipStream_t st);
+// wait_join = false: the join event is recorded on st2 but st does not wait for it (the caller
+// makes st wait later, after work that reads only the deterministic query slots)
 void launch_path(const RenderArgs &a, hipStream_t st, hipStream_t st2 = nullptr,
-                 hipEvent_t fork = nullptr, hipEvent_t join = nullptr);
+                 hipEvent_t fork = nullptr, hipEvent_t join = nullptr, bool wait_join = true);
 // float4 queries {x, y, z, 0} at the photons of a map (KNN_MODE_DK input)
 void launch_photon_queries(const float *pos4, int64_t n, float4 *q, hipStream_t st);
 // dense copy of the striped chunk fallback list; total length to *total

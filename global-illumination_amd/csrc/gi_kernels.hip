@@ -1855,7 +1855,7 @@ static void launch_mc_sub(const RenderArgs &a, hipStream_t st) {
 // them before returning (fork/join events). The two kernels write disjoint path slots and
 // append queries through the same atomic counters.
 void launch_path(const RenderArgs &a, hipStream_t st, hipStream_t st2, hipEvent_t fork,
-                 hipEvent_t join) {
+                 hipEvent_t join, bool wait_join) {
   const bool side = st2 && fork && join && a.total_mc > 0;
   hipStream_t ms = side ? st2 : st;
   // the Monte Carlo queues' counters are zeroed on st before the fork: a fill on the side stream
@@ -1924,7 +1924,7 @@ void launch_path(const RenderArgs &a, hipStream_t st, hipStream_t st2, hipEvent_
   }
   if (side) {
     (void)hipEventRecord(join, st2);
-    (void)hipStreamWaitEvent(st, join, 0);
+    if (wait_join) (void)hipStreamWaitEvent(st, join, 0);
   }
 }
 // Shard gather of a device set (gi_host.cpp render_multi): a device's output pixels packed in

@@ -221,19 +221,23 @@ def test_element_pretest_is_exact(scene, monkeypatch):
 
 
 @pytest.mark.parametrize("scene", ["cornell.scn", "jensen.scn"])
-def test_valid_first_query_order_is_exact(scene, monkeypatch):
-    """The k-NN launches take only the valid query slots, sorted ahead of the empty ones
-    (gi_sort.hip morton_order_valid; the photon lookups of PhotonMap_EstimateRadiance,
-    photonmap.cpp): the f32 image and the -v counters equal those of the r04 order that sorts and
-    walks every slot (GI_SORT_ALL=1), here with many empty slots (it 16, short paths)."""
+@pytest.mark.parametrize("var", ["GI_SORT_ALL", "GI_EARLY_KNN"])
+def test_knn_launch_order_is_exact(scene, var, monkeypatch):
+    """How the photon lookups (PhotonMap_EstimateRadiance, photonmap.cpp) are grouped into
+    launches does not change any result: (1) only the valid query slots, sorted ahead of the
+    empty ones (gi_sort.hip morton_order_valid), against the r04 order that sorts and walks every
+    slot (GI_SORT_ALL=1); (2) the deterministic slots' estimates run before the Monte Carlo side
+    stream joins and the appends' after it (GI_EARLY_KNN=1; cornell's hard light runs the plain
+    Monte Carlo kernel, where it applies), against one launch per list after the join (default). The f32 image and the -v counters are equal; -tt/-st 4 give Monte Carlo
+    paths, -it 16 many empty slots."""
     import gi_amd
     import gpu_util
     args = [gpu_util.scene(scene), "/tmp/so.png", "-resolution", "40", "32", "-aa", "1",
             "-global", "30000", "-caustic", "30000", "-it", "16", "-tt", "4", "-st", "4",
             "-seed", "5"]
     out = []
-    for v in ("0", "1"):
-        monkeypatch.setenv("GI_SORT_ALL", v)
+    for v in ("0", "1") if var == "GI_SORT_ALL" else ("1", "0"):
+        monkeypatch.setenv(var, v)
         r = gi_amd.Renderer(0)
         try:
             _, f, st, _ = gpu_util.run_gpu(r, args, want_float=True)
@@ -241,8 +245,9 @@ def test_valid_first_query_order_is_exact(scene, monkeypatch):
             r.close()
         out.append((f, st))
     np.testing.assert_array_equal(out[0][0], out[1][0])
-    for k in ("indirect_samples", "caustic_samples", "knn_queries"):
+    for k in ("monte_carlo_rays", "indirect_samples", "caustic_samples", "knn_queries"):
         assert out[0][1][k] == out[1][1][k], k
+    assert out[0][1]["monte_carlo_rays"] > 0
 
 
 def test_c5_settings_match_oracle(renderer):

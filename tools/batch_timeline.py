@@ -31,3 +31,22 @@ for bi, a in enumerate(prims):
         d[k] = d.get(k, 0) + (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
     print(f"batch {bi:2d} span {(t1 - t0) / 1e6:7.1f} ms: " +
           " ".join(f"{k}={v:.1f}" for k, v in d.items() if v >= 0.5))
+
+# idle time: the part of each batch's span with no kernel running on any stream, and the largest
+# gaps with the kernels on either side
+for bi, a in enumerate(prims):
+    b = prims[bi + 1] if bi + 1 < len(prims) else len(rows)
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:60])
+                for r in rows[a:b])
+    t0, end, idle, gaps = iv[0][0], iv[0][1], 0, []
+    prev = iv[0][2]
+    for s, e, n in iv[1:]:
+        if s > end:
+            idle += s - end
+            gaps.append(((s - end) / 1e6, prev, n))
+        if e > end:
+            end, prev = e, n
+    gaps.sort(reverse=True)
+    print(f"batch {bi:2d} idle {idle / 1e6:6.2f} ms of {(end - t0) / 1e6:7.1f}; largest: " +
+          "; ".join(f"{g:.2f} ms {p.split('(')[0][-28:]} -> {n.split('(')[0][-28:]}"
+                    for g, p, n in gaps[:3]))

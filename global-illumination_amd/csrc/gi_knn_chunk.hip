@@ -95,6 +95,9 @@ struct Cands {
   }
 };
 
+#ifndef D2X8_PHASED
+#define D2X8_PHASED 1
+#endif
 // d2 of the 8 candidates s0 .. s0 + 7 (s0 % 8 == 0, s0 + 8 <= CAPC): six broadcast reads
 template <int CAPC>
 __device__ __forceinline__ void cand_d2x8(const Cands<CAPC> &C, uint32_t s0, float qx, float qy,
@@ -102,6 +105,33 @@ __device__ __forceinline__ void cand_d2x8(const Cands<CAPC> &C, uint32_t s0, flo
   const float4 x0 = C.quad(0, s0), x1 = C.quad(0, s0 + 4);
   const float4 y0 = C.quad(1, s0), y1 = C.quad(1, s0 + 4);
   const float4 z0 = C.quad(2, s0), z1 = C.quad(2, s0 + 4);
+#if D2X8_PHASED
+  // metric() in packed pairs, each operation on all four pairs before the next one: no packed
+  // result is read by the next instruction (the dependent v_pk_* pairs otherwise take s_nop)
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
+  const f2 X[4] = {{x0.x, x0.y}, {x0.z, x0.w}, {x1.x, x1.y}, {x1.z, x1.w}};
+  const f2 Y[4] = {{y0.x, y0.y}, {y0.z, y0.w}, {y1.x, y1.y}, {y1.z, y1.w}};
+  const f2 Z[4] = {{z0.x, z0.y}, {z0.z, z0.w}, {z1.x, z1.y}, {z1.z, z1.w}};
+  f2 dx[4], dy[4], dz[4], r[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) dx[i] = qx2 - X[i];
+#pragma unroll
+  for (int i = 0; i < 4; i++) dy[i] = qy2 - Y[i];
+#pragma unroll
+  for (int i = 0; i < 4; i++) dz[i] = qz2 - Z[i];
+#pragma unroll
+  for (int i = 0; i < 4; i++) r[i] = dx[i] * dx[i];
+#pragma unroll
+  for (int i = 0; i < 4; i++) r[i] = __builtin_elementwise_fma(dy[i], dy[i], r[i]);
+#pragma unroll
+  for (int i = 0; i < 4; i++) r[i] = __builtin_elementwise_fma(dz[i], dz[i], r[i]);
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    d[2 * i] = r[i].x;
+    d[2 * i + 1] = r[i].y;
+  }
+#else
   d[0] = metric(qx, qy, qz, make_float4(x0.x, y0.x, z0.x, 0.f));
   d[1] = metric(qx, qy, qz, make_float4(x0.y, y0.y, z0.y, 0.f));
   d[2] = metric(qx, qy, qz, make_float4(x0.z, y0.z, z0.z, 0.f));
@@ -110,6 +140,7 @@ __device__ __forceinline__ void cand_d2x8(const Cands<CAPC> &C, uint32_t s0, flo
   d[5] = metric(qx, qy, qz, make_float4(x1.y, y1.y, z1.y, 0.f));
   d[6] = metric(qx, qy, qz, make_float4(x1.z, y1.z, z1.z, 0.f));
   d[7] = metric(qx, qy, qz, make_float4(x1.w, y1.w, z1.w, 0.f));
+#endif
 }
 
 // squared gap between a point/box and box B, same fp32 operation order as the photon metric
@@ -1171,6 +1202,8 @@ void knn_chunk_lane_kernel(KnnArgs a) {
           fk[i] = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)cidx[sl[i]];
         }
       }
+      // (a Batcher network sized to the wave's largest bracket, 4 / 8 / 12 keys, was measured
+      // slower, r05: 10 -> 35 spilled VGPRs, global k-NN 45.0 -> 47.1 ms per C2 launch)
 #pragma unroll
       for (int i = 0; i < LS_BR_L; i++)
 #pragma unroll

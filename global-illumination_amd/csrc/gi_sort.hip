@@ -22,6 +22,45 @@ __device__ __forceinline__ uint32_t spread10(uint32_t v) {
   return v;
 }
 
+#ifndef KEY_HILBERT
+#define KEY_HILBERT 1
+#endif
+// 30-bit space-filling-curve key of a 10-bit cell (x, y, z). KEY_HILBERT: the 3-D Hilbert curve
+// (Skilling's axes-to-transpose, "Programming the Hilbert curve", AIP Conf. Proc. 707, 2004),
+// its transposed bits interleaved as Morton's are: consecutive keys are face-adjacent cells, so
+// a 64-query chunk of the sorted list is more compact than a Z-order run (a floor patch at C2's
+// query density: chunk radius 0.00170 -> 0.00133, photons gathered per chunk 87 -> 77;
+// tools/sim_chunks.py). Only the order of the k-NN launches changes, never a result.
+__device__ __forceinline__ uint32_t curve_key10(uint32_t x, uint32_t y, uint32_t z) {
+#if KEY_HILBERT
+  uint32_t X[3] = {x, y, z};
+  for (uint32_t Q = 1u << 9; Q > 1u; Q >>= 1) {
+    const uint32_t P = Q - 1u;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      if (X[i] & Q) {
+        X[0] ^= P;  // invert
+      } else {      // exchange
+        const uint32_t t = (X[0] ^ X[i]) & P;
+        X[0] ^= t;
+        X[i] ^= t;
+      }
+    }
+  }
+  X[1] ^= X[0];
+  X[2] ^= X[1];
+  uint32_t t = 0;
+  for (uint32_t Q = 1u << 9; Q > 1u; Q >>= 1)
+    if (X[2] & Q) t ^= Q - 1u;
+  X[0] ^= t;
+  X[1] ^= t;
+  X[2] ^= t;
+  return (spread10(X[0]) << 2) | (spread10(X[1]) << 1) | spread10(X[2]);
+#else
+  return (spread10(x) << 2) | (spread10(y) << 1) | spread10(z);
+#endif
+}
+
 __global__ void morton_kernel(const float4 *q, int64_t n, float ox, float oy, float oz,
                               float sx, float sy, float sz, float cmax, uint32_t *keys, uint32_t *vals) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -30,7 +69,7 @@ __global__ void morton_kernel(const float4 *q, int64_t n, float ox, float oy, fl
   float fx = fminf(fmaxf((p.x - ox) * sx, 0.0f), cmax);
   float fy = fminf(fmaxf((p.y - oy) * sy, 0.0f), cmax);
   float fz = fminf(fmaxf((p.z - oz) * sz, 0.0f), cmax);
-  keys[i] = (spread10((uint32_t)fx) << 2) | (spread10((uint32_t)fy) << 1) | spread10((uint32_t)fz);
+  keys[i] = curve_key10((uint32_t)fx, (uint32_t)fy, (uint32_t)fz);
   vals[i] = (uint32_t)i;
 }
 
@@ -100,9 +139,7 @@ __global__ void morton_valid_kernel(const float4 *q, int64_t n, float ox, float 
   float fx = fminf(fmaxf((p.x - ox) * sx, 0.0f), cmax);
   float fy = fminf(fmaxf((p.y - oy) * sy, 0.0f), cmax);
   float fz = fminf(fmaxf((p.z - oz) * sz, 0.0f), cmax);
-  keys[i] = valid ? ((spread10((uint32_t)fx) << 2) | (spread10((uint32_t)fy) << 1) |
-                     spread10((uint32_t)fz))
-                  : (1u << 30);
+  keys[i] = valid ? curve_key10((uint32_t)fx, (uint32_t)fy, (uint32_t)fz) : (1u << 30);
   vals[i] = (uint32_t)i;
 }
 

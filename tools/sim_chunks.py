@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Chunk compactness of the k-NN launch order (gi_sort.hip curve_key10), simulated on the CPU:
+the global photon map of cornell.scn (oracle restatement, 1M photons), queries uniform on a 0.1 x
+0.1 floor patch at a given density (C2's global list: ~36 M valid queries per unit^2 per batch),
+sorted by 10-bit-per-axis Morton or Hilbert keys and cut into chunks of 64. Per chunk: rho (the
+largest query distance from the box centre) and the photons the chunk kernel gathers (a: within
+d_K(centre) + rho of the chunk box, gi_knn_chunk.hip chunk_bound_gather), with three tighter
+regions for reference (b: ball of d_K(c) + 2 rho around the centre; d: union of the balls
+d_K(c) + |q - c| around each query; c: union of the exact K-balls). Test infrastructure.
+usage: python3 tools/sim_chunks.py [density]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+import numpy as np
+from scipy.spatial import cKDTree
+
+GPOS = '/tmp/gi_sim_gpos.npy'
+if not os.path.exists(GPOS):
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    sys.path.insert(0, os.path.join(ROOT, 'global-illumination_amd'))
+    import oracle_lib
+    g, _c, _e = oracle_lib.map_photons([os.path.join(ROOT, 'tests/scenes/cornell.scn'), '/tmp/x.png',
+                                        '-global', '1000000', '-caustic', '1000000', '-threads', '8'])
+    np.save(GPOS, g['pos'])
+P=np.load(GPOS).astype(np.float32)
+T=cKDTree(P.astype(np.float64))
+bmin=np.array([0,0,0],np.float32); bmax=np.array([1.112,1.0976,1.1184],np.float32)
+def spread(v):
+    v=v.astype(np.uint64)&0x3ff
+    v=(v|(v<<16))&0x30000ff; v=(v|(v<<8))&0x300f00f; v=(v|(v<<4))&0x30c30c3; v=(v|(v<<2))&0x9249249
+    return v
+def morton(f): return (spread(f[:,0])<<2)|(spread(f[:,1])<<1)|spread(f[:,2])
+def hilbert(f, bits=10):
+    # Skilling's AxestoTranspose, vectorized; then interleave transposed bits (x first)
+    X=[f[:,i].astype(np.int64).copy() for i in range(3)]
+    M=1<<(bits-1); Q=M
+    while Q>1:
+        Pm=Q-1
+        for i in range(3):
+            m=(X[i]&Q)!=0
+            # if bit set: invert low bits of X[0]; else exchange low bits of X[0] and X[i]
+            X0=X[0].copy()
+            X[0]=np.where(m, X[0]^Pm, X[0])
+            t=np.where(~m, (X0^X[i])&Pm, 0)
+            X[0]=np.where(~m, X[0]^t, X[0]); X[i]=np.where(~m, X[i]^t, X[i])
+        Q>>=1
+    for i in range(1,3): X[i]^=X[i-1]
+    t=np.zeros_like(X[0]); Q=M
+    while Q>1:
+        t=np.where((X[2]&Q)!=0, t^(Q-1), t); Q>>=1
+    for i in range(3): X[i]^=t
+    key=np.zeros_like(X[0])
+    for b in range(bits-1,-1,-1):
+        for i in range(3):
+            key=(key<<1)|((X[i]>>b)&1)
+    return key
+rng=np.random.default_rng(0)
+K=50; D=float(sys.argv[1]) if len(sys.argv)>1 else 36e6
+n=int(D*0.01)
+q=np.zeros((n,3),np.float32); q[:,0]=0.4+0.1*rng.random(n); q[:,2]=0.4+0.1*rng.random(n)
+f=np.clip((q-bmin)*(1023/(bmax-bmin)),0,1023).astype(np.uint32)
+for name,key in (('morton',morton(f)),('hilbert',hilbert(f))):
+    qs=q[np.argsort(key,kind='stable')]
+    nch=min(n//64-2,2000)
+    sel=np.random.default_rng(1).choice(n//64-2, nch, replace=False)+1
+    res={'a':[],'b':[],'d':[],'c':[],'rho':[]}
+    for ci in sel:
+        Q=qs[ci*64:(ci+1)*64].astype(np.float64)
+        bl,bh=Q.min(0),Q.max(0); cc=0.5*(bl+bh)
+        dq=np.sqrt(((Q-cc)**2).sum(1)); r=dq.max()
+        dk=T.query(cc,K)[0][-1]; U=dk+r
+        idx=T.query_ball_point(cc, U+np.linalg.norm(bh-bl)/2+r+1e-9)
+        pp=P[idx].astype(np.float64)
+        g=np.maximum(np.maximum(bl-pp, pp-bh),0); gd=np.sqrt((g**2).sum(1))
+        res['a'].append((gd<=U).sum())
+        dc=np.sqrt(((pp-cc)**2).sum(1)); res['b'].append((dc<=dk+2*r).sum())
+        dpq=np.sqrt(((pp[:,None,:]-Q[None,:,:])**2).sum(2))
+        res['d'].append((dpq<=(dk+dq)[None,:]).any(1).sum())
+        dkq=T.query(Q,K)[0][:,-1]
+        res['c'].append((dpq<=dkq[None,:]).any(1).sum())
+        res['rho'].append(r)
+    print(name, ' '.join(f"{k}={np.mean(v):.4g}" for k,v in res.items()))

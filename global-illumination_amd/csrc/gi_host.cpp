@@ -358,6 +358,13 @@ struct gi_ctx {
   // render query needs it (GI_KNN_GENERAL=-1; exercises render_common's re-run)
   int knn_general_mode = 0;
   bool sort_all = false;  // GI_SORT_ALL=1: sort / search every list slot, empty ones included
+  // launch-order cells per axis for the global / caustic list (GI_KEY_BITS_G / _C; > 10: 64-bit
+  // keys, gi_sort.hip curve64_valid_kernel). The caustic queries crowd into foci far smaller than
+  // a 10-bit cell of the scene box, where a cell's queries stay in slot order: 16-bit cells cut
+  // the C4 shard's caustic k-NN 207 -> 155 ms per launch (second-pass queries 37.8 % -> 14.9 %).
+  // The global list (C2: 400 M slots, one query per ~cell) keeps 32-bit keys: a 64-bit sort
+  // would cost more than it saves (profiles/r05_key_bits_ab.txt).
+  int key_bits[2] = {10, 16};
   // GI_EARLY_KNN=1: in a batch with Monte Carlo paths on the side stream, the k-NN of the
   // deterministic query slots runs before the join, beside the side stream's tail (off by
   // default: C2 -0.4 % per frame, but the global k-NN launches that share the GPU with the
@@ -1263,7 +1270,8 @@ int knn_list(gi_ctx *c, int mi, const float4 *qpos, const QShade *qshade, int64_
       HIPCHK(c, morton_order(qpos, nq, c->sbmin, c->sbmax, X.sorter, &perm, X.st));
     } else {
       int64_t nv = 0;
-      HIPCHK(c, morton_order_valid(qpos, nq, c->sbmin, c->sbmax, X.sorter, &perm, &nv, X.st));
+      HIPCHK(c, morton_order_valid(qpos, nq, c->sbmin, c->sbmax, X.sorter, &perm, &nv, X.st,
+                                   c->key_bits[mi]));
       nq = nv;
       k.nq = nv;
       if (nv == 0) return GI_OK;
@@ -1706,6 +1714,8 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_IND_FRAC")) c->ind_frac = std::min(1.0, std::max(1e-6, atof(s)));
   if (const char *s = getenv("GI_KNN_KERNEL")) c->knn_kernel_kind = atoi(s);
   if (const char *s = getenv("GI_SORT_ALL")) c->sort_all = atoi(s) != 0;
+  if (const char *s = getenv("GI_KEY_BITS_G")) c->key_bits[0] = std::max(1, std::min(20, atoi(s)));
+  if (const char *s = getenv("GI_KEY_BITS_C")) c->key_bits[1] = std::max(1, std::min(20, atoi(s)));
   if (const char *s = getenv("GI_EARLY_KNN")) c->early_knn = atoi(s) != 0;
   *out = c;
   return GI_OK;

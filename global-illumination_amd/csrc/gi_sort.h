@@ -14,8 +14,10 @@ hipError_t morton_order(const float4 *q, int64_t n, const float bmin[3], const f
 // the same with the empty slots (meta == QMETA_NONE) sorted after every valid query: the first
 // *nvalid entries of the permutation are the valid queries in morton_order's order, so the k-NN
 // launch takes only those (synchronises st for the count)
+// key_bits > 10: cells of key_bits (<= 20) bits per axis and 64-bit keys
 hipError_t morton_order_valid(const float4 *q, int64_t n, const float bmin[3], const float bmax[3],
-                              SortScratch &s, uint32_t **perm_out, int64_t *nvalid, hipStream_t st);
+                              SortScratch &s, uint32_t **perm_out, int64_t *nvalid, hipStream_t st,
+                              int key_bits = 10);
 void sort_scratch_release(SortScratch &s);
 
 struct KeySortScratch {

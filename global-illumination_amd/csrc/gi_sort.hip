@@ -61,6 +61,40 @@ __device__ __forceinline__ uint32_t curve_key10(uint32_t x, uint32_t y, uint32_t
 #endif
 }
 
+// the same curve on B bits per axis (11 <= B <= 20) as a 64-bit key (3B bits)
+__device__ __forceinline__ uint64_t spread21(uint32_t x) {
+  uint64_t v = x & 0x1fffffu;
+  v = (v | (v << 32)) & 0x1f00000000ffffull;
+  v = (v | (v << 16)) & 0x1f0000ff0000ffull;
+  v = (v | (v << 8)) & 0x100f00f00f00f00full;
+  v = (v | (v << 4)) & 0x10c30c30c30c30c3ull;
+  v = (v | (v << 2)) & 0x1249249249249249ull;
+  return v;
+}
+template <int B>
+__device__ __forceinline__ uint64_t curve_key64(uint32_t x, uint32_t y, uint32_t z) {
+  uint32_t X[3] = {x, y, z};
+  for (uint32_t Q = 1u << (B - 1); Q > 1u; Q >>= 1) {
+    const uint32_t P = Q - 1u;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      if (X[i] & Q) {
+        X[0] ^= P;
+      } else {
+        const uint32_t t = (X[0] ^ X[i]) & P;
+        X[0] ^= t;
+        X[i] ^= t;
+      }
+    }
+  }
+  X[1] ^= X[0];
+  X[2] ^= X[1];
+  uint32_t t = 0;
+  for (uint32_t Q = 1u << (B - 1); Q > 1u; Q >>= 1)
+    if (X[2] & Q) t ^= Q - 1u;
+  return (spread21(X[0] ^ t) << 2) | (spread21(X[1] ^ t) << 1) | spread21(X[2] ^ t);
+}
+
 __global__ void morton_kernel(const float4 *q, int64_t n, float ox, float oy, float oz,
                               float sx, float sy, float sz, float cmax, uint32_t *keys, uint32_t *vals) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -143,6 +177,42 @@ __global__ void morton_valid_kernel(const float4 *q, int64_t n, float ox, float 
   vals[i] = (uint32_t)i;
 }
 
+// morton_valid_kernel with B-bit cells (64-bit keys; the empty slots get 2^(3B))
+template <int B>
+__global__ void curve64_valid_kernel(const float4 *q, int64_t n, float ox, float oy, float oz,
+                                     float sx, float sy, float sz, float cmax, uint64_t *keys,
+                                     uint32_t *vals) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float4 p = q[i];
+  const bool valid = __float_as_uint(p.w) != 0xffffffffu;  // QMETA_NONE (gi_kernels.h)
+  float fx = fminf(fmaxf((p.x - ox) * sx, 0.0f), cmax);
+  float fy = fminf(fmaxf((p.y - oy) * sy, 0.0f), cmax);
+  float fz = fminf(fmaxf((p.z - oz) * sz, 0.0f), cmax);
+  keys[i] = valid ? curve_key64<B>((uint32_t)fx, (uint32_t)fy, (uint32_t)fz) : (1ull << (3 * B));
+  vals[i] = (uint32_t)i;
+}
+__global__ void __launch_bounds__(64) first_empty64_kernel(const uint64_t *k, int64_t n,
+                                                           uint64_t empty,
+                                                           unsigned long long *out) {
+  int64_t lo = 0, hi = n;
+  const int lane = threadIdx.x;
+  while (lo < hi) {
+    const int64_t step = (hi - lo + 63) / 64;
+    const int64_t p = lo + lane * step;
+    const uint64_t m = __ballot(p >= hi || k[p] >= empty);
+    if (m == 0) {
+      lo += 63 * step + 1;
+      continue;
+    }
+    const int f = __ffsll((unsigned long long)m) - 1;
+    const int64_t nhi = lo + f * step;
+    lo = f ? lo + (f - 1) * step + 1 : lo;
+    hi = nhi < hi ? nhi : hi;
+  }
+  if (lane == 0) *out = (unsigned long long)lo;
+}
+
 // the number of valid queries = the first sorted key >= 2^30, by a 64-way search in one wave
 // (a per-wave atomic count in morton_valid_kernel serialised 6M same-address atomics: r05i,
 // +32 ms per list)
@@ -167,7 +237,8 @@ __global__ void __launch_bounds__(64) first_empty_kernel(const uint32_t *k, int6
 }
 
 hipError_t morton_order_valid(const float4 *q, int64_t n, const float bmin[3], const float bmax[3],
-                              SortScratch &s, uint32_t **perm_out, int64_t *nvalid, hipStream_t st) {
+                              SortScratch &s, uint32_t **perm_out, int64_t *nvalid, hipStream_t st,
+                              int key_bits) {
   *perm_out = nullptr;
   *nvalid = 0;
   if (n <= 0) return hipSuccess;
@@ -192,12 +263,47 @@ hipError_t morton_order_valid(const float4 *q, int64_t n, const float bmin[3], c
     return r;
   };
   size_t b4 = (size_t)n * 4;
-  if ((e = grow(s.k0, s.k0_cap, b4 + 16)) != hipSuccess) return e;
-  if ((e = grow(s.k1, s.k1_cap, b4)) != hipSuccess) return e;
+  const bool wide = key_bits > 10;
+  const size_t kb = wide ? 2 * b4 : b4;
+  if ((e = grow(s.k0, s.k0_cap, kb + 16)) != hipSuccess) return e;
+  if ((e = grow(s.k1, s.k1_cap, kb)) != hipSuccess) return e;
   if ((e = grow(s.v0, s.v0_cap, b4)) != hipSuccess) return e;
   if ((e = grow(s.v1, s.v1_cap, b4)) != hipSuccess) return e;
   // the valid count lives past the keys (8 B, aligned)
-  auto *d_cnt = reinterpret_cast<unsigned long long *>((char *)s.k0 + ((b4 + 7) & ~(size_t)7));
+  auto *d_cnt = reinterpret_cast<unsigned long long *>((char *)s.k0 + ((kb + 7) & ~(size_t)7));
+  if (wide) {
+    // B-bit cells, 64-bit keys: 3B + 1 key bits, (3B + 1) / 8 rounded up radix passes
+    const int B = key_bits > 20 ? 20 : key_bits;
+    const float cm = (float)((1 << B) - 1);
+    float sw[3];
+    for (int i = 0; i < 3; i++) {
+      float ext = bmax[i] - bmin[i];
+      sw[i] = ext > 0 ? cm / ext : 0.0f;
+    }
+    const unsigned g = (unsigned)((n + 255) / 256);
+#define CURVE64_CASE(b)                                                                      \
+  case b:                                                                                    \
+    curve64_valid_kernel<b><<<g, 256, 0, st>>>(q, n, bmin[0], bmin[1], bmin[2], sw[0], sw[1], \
+                                               sw[2], cm, (uint64_t *)s.k0, (uint32_t *)s.v0); \
+    break;
+    switch (B) {
+      CURVE64_CASE(11) CURVE64_CASE(12) CURVE64_CASE(13) CURVE64_CASE(14) CURVE64_CASE(15)
+      CURVE64_CASE(16) CURVE64_CASE(17) CURVE64_CASE(18) CURVE64_CASE(19) default:
+      CURVE64_CASE(20)
+    }
+#undef CURVE64_CASE
+    size_t tb = 0;
+    e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint64_t *)s.k0, (uint64_t *)s.k1,
+                                           (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0,
+                                           3 * B + 1, st);
+    if (e != hipSuccess) return e;
+    if ((e = grow(s.tmp, s.tmp_cap, tb + 256)) != hipSuccess) return e;
+    e = hipcub::DeviceRadixSort::SortPairs(s.tmp, tb, (const uint64_t *)s.k0, (uint64_t *)s.k1,
+                                           (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0,
+                                           3 * B + 1, st);
+    if (e != hipSuccess) return e;
+    first_empty64_kernel<<<1, 64, 0, st>>>((const uint64_t *)s.k1, n, 1ull << (3 * B), d_cnt);
+  } else {
   constexpr int bits = 10;
   const float cmax = (float)((1 << bits) - 1);
   float sc[3];
@@ -220,6 +326,7 @@ hipError_t morton_order_valid(const float4 *q, int64_t n, const float bmin[3], c
                                          3 * bits + 1, st);
   if (e != hipSuccess) return e;
   first_empty_kernel<<<1, 64, 0, st>>>((const uint32_t *)s.k1, n, d_cnt);
+  }
   unsigned long long nv = 0;
   if ((e = hipMemcpyAsync(&nv, d_cnt, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
   if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;

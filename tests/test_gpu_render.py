@@ -221,14 +221,18 @@ def test_element_pretest_is_exact(scene, monkeypatch):
 
 
 @pytest.mark.parametrize("scene", ["cornell.scn", "jensen.scn"])
-@pytest.mark.parametrize("var", ["GI_SORT_ALL", "GI_EARLY_KNN"])
-def test_knn_launch_order_is_exact(scene, var, monkeypatch):
+@pytest.mark.parametrize("var,vals", [("GI_SORT_ALL", ("0", "1")), ("GI_EARLY_KNN", ("1", "0")),
+                                      ("GI_KEY_BITS_C", ("16", "10")),
+                                      ("GI_KEY_BITS_G", ("10", "20"))])
+def test_knn_launch_order_is_exact(scene, var, vals, monkeypatch):
     """How the photon lookups (PhotonMap_EstimateRadiance, photonmap.cpp) are grouped into
     launches does not change any result: (1) only the valid query slots, sorted ahead of the
     empty ones (gi_sort.hip morton_order_valid), against the r04 order that sorts and walks every
     slot (GI_SORT_ALL=1); (2) the deterministic slots' estimates run before the Monte Carlo side
     stream joins and the appends' after it (GI_EARLY_KNN=1; cornell's hard light runs the plain
-    Monte Carlo kernel, where it applies), against one launch per list after the join (default). The f32 image and the -v counters are equal; -tt/-st 4 give Monte Carlo
+    Monte Carlo kernel, where it applies), against one launch per list after the join (default);
+    (3) the launch order's Hilbert cells per axis (gi_sort.hip: 10 bits in 32-bit keys, more in
+    64-bit keys; defaults 10 global, 16 caustic) against other resolutions. The f32 image and the -v counters are equal; -tt/-st 4 give Monte Carlo
     paths, -it 16 many empty slots."""
     import gi_amd
     import gpu_util
@@ -236,7 +240,7 @@ def test_knn_launch_order_is_exact(scene, var, monkeypatch):
             "-global", "30000", "-caustic", "30000", "-it", "16", "-tt", "4", "-st", "4",
             "-seed", "5"]
     out = []
-    for v in ("0", "1") if var == "GI_SORT_ALL" else ("1", "0"):
+    for v in vals:
         monkeypatch.setenv(var, v)
         r = gi_amd.Renderer(0)
         try:

@@ -365,6 +365,9 @@ struct gi_ctx {
   // The global list (C2: 400 M slots, one query per ~cell) keeps 32-bit keys: a 64-bit sort
   // would cost more than it saves (profiles/r05_key_bits_ab.txt).
   int key_bits[2] = {10, 16};
+  // GI_ROW_ORDER (default 1): the global list's valid slots compacted from the row masks before
+  // the sort (gi_sort.h curve_order_rows) instead of sorting every slot with the empty ones last
+  bool row_order = true;
   // GI_EARLY_KNN=1: in a batch with Monte Carlo paths on the side stream, the k-NN of the
   // deterministic query slots runs before the join, beside the side stream's tail (off by
   // default: C2 -0.4 % per frame, but the global k-NN launches that share the GPU with the
@@ -1244,8 +1247,17 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
 }
 
 // run the k-NN estimate of one query list into out[slot] (Morton-ordered launch)
+// the global list's slot layout (render_pixels): primary slots, tiled indirect slots with their
+// query row masks, appends from qbase (gi_sort.h curve_order_rows)
+struct ListRows {
+  int64_t nprim;
+  const uint64_t *qmask;
+  int64_t trows;
+  uint32_t qbase;
+};
+
 int knn_list(gi_ctx *c, int mi, const float4 *qpos, const QShade *qshade, int64_t nq,
-             double *out, double *ms) {
+             double *out, double *ms, const ListRows *rows = nullptr) {
   MapExec &X = c->mx[mi];
   KnnArgs k = knn_args(c, mi);
   k.qpos = qpos;
@@ -1268,6 +1280,14 @@ int knn_list(gi_ctx *c, int mi, const float4 *qpos, const QShade *qshade, int64_
     uint32_t *perm = nullptr;
     if (c->sort_all) {
       HIPCHK(c, morton_order(qpos, nq, c->sbmin, c->sbmax, X.sorter, &perm, X.st));
+    } else if (rows && c->row_order && c->key_bits[mi] <= 10) {
+      // compacted from the row masks: the empty slots are never read or sorted
+      int64_t nv = 0;
+      HIPCHK(c, curve_order_rows(qpos, rows->nprim, rows->qmask, rows->trows, rows->qbase, nq,
+                                 c->sbmin, c->sbmax, X.sorter, &perm, &nv, X.st));
+      nq = nv;
+      k.nq = nv;
+      if (nv == 0) return GI_OK;
     } else {
       int64_t nv = 0;
       HIPCHK(c, morton_order_valid(qpos, nq, c->sbmin, c->sbmax, X.sorter, &perm, &nv, X.st,
@@ -1548,9 +1568,13 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     for (int l = 0; l < 2; l++) {
       if (!run[l]) continue;
       const uint32_t q0 = early ? qbase[l] : 0u;  // early: the deterministic part is done
+      // the global list's launch order from its row masks (GI_ROW_ORDER, default on)
+      ListRows lr{nprim, a.ind_qmask, (int64_t)(tind / 64), qbase[0]};
+      const bool use_rows = l == 0 && q0 == 0 && a.ind_qmask && (a.total_ind > 0 || tind == 0);
       if (nq[l] > q0)
         rcm[l] = knn_list(c, l, a.qpos[l] + q0, a.qshade[l] + q0, nq[l] - q0,
-                          c->qout[l].as<double>() + 3 * (size_t)q0, rs ? &knn_ms[l] : nullptr);
+                          c->qout[l].as<double>() + 3 * (size_t)q0, rs ? &knn_ms[l] : nullptr,
+                          use_rows ? &lr : nullptr);
       if (rcm[l]) break;
     }
     for (int l = 0; l < 2; l++) {
@@ -1714,6 +1738,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_IND_FRAC")) c->ind_frac = std::min(1.0, std::max(1e-6, atof(s)));
   if (const char *s = getenv("GI_KNN_KERNEL")) c->knn_kernel_kind = atoi(s);
   if (const char *s = getenv("GI_SORT_ALL")) c->sort_all = atoi(s) != 0;
+  if (const char *s = getenv("GI_ROW_ORDER")) c->row_order = atoi(s) != 0;
   if (const char *s = getenv("GI_KEY_BITS_G")) c->key_bits[0] = std::max(1, std::min(20, atoi(s)));
   if (const char *s = getenv("GI_KEY_BITS_C")) c->key_bits[1] = std::max(1, std::min(20, atoi(s)));
   if (const char *s = getenv("GI_EARLY_KNN")) c->early_knn = atoi(s) != 0;

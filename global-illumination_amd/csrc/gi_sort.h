@@ -7,6 +7,9 @@ namespace gi {
 struct SortScratch {
   void *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *v1 = nullptr, *tmp = nullptr;
   size_t k0_cap = 0, k1_cap = 0, v0_cap = 0, v1_cap = 0, tmp_cap = 0;
+  // curve_order_rows: the row masks, their counts / offsets and the compacted slot list
+  void *rows = nullptr, *cnt = nullptr, *vl = nullptr;
+  size_t rows_cap = 0, cnt_cap = 0, vl_cap = 0;
 };
 // returns a device permutation (sorted position -> query index) valid until the next call
 hipError_t morton_order(const float4 *q, int64_t n, const float bmin[3], const float bmax[3],
@@ -18,6 +21,16 @@ hipError_t morton_order(const float4 *q, int64_t n, const float bmin[3], const f
 hipError_t morton_order_valid(const float4 *q, int64_t n, const float bmin[3], const float bmax[3],
                               SortScratch &s, uint32_t **perm_out, int64_t *nvalid, hipStream_t st,
                               int key_bits = 10);
+// The global list's launch order built from its slot layout instead of a sort over every slot:
+// primary slots [0, nprim) (validity read from q), then the tiled indirect slots [nprim,
+// nprim + 64 trows) whose row masks qmask[r] mark the entries holding a query (the reduction's
+// own masks, gi_kernels.hip ind_kernel / ind_cont_kernel), then the appends [qbase, nq), all
+// valid. The valid slots are compacted (row popcounts, a scan, a scatter: no per-slot pass over
+// the empty ones), keyed like morton_order_valid and sorted: the first *nvalid entries of the
+// permutation are the same queries, in the same order, as morton_order_valid's.
+hipError_t curve_order_rows(const float4 *q, int64_t nprim, const uint64_t *qmask, int64_t trows,
+                            uint32_t qbase, int64_t nq, const float bmin[3], const float bmax[3],
+                            SortScratch &s, uint32_t **perm_out, int64_t *nvalid, hipStream_t st);
 void sort_scratch_release(SortScratch &s);
 
 struct KeySortScratch {

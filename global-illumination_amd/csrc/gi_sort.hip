@@ -213,6 +213,47 @@ __global__ void __launch_bounds__(64) first_empty64_kernel(const uint64_t *k, in
   if (lane == 0) *out = (unsigned long long)lo;
 }
 
+// curve_order_rows: bit b of row r = primary slot 64 r + b holds a query (one wave per row)
+__global__ void prim_rows_kernel(const float4 *q, int64_t nprim, uint64_t *rows) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool v = i < nprim && __float_as_uint(q[i].w) != 0xffffffffu;  // QMETA_NONE
+  const uint64_t m = __ballot(v);
+  if ((threadIdx.x & 63) == 0 && i < nprim) rows[i >> 6] = m;
+}
+__global__ void row_popc_kernel(const uint64_t *rows, int64_t R, uint32_t *cnt) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < R) cnt[r] = (uint32_t)__popcll(rows[r]);
+}
+// lane b of row r's wave writes slot(r, b) to its rank among the row's set bits
+__global__ void row_scatter_kernel(const uint64_t *rows, const uint32_t *off, int64_t Rp,
+                                   int64_t R, int64_t nprim, uint32_t *vl) {
+  const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= R) return;
+  const uint64_t m = rows[r];
+  if ((m >> lane) & 1ull) {
+    const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    const int64_t slot = r < Rp ? 64 * r + lane : nprim + 64 * (r - Rp) + lane;
+    vl[off[r] + rank] = (uint32_t)slot;
+  }
+}
+// keys of the compacted list: entries [0, ndet) from vl, then the appends qbase + (i - ndet)
+__global__ void curve_list_kernel(const float4 *q, const uint32_t *vl, int64_t ndet,
+                                  uint32_t qbase, int64_t n, float ox, float oy, float oz,
+                                  float sx, float sy, float sz, float cmax, uint32_t *keys,
+                                  uint32_t *vals) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t slot = i < ndet ? vl[i] : qbase + (uint32_t)(i - ndet);
+  const float4 p = q[slot];
+  const bool valid = __float_as_uint(p.w) != 0xffffffffu;  // (always, by the masks)
+  float fx = fminf(fmaxf((p.x - ox) * sx, 0.0f), cmax);
+  float fy = fminf(fmaxf((p.y - oy) * sy, 0.0f), cmax);
+  float fz = fminf(fmaxf((p.z - oz) * sz, 0.0f), cmax);
+  keys[i] = valid ? curve_key10((uint32_t)fx, (uint32_t)fy, (uint32_t)fz) : (1u << 30);
+  vals[i] = slot;
+}
+
 // the number of valid queries = the first sorted key >= 2^30, by a 64-way search in one wave
 // (a per-wave atomic count in morton_valid_kernel serialised 6M same-address atomics: r05i,
 // +32 ms per list)
@@ -392,10 +433,99 @@ void sort_scratch_release(KeySortScratch &s) {
 }
 
 void sort_scratch_release(SortScratch &s) {
-  void *ps[] = {s.k0, s.k1, s.v0, s.v1, s.tmp};
+  void *ps[] = {s.k0, s.k1, s.v0, s.v1, s.tmp, s.rows, s.cnt, s.vl};
   for (void *p : ps)
     if (p) hipFree(p);
   s = SortScratch();
+}
+
+hipError_t curve_order_rows(const float4 *q, int64_t nprim, const uint64_t *qmask, int64_t trows,
+                            uint32_t qbase, int64_t nq, const float bmin[3], const float bmax[3],
+                            SortScratch &s, uint32_t **perm_out, int64_t *nvalid, hipStream_t st) {
+  *perm_out = nullptr;
+  *nvalid = 0;
+  if (nq <= 0) return hipSuccess;
+  hipError_t e;
+  auto grow = [&](void *&p, size_t &cap, size_t bytes) -> hipError_t {
+    if (bytes <= cap && p) return hipSuccess;
+    size_t want = cap ? std::max(bytes, cap + cap / 2) : bytes;  // headroom (gi_host.cpp DBuf)
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (want > bytes) {
+      size_t fr = 0, tot = 0;
+      if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < want + tot / 4) want = bytes;
+    }
+    hipError_t r = hipMalloc(&p, want);
+    if (r != hipSuccess && want > bytes) {
+      (void)hipGetLastError();
+      want = bytes;
+      r = hipMalloc(&p, want);
+    }
+    if (r == hipSuccess) cap = want;
+    return r;
+  };
+  const int64_t Rp = (nprim + 63) / 64, R = Rp + trows;
+  if ((e = grow(s.rows, s.rows_cap, (size_t)(R + 1) * 8)) != hipSuccess) return e;
+  if ((e = grow(s.cnt, s.cnt_cap, (size_t)(2 * R + 2) * 4)) != hipSuccess) return e;
+  uint64_t *rows = (uint64_t *)s.rows;
+  uint32_t *cnt = (uint32_t *)s.cnt, *off = cnt + (R + 1);
+  if (nprim > 0) prim_rows_kernel<<<(unsigned)((nprim + 255) / 256), 256, 0, st>>>(q, nprim, rows);
+  if (trows > 0 &&
+      (e = hipMemcpyAsync(rows + Rp, qmask, (size_t)trows * 8, hipMemcpyDeviceToDevice, st)) != hipSuccess)
+    return e;
+  if (R > 0) row_popc_kernel<<<(unsigned)((R + 255) / 256), 256, 0, st>>>(rows, R, cnt);
+  // exclusive offsets of the rows' counts, the total at off[R]
+  if ((e = hipMemsetAsync(cnt + R, 0, 4, st)) != hipSuccess) return e;
+  size_t tb = 0;
+  e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, off, (int)(R + 1), st);
+  if (e != hipSuccess) return e;
+  if ((e = grow(s.tmp, s.tmp_cap, tb + 256)) != hipSuccess) return e;
+  e = hipcub::DeviceScan::ExclusiveSum(s.tmp, tb, cnt, off, (int)(R + 1), st);
+  if (e != hipSuccess) return e;
+  uint32_t ndet = 0;
+  if ((e = hipMemcpyAsync(&ndet, off + R, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+  if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+  const int64_t napp = nq > (int64_t)qbase ? nq - (int64_t)qbase : 0;
+  const int64_t n = (int64_t)ndet + napp;
+  if (n == 0) return hipSuccess;
+  size_t b4 = (size_t)n * 4;
+  if ((e = grow(s.vl, s.vl_cap, (size_t)ndet * 4 + 4)) != hipSuccess) return e;
+  if ((e = grow(s.k0, s.k0_cap, b4 + 16)) != hipSuccess) return e;
+  if ((e = grow(s.k1, s.k1_cap, b4)) != hipSuccess) return e;
+  if ((e = grow(s.v0, s.v0_cap, b4)) != hipSuccess) return e;
+  if ((e = grow(s.v1, s.v1_cap, b4)) != hipSuccess) return e;
+  if (R > 0)
+    row_scatter_kernel<<<(unsigned)((R + 3) / 4), 256, 0, st>>>(rows, off, Rp, R, nprim,
+                                                                 (uint32_t *)s.vl);
+  constexpr int bits = 10;
+  const float cmax = (float)((1 << bits) - 1);
+  float sc[3];
+  for (int i = 0; i < 3; i++) {
+    float ext = bmax[i] - bmin[i];
+    sc[i] = ext > 0 ? cmax / ext : 0.0f;
+  }
+  curve_list_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(
+      q, (const uint32_t *)s.vl, (int64_t)ndet, qbase, n, bmin[0], bmin[1], bmin[2], sc[0], sc[1],
+      sc[2], cmax, (uint32_t *)s.k0, (uint32_t *)s.v0);
+  auto *d_cnt = reinterpret_cast<unsigned long long *>((char *)s.k0 + ((b4 + 7) & ~(size_t)7));
+  tb = 0;
+  e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t *)s.k0, (uint32_t *)s.k1,
+                                         (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0,
+                                         3 * bits + 1, st);
+  if (e != hipSuccess) return e;
+  if ((e = grow(s.tmp, s.tmp_cap, tb + 256)) != hipSuccess) return e;
+  e = hipcub::DeviceRadixSort::SortPairs(s.tmp, tb, (const uint32_t *)s.k0, (uint32_t *)s.k1,
+                                         (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0,
+                                         3 * bits + 1, st);
+  if (e != hipSuccess) return e;
+  first_empty_kernel<<<1, 64, 0, st>>>((const uint32_t *)s.k1, n, d_cnt);
+  unsigned long long nv = 0;
+  if ((e = hipMemcpyAsync(&nv, d_cnt, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+  if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+  *nvalid = (int64_t)nv;
+  *perm_out = (uint32_t *)s.v1;
+  return hipSuccess;
 }
 
 }  // namespace gi

@@ -223,7 +223,8 @@ def test_element_pretest_is_exact(scene, monkeypatch):
 @pytest.mark.parametrize("scene", ["cornell.scn", "jensen.scn"])
 @pytest.mark.parametrize("var,vals", [("GI_SORT_ALL", ("0", "1")), ("GI_EARLY_KNN", ("1", "0")),
                                       ("GI_KEY_BITS_C", ("16", "10")),
-                                      ("GI_KEY_BITS_G", ("10", "20"))])
+                                      ("GI_KEY_BITS_G", ("10", "20")),
+                                      ("GI_ROW_ORDER", ("1", "0"))])
 def test_knn_launch_order_is_exact(scene, var, vals, monkeypatch):
     """How the photon lookups (PhotonMap_EstimateRadiance, photonmap.cpp) are grouped into
     launches does not change any result: (1) only the valid query slots, sorted ahead of the
@@ -232,7 +233,9 @@ def test_knn_launch_order_is_exact(scene, var, vals, monkeypatch):
     stream joins and the appends' after it (GI_EARLY_KNN=1; cornell's hard light runs the plain
     Monte Carlo kernel, where it applies), against one launch per list after the join (default);
     (3) the launch order's Hilbert cells per axis (gi_sort.hip: 10 bits in 32-bit keys, more in
-    64-bit keys; defaults 10 global, 16 caustic) against other resolutions. The f32 image and the -v counters are equal; -tt/-st 4 give Monte Carlo
+    64-bit keys; defaults 10 global, 16 caustic) against other resolutions; (4) the global list's
+    valid slots compacted from the indirect row masks before the sort (GI_ROW_ORDER=1, default)
+    against the sort of every slot with the empty ones last. The f32 image and the -v counters are equal; -tt/-st 4 give Monte Carlo
     paths, -it 16 many empty slots."""
     import gi_amd
     import gpu_util

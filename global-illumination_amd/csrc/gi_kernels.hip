@@ -590,13 +590,41 @@ __device__ __forceinline__ void path_init(PathCtx &P, const RenderArgs &a, int64
   P.cont_slot = -1;
 }
 
+// the six -v counters of a wave, two per 64-bit word through three wave reductions instead of
+// six (a lane's counts are below 2^25, so 64 of them cannot carry into the upper half; a wave
+// with a larger count, never seen, takes the six reductions)
 __device__ __forceinline__ void path_stats(const RenderArgs &a, const Counts &cnt) {
-  wave_add(&a.stats[ST_SHADOW], cnt.shadow);
-  wave_add(&a.stats[ST_MONTE], cnt.monte);
-  wave_add(&a.stats[ST_TRANS], cnt.trans);
-  wave_add(&a.stats[ST_SPEC], cnt.spec);
-  wave_add(&a.stats[ST_INDIRECT], cnt.indirect);
-  wave_add(&a.stats[ST_CAUSTIC], cnt.caustic);
+#ifndef PACKED_STATS
+#define PACKED_STATS 1
+#endif
+  const uint32_t any = cnt.shadow | cnt.monte | cnt.trans | cnt.spec | cnt.indirect | cnt.caustic;
+  if (!PACKED_STATS || __ballot((any >> 25) != 0u)) {
+    wave_add(&a.stats[ST_SHADOW], cnt.shadow);
+    wave_add(&a.stats[ST_MONTE], cnt.monte);
+    wave_add(&a.stats[ST_TRANS], cnt.trans);
+    wave_add(&a.stats[ST_SPEC], cnt.spec);
+    wave_add(&a.stats[ST_INDIRECT], cnt.indirect);
+    wave_add(&a.stats[ST_CAUSTIC], cnt.caustic);
+    return;
+  }
+  uint64_t v0 = (uint64_t)cnt.shadow | ((uint64_t)cnt.monte << 32);
+  uint64_t v1 = (uint64_t)cnt.trans | ((uint64_t)cnt.spec << 32);
+  uint64_t v2 = (uint64_t)cnt.indirect | ((uint64_t)cnt.caustic << 32);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    v0 += __shfl_xor(v0, o, 64);
+    v1 += __shfl_xor(v1, o, 64);
+    v2 += __shfl_xor(v2, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    unsigned long long *sd = stat_stripe(a.stats);
+    const uint64_t v[6] = {v0 & 0xffffffffu, v0 >> 32, v1 & 0xffffffffu, v1 >> 32,
+                           v2 & 0xffffffffu, v2 >> 32};
+    const int id[6] = {ST_SHADOW, ST_MONTE, ST_TRANS, ST_SPEC, ST_INDIRECT, ST_CAUSTIC};
+#pragma unroll
+    for (int i = 0; i < 6; i++)
+      if (v[i]) atomicAdd(sd + id[i], (unsigned long long)v[i]);
+  }
 }
 
 // Path slots of primary sample p are [path_off[p], path_off[p+1]): slot 0 = the sample's own

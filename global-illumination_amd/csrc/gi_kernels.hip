@@ -594,11 +594,8 @@ __device__ __forceinline__ void path_init(PathCtx &P, const RenderArgs &a, int64
 // six (a lane's counts are below 2^25, so 64 of them cannot carry into the upper half; a wave
 // with a larger count, never seen, takes the six reductions)
 __device__ __forceinline__ void path_stats(const RenderArgs &a, const Counts &cnt) {
-#ifndef PACKED_STATS
-#define PACKED_STATS 1
-#endif
   const uint32_t any = cnt.shadow | cnt.monte | cnt.trans | cnt.spec | cnt.indirect | cnt.caustic;
-  if (!PACKED_STATS || __ballot((any >> 25) != 0u)) {
+  if (__ballot((any >> 25) != 0u)) {
     wave_add(&a.stats[ST_SHADOW], cnt.shadow);
     wave_add(&a.stats[ST_MONTE], cnt.monte);
     wave_add(&a.stats[ST_TRANS], cnt.trans);
@@ -1517,11 +1514,30 @@ __global__ __launch_bounds__(256) void reduce_prim_kernel(RenderArgs a) {
   const int M = (int)((int64_t)a.ind_rows[T + 1] - r0);
   double c0 = 0, c1 = 0, c2 = 0;
   const double *bs = a.base;
+  // RB entries' loads are issued before their additions (the sums stay in order): a primary on
+  // the glass has hundreds of Monte Carlo paths and appends, and one dependent memory round trip
+  // per entry made it the batch's longest thread
+#ifndef REDUCE_RB
+#define REDUCE_RB 8
+#endif
+  constexpr int RB = REDUCE_RB;
   if (own)
-    for (uint32_t g = a.path_off[b], p1 = a.path_off[b + 1]; g < p1; g++) {
-      c0 += bs[3 * (int64_t)g];
-      c1 += bs[3 * (int64_t)g + 1];
-      c2 += bs[3 * (int64_t)g + 2];
+    for (uint32_t g0 = a.path_off[b], p1 = a.path_off[b + 1]; g0 < p1; g0 += RB) {
+      double v[3 * RB];
+#pragma unroll
+      for (int u = 0; u < RB; u++) {
+        const int64_t g = g0 + u < p1 ? (int64_t)g0 + u : (int64_t)g0;
+        v[3 * u] = bs[3 * g];
+        v[3 * u + 1] = bs[3 * g + 1];
+        v[3 * u + 2] = bs[3 * g + 2];
+      }
+#pragma unroll
+      for (int u = 0; u < RB; u++)
+        if (g0 + u < p1) {
+          c0 += v[3 * u];
+          c1 += v[3 * u + 1];
+          c2 += v[3 * u + 2];
+        }
     }
   tiled_row_sum(a.ind_bmask, bs + 3 * a.ind_g0, r0, M, lane, c0, c1, c2);
   // each list in (primary, slot in primary, query in path) order: the primary's own query
@@ -1539,8 +1555,34 @@ __global__ __launch_bounds__(256) void reduce_prim_kernel(RenderArgs a) {
     };
     if (own) {
       add(b);
-      uint32_t q0 = a.qseg[l][b], q1 = a.qseg[l][b + 1];
-      for (uint32_t q = q0; q < q1; q++) add((int64_t)a.qapp[l] + a.sslot[l][q]);
+      const uint32_t q0 = a.qseg[l][b], q1 = a.qseg[l][b + 1];
+      const uint32_t *ss = a.sslot[l];
+      const int64_t qa = (int64_t)a.qapp[l];
+      for (uint32_t qb = q0; qb < q1; qb += RB) {
+        int64_t sl[RB];
+        bool on[RB];
+        double v[3 * RB];
+#pragma unroll
+        for (int u = 0; u < RB; u++) sl[u] = qa + ss[qb + u < q1 ? qb + u : qb];
+#pragma unroll
+        for (int u = 0; u < RB; u++) on[u] = qb + u < q1 && qk[sl[u]] != ~0ull;
+#pragma unroll
+        for (int u = 0; u < RB; u++) {
+          v[3 * u] = v[3 * u + 1] = v[3 * u + 2] = 0.0;
+          if (on[u]) {
+            v[3 * u] = qo[3 * sl[u]];
+            v[3 * u + 1] = qo[3 * sl[u] + 1];
+            v[3 * u + 2] = qo[3 * sl[u] + 2];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < RB; u++)
+          if (on[u]) {
+            c0 += v[3 * u];
+            c1 += v[3 * u + 1];
+            c2 += v[3 * u + 2];
+          }
+      }
     }
     if (l == 0) tiled_row_sum(a.ind_qmask, qo + 3 * a.qind_base, r0, M, lane, c0, c1, c2);
   }

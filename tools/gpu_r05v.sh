@@ -1,0 +1,15 @@
+#!/bin/bash
+# r05: reduce_prim loads issued 8 entries ahead of their in-order sums (in-tree) against exp/base (REDUCE_RB=1):
+# parity suites on the in-tree library, then the interleaved C2 / C3 A/B (tools/gpu_ab.sh).
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+D=gpurun_out/r05v
+mkdir -p $D
+timeout -k 10 900 python -u -m pytest tests/test_gpu_render.py tests/test_gpu_configs.py tests/test_gpu_scenes.py tests/test_gpu_features.py -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread > $D/pytest.log 2>&1
+rc=$?
+tail -3 $D/pytest.log
+[ $rc -le 1 ] || exit $rc
+bash tools/gpu_ab.sh 2 || exit 1
+grep -h '"global"' /dev/null; for f in gpurun_out/ab/c2.*.log; do grep '^{' $f | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$f', 'global', r['global']['avg_launch_ms'], 'frac', r['frac'], 'caustic', r['caustic_kernel']['avg_launch_ms'])"; done
+exit $rc

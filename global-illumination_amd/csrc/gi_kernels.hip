@@ -1946,6 +1946,10 @@ void launch_path(const RenderArgs &a, hipStream_t st, hipStream_t st2, hipEvent_
     (void)hipEventRecord(fork, st);
     (void)hipStreamWaitEvent(st2, fork, 0);
   }
+  // the primaries' own slots first: enqueued behind the Monte Carlo kernel, this small kernel
+  // waited for CU slots until that kernel's blocks drained (cold C2 frame: 47 ms), holding back
+  // the indirect kernel behind it on st; it reads and writes nothing the Monte Carlo paths touch
+  if (a.nprim > 0) slot0_kernel<<<nblk(a.nprim, 256), 256, 0, st>>>(a);
   if (a.total_mc > 0) {
     unsigned g = nblk(a.total_mc, 128);
     if (a.mc_cont && a.mc_next) {
@@ -1982,7 +1986,6 @@ void launch_path(const RenderArgs &a, hipStream_t st, hipStream_t st2, hipEvent_
       mc_kernel<KINDS_ALL, false, false><<<g, 128, 0, ms>>>(a);
     }
   }
-  if (a.nprim > 0) slot0_kernel<<<nblk(a.nprim, 256), 256, 0, st>>>(a);
   if (a.total_ind > 0) {
     unsigned g = nblk(a.tind, 128);
     if (!a.split_ind) ind_kernel<2, false, KINDS_ALL><<<g, 128, 0, st>>>(a);

@@ -3,7 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-D=gpurun_out/r05o
+D=${D:-gpurun_out/r05o}
 mkdir -p $D
 timeout -k 10 300 python3 bench.py --scene jensen.scn --global-photons 2176 --caustic-photons 4000000 --steps 2 --warmup 1 --no-cpu-baseline > $D/c3.log 2>&1 || { tail -5 $D/c3.log; exit 1; }
 grep '^{' $D/c3.log | tail -1 > $D/c3.json

@@ -308,8 +308,10 @@ def main():
         except ImportError:
             pass
 
-    # the first frame (the drop-in CLI renders exactly one): its device buffers are sized
-    # before the first batch (gi_host.cpp presize_batches), reported as first_frame_ms
+    # the first frame (the drop-in CLI renders exactly one), reported as first_frame_ms: its
+    # device buffers grow during it (started right after another process that
+    # held >100 GB of the GPU exits, an allocation can wait seconds for the driver to clear
+    # that memory)
     first_ms = None
     for i in range(a.warmup):
         if i == 0:

@@ -58,7 +58,11 @@ struct DBuf {
     return grow(bytes);
   }
   hipError_t grow(size_t bytes) {
-    size_t grown = cap ? cap + cap / 2 : 0;
+    // headroom for a buffer that has grown before: 1.5x the old capacity, but at most 1/8 above
+    // the request (the device memory a process leaves behind is cleared by the driver before
+    // another process can use it: a next process that needs more than the clean remainder waits
+    // seconds, so the footprint is kept near what a frame needs)
+    size_t grown = cap ? std::min(cap + cap / 2, bytes + bytes / 8) : 0;
     if (p) hipFree(p);
     p = nullptr;
     cap = 0;

@@ -114,7 +114,7 @@ hipError_t morton_order(const float4 *q, int64_t n, const float bmin[3], const f
   hipError_t e;
   auto grow = [&](void *&p, size_t &cap, size_t bytes) -> hipError_t {
     if (bytes <= cap && p) return hipSuccess;
-    size_t want = cap ? std::max(bytes, cap + cap / 2) : bytes;  // headroom (gi_host.cpp DBuf)
+    size_t want = cap ? std::max(bytes, std::min(cap + cap / 2, bytes + bytes / 8)) : bytes;  // headroom (gi_host.cpp DBuf)
     if (p) hipFree(p);
     p = nullptr;
     cap = 0;
@@ -286,7 +286,7 @@ hipError_t morton_order_valid(const float4 *q, int64_t n, const float bmin[3], c
   hipError_t e;
   auto grow = [&](void *&p, size_t &cap, size_t bytes) -> hipError_t {
     if (bytes <= cap && p) return hipSuccess;
-    size_t want = cap ? std::max(bytes, cap + cap / 2) : bytes;  // headroom (gi_host.cpp DBuf)
+    size_t want = cap ? std::max(bytes, std::min(cap + cap / 2, bytes + bytes / 8)) : bytes;  // headroom (gi_host.cpp DBuf)
     if (p) hipFree(p);
     p = nullptr;
     cap = 0;
@@ -389,7 +389,7 @@ hipError_t key_order(const uint64_t *keys, int64_t n, int key_bits, KeySortScrat
   hipError_t e;
   auto grow = [&](void *&p, size_t &cap, size_t bytes) -> hipError_t {
     if (bytes <= cap && p) return hipSuccess;
-    size_t want = cap ? std::max(bytes, cap + cap / 2) : bytes;  // headroom (gi_host.cpp DBuf)
+    size_t want = cap ? std::max(bytes, std::min(cap + cap / 2, bytes + bytes / 8)) : bytes;  // headroom (gi_host.cpp DBuf)
     if (p) hipFree(p);
     p = nullptr;
     cap = 0;
@@ -448,7 +448,7 @@ hipError_t curve_order_rows(const float4 *q, int64_t nprim, const uint64_t *qmas
   hipError_t e;
   auto grow = [&](void *&p, size_t &cap, size_t bytes) -> hipError_t {
     if (bytes <= cap && p) return hipSuccess;
-    size_t want = cap ? std::max(bytes, cap + cap / 2) : bytes;  // headroom (gi_host.cpp DBuf)
+    size_t want = cap ? std::max(bytes, std::min(cap + cap / 2, bytes + bytes / 8)) : bytes;  // headroom (gi_host.cpp DBuf)
     if (p) hipFree(p);
     p = nullptr;
     cap = 0;

@@ -1,6 +1,6 @@
 #!/bin/bash
 # r05: MC figure pins + group-kernel parity, then C2 A/B of the large-K group fallback
-# (GI_KNN_GROUP / GI_GROUP_CAP), then tools/gpu_r05b.sh (C4 path-kernel A/B, cold frames).
+# (GI_KNN_GROUP / GI_GROUP_CAP), then tools/r05/gpu_r05b.sh (C4 path-kernel A/B, cold frames).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -16,5 +16,5 @@ for g in "1 512" "2 512" "4 512" "4 320" "2 320"; do
   GI_KNN_GROUP=$1 GI_GROUP_CAP=$2 timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $D/c2_g$1_$2.log 2>&1 || { tail -5 $D/c2_g$1_$2.log; exit 1; }
   grep '^{' $D/c2_g$1_$2.log | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); c=d['roofline']['caustic_kernel']; print('group $1 cap $2', d['value'], d['ms_per_step'], 'caustic', c['avg_launch_ms'], 'fallback', c['fallback_avg_ms'], c['fallback_query_frac'], d['image_sha16'])"
 done
-bash tools/gpu_r05b.sh
+bash tools/r05/gpu_r05b.sh
 exit $rc

@@ -7,4 +7,4 @@ D=gpurun_out/r05z
 mkdir -p $D
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $D/smoke.log 2>&1 || { tail -5 $D/smoke.log; exit 1; }
 tail -1 $D/smoke.log
-bash tools/gpu_r05o.sh
+bash tools/r05/gpu_r05o.sh

@@ -335,6 +335,8 @@ __device__ __forceinline__ void wave_estimate(const KnnArgs &a, int64_t qi, floa
 #ifndef SWEEP_H
 #define SWEEP_H 6
 #endif
+// a sweep reads one leaf box per lane: at most 64 leaves (SWEEP_H 7 gave wrong sets, r05)
+static_assert(SWEEP_H >= 0 && SWEEP_H <= 6, "leaf sweep: one leaf per lane of a 64-wide wave");
 template <int CAP, int LB, bool PROF, bool FUSE, bool SWEEP, bool GEN = true>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FUSE ? WAVE_WPE : 1)))
 void knn_wave_kernel(KnnArgs a) {

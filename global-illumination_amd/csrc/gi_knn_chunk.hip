@@ -289,6 +289,7 @@ struct ChunkProf {
 #ifndef CHUNK_SWEEP_H
 #define CHUNK_SWEEP_H 6
 #endif
+static_assert(CHUNK_SWEEP_H >= 0 && CHUNK_SWEEP_H <= 6, "leaf sweep: one leaf per lane of a 64-wide wave");
 template <typename BoxD, typename Leaf>
 __device__ __forceinline__ uint32_t walk_within(const float *nodes, int L, float bound, uint32_t *stk,
                                                 BoxD boxd, Leaf leaf, int root = 1) {

@@ -1726,6 +1726,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_PHOTON_RATE0"))  // test knob: first launch's slots per photon
     c->prate[0] = c->prate[1] = std::max(0.0, atof(s));
   if (const char *s = getenv("GI_CHUNK_MINSUB_BIG")) c->chunk_minsub_big = std::min(64, std::max(1, atoi(s)));
+  if (const char *s = getenv("GI_CHUNK_CAP_BIG")) c->chunk_cap_big = std::max(1, atoi(s));
   if (const char *s = getenv("GI_CHUNK_CAP_BIG2")) c->chunk_cap_big2 = atoi(s);
   if (const char *s = getenv("GI_CHUNK_CAP_BIG3")) c->chunk_cap_big3 = atoi(s);
   if (const char *s = getenv("GI_CHUNK_MINSUB")) c->chunk_minsub = std::min(64, std::max(1, atoi(s)));

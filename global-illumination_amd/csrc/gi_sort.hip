@@ -10,6 +10,10 @@
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
 #include "gi_sort.h"
+#ifndef FUSED_ROW_KEYS
+#define FUSED_ROW_KEYS 1
+#endif
+#define FUSED_ROW_KEYS_ON FUSED_ROW_KEYS
 
 namespace gi {
 
@@ -254,6 +258,43 @@ __global__ void curve_list_kernel(const float4 *q, const uint32_t *vl, int64_t n
   vals[i] = slot;
 }
 
+// the scatter and the keys in one pass (FUSED_ROW_KEYS): lane b of row r's wave writes the key
+// and slot of its query at the query's compacted position; the appends get theirs in
+// append_keys_kernel. Same keys at the same positions as row_scatter + curve_list.
+__device__ __forceinline__ uint32_t slot_key10(const float4 *q, uint32_t slot, float ox, float oy,
+                                               float oz, float sx, float sy, float sz, float cmax) {
+  const float4 p = q[slot];
+  const bool valid = __float_as_uint(p.w) != 0xffffffffu;  // (always, by the masks)
+  float fx = fminf(fmaxf((p.x - ox) * sx, 0.0f), cmax);
+  float fy = fminf(fmaxf((p.y - oy) * sy, 0.0f), cmax);
+  float fz = fminf(fmaxf((p.z - oz) * sz, 0.0f), cmax);
+  return valid ? curve_key10((uint32_t)fx, (uint32_t)fy, (uint32_t)fz) : (1u << 30);
+}
+__global__ void row_keys_kernel(const uint64_t *rows, const uint32_t *off, int64_t Rp, int64_t R,
+                                int64_t nprim, const float4 *q, float ox, float oy, float oz,
+                                float sx, float sy, float sz, float cmax, uint32_t *keys,
+                                uint32_t *vals) {
+  const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= R) return;
+  const uint64_t m = rows[r];
+  if ((m >> lane) & 1ull) {
+    const uint32_t at = off[r] + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    const uint32_t slot = (uint32_t)(r < Rp ? 64 * r + lane : nprim + 64 * (r - Rp) + lane);
+    keys[at] = slot_key10(q, slot, ox, oy, oz, sx, sy, sz, cmax);
+    vals[at] = slot;
+  }
+}
+__global__ void append_keys_kernel(const float4 *q, uint32_t qbase, int64_t napp, int64_t ndet,
+                                   float ox, float oy, float oz, float sx, float sy, float sz,
+                                   float cmax, uint32_t *keys, uint32_t *vals) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= napp) return;
+  const uint32_t slot = qbase + (uint32_t)i;
+  keys[ndet + i] = slot_key10(q, slot, ox, oy, oz, sx, sy, sz, cmax);
+  vals[ndet + i] = slot;
+}
+
 // the number of valid queries = the first sorted key >= 2^30, by a 64-way search in one wave
 // (a per-wave atomic count in morton_valid_kernel serialised 6M same-address atomics: r05i,
 // +32 ms per list)
@@ -490,14 +531,11 @@ hipError_t curve_order_rows(const float4 *q, int64_t nprim, const uint64_t *qmas
   const int64_t n = (int64_t)ndet + napp;
   if (n == 0) return hipSuccess;
   size_t b4 = (size_t)n * 4;
-  if ((e = grow(s.vl, s.vl_cap, (size_t)ndet * 4 + 4)) != hipSuccess) return e;
+  if (!FUSED_ROW_KEYS_ON && (e = grow(s.vl, s.vl_cap, (size_t)ndet * 4 + 4)) != hipSuccess) return e;
   if ((e = grow(s.k0, s.k0_cap, b4 + 16)) != hipSuccess) return e;
   if ((e = grow(s.k1, s.k1_cap, b4)) != hipSuccess) return e;
   if ((e = grow(s.v0, s.v0_cap, b4)) != hipSuccess) return e;
   if ((e = grow(s.v1, s.v1_cap, b4)) != hipSuccess) return e;
-  if (R > 0)
-    row_scatter_kernel<<<(unsigned)((R + 3) / 4), 256, 0, st>>>(rows, off, Rp, R, nprim,
-                                                                 (uint32_t *)s.vl);
   constexpr int bits = 10;
   const float cmax = (float)((1 << bits) - 1);
   float sc[3];
@@ -505,9 +543,23 @@ hipError_t curve_order_rows(const float4 *q, int64_t nprim, const uint64_t *qmas
     float ext = bmax[i] - bmin[i];
     sc[i] = ext > 0 ? cmax / ext : 0.0f;
   }
-  curve_list_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(
-      q, (const uint32_t *)s.vl, (int64_t)ndet, qbase, n, bmin[0], bmin[1], bmin[2], sc[0], sc[1],
-      sc[2], cmax, (uint32_t *)s.k0, (uint32_t *)s.v0);
+  if (FUSED_ROW_KEYS) {
+    if (R > 0)
+      row_keys_kernel<<<(unsigned)((R + 3) / 4), 256, 0, st>>>(
+          rows, off, Rp, R, nprim, q, bmin[0], bmin[1], bmin[2], sc[0], sc[1], sc[2], cmax,
+          (uint32_t *)s.k0, (uint32_t *)s.v0);
+    if (napp > 0)
+      append_keys_kernel<<<(unsigned)((napp + 255) / 256), 256, 0, st>>>(
+          q, qbase, napp, (int64_t)ndet, bmin[0], bmin[1], bmin[2], sc[0], sc[1], sc[2], cmax,
+          (uint32_t *)s.k0, (uint32_t *)s.v0);
+  } else {
+    if (R > 0)
+      row_scatter_kernel<<<(unsigned)((R + 3) / 4), 256, 0, st>>>(rows, off, Rp, R, nprim,
+                                                                   (uint32_t *)s.vl);
+    curve_list_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(
+        q, (const uint32_t *)s.vl, (int64_t)ndet, qbase, n, bmin[0], bmin[1], bmin[2], sc[0],
+        sc[1], sc[2], cmax, (uint32_t *)s.k0, (uint32_t *)s.v0);
+  }
   auto *d_cnt = reinterpret_cast<unsigned long long *>((char *)s.k0 + ((b4 + 7) & ~(size_t)7));
   tb = 0;
   e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t *)s.k0, (uint32_t *)s.k1,

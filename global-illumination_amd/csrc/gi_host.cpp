@@ -1741,6 +1741,7 @@ int gi_create(gi_ctx **out, int dev) {
   if (const char *s = getenv("GI_ELEM_PRETEST")) c->elem_pretest = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_FB_ALL")) c->chunk_fb_all = atoi(s) != 0;
   if (const char *s = getenv("GI_IND_FRAC")) c->ind_frac = std::min(1.0, std::max(1e-6, atof(s)));
+  if (const char *s = getenv("GI_IND_WAVES")) c->ind_waves = std::min(4, std::max(2, atoi(s)));
   if (const char *s = getenv("GI_KNN_KERNEL")) c->knn_kernel_kind = atoi(s);
   if (const char *s = getenv("GI_SORT_ALL")) c->sort_all = atoi(s) != 0;
   if (const char *s = getenv("GI_ROW_ORDER")) c->row_order = atoi(s) != 0;

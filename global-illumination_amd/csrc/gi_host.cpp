@@ -316,6 +316,10 @@ struct gi_ctx {
   DBuf kd_ph;                    // emission-ordered photons uploaded for the device build
   int wave_cap_mul = 1;
   int chunk_cap_big = 512;        // large-K chunk kernel: LDS candidates of the first pass
+  // large-K chunk kernel: the centre's dk bound refined to the exact d_K(c) (GI_CHUNK_DK_EXACT,
+  // default on: C4 shard caustic k-NN 154.7 -> 145.1 ms per launch, C2 / C3 frames -0.7 / -1.0 %;
+  // profiles/r05_dk_exact_ab.txt)
+  bool chunk_dk_exact = true;
   int chunk_minsub_big = 64;      // large-K chunk kernel: overflowing chunks retried down to this (64: none, measured best)
   int chunk_minsub = 32;          // chunk kernel: overflowing chunks retried as halves (measured best with the dk bound)
   double fb_ms[2] = {0, 0};       // final fallback kernel's time and queries per map (since the
@@ -977,6 +981,7 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
     k.fb_count = X.fb_count.as<uint32_t>();
     k.fb_cap_s = cap_s;
     k.chunk_minsub = c->chunk_minsub_big;
+    k.dk_exact = c->chunk_dk_exact ? 1 : 0;
     HIPCHK(c, hipEventRecord(X.ev0, X.st));
     if (!launch_knn_chunk_big(k, c->chunk_cap_big, X.st))
       return fail(c, GI_ERR_ARG, "k-NN launch: large-K chunk kernel unavailable");
@@ -1727,6 +1732,7 @@ int gi_create(gi_ctx **out, int dev) {
     c->prate[0] = c->prate[1] = std::max(0.0, atof(s));
   if (const char *s = getenv("GI_CHUNK_MINSUB_BIG")) c->chunk_minsub_big = std::min(64, std::max(1, atoi(s)));
   if (const char *s = getenv("GI_CHUNK_CAP_BIG")) c->chunk_cap_big = std::max(1, atoi(s));
+  if (const char *s = getenv("GI_CHUNK_DK_EXACT")) c->chunk_dk_exact = atoi(s) != 0;
   if (const char *s = getenv("GI_CHUNK_CAP_BIG2")) c->chunk_cap_big2 = atoi(s);
   if (const char *s = getenv("GI_CHUNK_CAP_BIG3")) c->chunk_cap_big3 = atoi(s);
   if (const char *s = getenv("GI_CHUNK_MINSUB")) c->chunk_minsub = std::min(64, std::max(1, atoi(s)));

@@ -288,6 +288,7 @@ struct KnnArgs {
   int32_t stat_off;        // 0 (global map) or ST_KNN_MAP (caustic map)
   int32_t sel_slack;       // query-per-wave kernel: re-select once K + slack candidates held
   int32_t chunk_minsub;    // chunk kernel: smallest query group an overflowing chunk is split to
+  int32_t dk_exact;        // large-K chunk kernel: refine the dk bound of the centre to the exact d_K(c)
   int32_t qpl;             // per-lane kernel: consecutive (sorted) queries per lane
   int32_t dbg;             // diagnostics: chunk kernel phase skips (timing only)
   int32_t general;         // 1: a query may need EstimateRadiance's general form (pow: specular

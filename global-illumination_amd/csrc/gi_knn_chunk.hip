@@ -348,6 +348,73 @@ __device__ __forceinline__ uint32_t walk_within(const float *nodes, int L, float
   return reads;
 }
 
+// the exact K-th distance from c (the chunk centre): every photon within RA2 (an upper bound of
+// d_K(c)^2) gathered into the LDS candidate arrays, then a wave select; false (dk2 untouched)
+// when they overflow the arrays or fewer than K lie within RA2
+template <int CAPC>
+__device__ __forceinline__ bool exact_dk2(const KnnArgs &a, int lane, float cx, float cy, float cz,
+                                          float RA2, const Cands<CAPC> &cpos, uint32_t *cidx,
+                                          uint32_t *hist, uint32_t *stk, ChunkProf &P,
+                                          float &dk2) {
+  constexpr int PER = (CAPC + 63) / 64;
+  const float4 *pos = reinterpret_cast<const float4 *>(a.map.pos4);
+  const int L = a.map.nleaves;
+  const int64_t N = a.map.n;
+  const int K = a.K;
+  // exact d_K(c): gather the photons within that radius of c and select the K-th
+  uint32_t na = 0;
+  bool ovf = false;
+  uint32_t rd = walk_within(a.map.nodes, L, RA2, stk,
+      [&](const KdNode &b) { return kd_box_d2(b.lo, b.hi, cx, cy, cz); },
+      [&](int lf) {
+        int64_t a0 = ((int64_t)lf * N) / L, a1 = ((int64_t)(lf + 1) * N) / L;
+        for (int64_t bb = a0; bb < a1; bb += 64) {
+          int64_t ii = bb + lane;
+          bool take = false;
+          float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (ii < a1) {
+            p = pos[ii];
+            take = metric(cx, cy, cz, p) <= RA2;
+          }
+          uint64_t m = __ballot(take);
+          uint32_t nn = (uint32_t)__popcll(m);
+          if (na + nn > (uint32_t)CAPC) { ovf = true; return true; }
+          if (take) {
+            uint32_t off = na + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            cpos.put(off, p);
+            cidx[off] = (uint32_t)ii;
+          }
+          na += nn;
+        }
+        return false;
+      });
+  if (P.on) P.c[5] += rd;
+  __syncthreads();
+  if (!ovf && na >= (uint32_t)K) {
+    uint64_t kc[PER];
+    float mn = INFINITY, mx = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < PER; u++) {
+      uint32_t s = (uint32_t)(u * 64 + lane);
+      kc[u] = ~0ull;
+      if (s < na) {
+        float dd = cpos.d2(cx, cy, cz, s);
+        kc[u] = ((uint64_t)__float_as_uint(dd) << 32) | (uint64_t)s;
+        mn = fminf(mn, dd);
+        mx = fmaxf(mx, dd);
+      }
+    }
+    if (na > (uint32_t)K) wave_select_k<PER>(kc, K, mn, mx, hist, cidx, lane);
+    float km = 0.0f;
+#pragma unroll
+    for (int u = 0; u < PER; u++)
+      if (kc[u] != ~0ull) km = fmaxf(km, __uint_as_float((uint32_t)(kc[u] >> 32)));
+    dk2 = wmaxf(km);
+  }
+  __syncthreads();
+  return !ovf && na >= (uint32_t)K;
+}
+
 template <int CAPC>
 __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, bool valid, float4 qp,
                                                    uint32_t cap, const Cands<CAPC> &cpos, uint32_t *cidx,
@@ -416,6 +483,17 @@ __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, b
       best = -wmax(-best);
       if (best < INFINITY) {
         G.dkc = best * (1.0 + 1e-6) + 1e-12;
+        // large-K chunk kernel (KnnArgs::dk_exact): the bound refined to the exact d_K(c) from
+        // the photons within it, so U = d_K(c) + rho as in the lane kernel (a tighter gather,
+        // fewer overflowing chunks); the dk bound stays when they overflow the LDS arrays
+        if (CAPC <= 512 && a.dk_exact && K <= (int)CAPC) {
+          float dk2 = 0.0f;
+          const float RA2 = __double2float_ru(G.dkc * G.dkc * (1.0 + 1e-5));
+          if (exact_dk2<CAPC>(a, lane, cx, cy, cz, RA2, cpos, cidx, hist, stk, P, dk2)) {
+            G.dkc = sqrt((double)dk2 * (1.0 + 1e-5));
+            G.dkc_exact = true;
+          }
+        }
         double ub = G.dkc + rho * (1.0 + 1e-6) + 1e-12;
         if (ub < U) U = ub;
       }
@@ -426,59 +504,10 @@ __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, b
       float dk2 = __shfl(sorted, K - 1, 64);  // >= d_K(c): K-th over a subset of photons
       // exact d_K(c): gather the photons within that radius of c and select the K-th
       float RA2 = __double2float_ru((double)dk2 * (1.0 + 1e-5));
-      uint32_t na = 0;
-      bool ovf = false;
-      uint32_t rd = walk_within(a.map.nodes, L, RA2, stk,
-          [&](const KdNode &b) { return kd_box_d2(b.lo, b.hi, cx, cy, cz); },
-          [&](int lf) {
-            int64_t a0 = ((int64_t)lf * N) / L, a1 = ((int64_t)(lf + 1) * N) / L;
-            for (int64_t bb = a0; bb < a1; bb += 64) {
-              int64_t ii = bb + lane;
-              bool take = false;
-              float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-              if (ii < a1) {
-                p = pos[ii];
-                take = metric(cx, cy, cz, p) <= RA2;
-              }
-              uint64_t m = __ballot(take);
-              uint32_t nn = (uint32_t)__popcll(m);
-              if (na + nn > (uint32_t)CAPC) { ovf = true; return true; }
-              if (take) {
-                uint32_t off = na + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                cpos.put(off, p);
-                cidx[off] = (uint32_t)ii;
-              }
-              na += nn;
-            }
-            return false;
-          });
-      if (P.on) P.c[5] += rd;
-      __syncthreads();
-      if (!ovf && na >= (uint32_t)K) {
-        uint64_t kc[PER];
-        float mn = INFINITY, mx = -INFINITY;
-#pragma unroll
-        for (int u = 0; u < PER; u++) {
-          uint32_t s = (uint32_t)(u * 64 + lane);
-          kc[u] = ~0ull;
-          if (s < na) {
-            float dd = cpos.d2(cx, cy, cz, s);
-            kc[u] = ((uint64_t)__float_as_uint(dd) << 32) | (uint64_t)s;
-            mn = fminf(mn, dd);
-            mx = fmaxf(mx, dd);
-          }
-        }
-        if (na > (uint32_t)K) wave_select_k<PER>(kc, K, mn, mx, hist, cidx, lane);
-        float km = 0.0f;
-#pragma unroll
-        for (int u = 0; u < PER; u++)
-          if (kc[u] != ~0ull) km = fmaxf(km, __uint_as_float((uint32_t)(kc[u] >> 32)));
-        dk2 = wmaxf(km);
-      }
-      __syncthreads();
+      const bool ex = exact_dk2<CAPC>(a, lane, cx, cy, cz, RA2, cpos, cidx, hist, stk, P, dk2);
       // metric -> true distance: 1e-5 relative margin covers the fp32 rounding
       G.dkc = sqrt((double)dk2 * (1.0 + 1e-5));
-      G.dkc_exact = !ovf && na >= (uint32_t)K;
+      G.dkc_exact = ex;
       double ub = G.dkc + rho * (1.0 + 1e-6) + 1e-12;
       if (ub < U) U = ub;
     }
@@ -1265,7 +1294,6 @@ void knn_chunk_big_kernel(KnnArgs a) {
   const Cands<CAPC> cpos{cbase};
   uint32_t *const cidx = reinterpret_cast<uint32_t *>(cbase + 4 * CAPC);
   uint32_t *const crgbe = cidx + CAPC;
-  __shared__ uint32_t hist[4];       // unused by the dk bound (chunk_bound_gather signature)
   __shared__ uint32_t stk[64];
   // kept-candidate bitmask [word][lane] during the collect and the estimate; during the counting
   // passes the lanes' LS_NBB 16-bit bin counters, two per word [w][lane]
@@ -1296,7 +1324,8 @@ void knn_chunk_big_kernel(KnnArgs a) {
     const bool act = valid && ((gm >> lane) & 1ull);
     if (P.on) P.t = clock64();
     ChunkGeom G;
-    chunk_bound_gather<CAPC>(a, lane, act, qp, CAPC, cpos, cidx, crgbe, hist, stk, G, P);
+    // selw (>= 256 words, idle until the counting passes) is the exact bound's select scratch
+    chunk_bound_gather<CAPC>(a, lane, act, qp, CAPC, cpos, cidx, crgbe, selw, stk, G, P);
     __syncthreads();
     if (G.overflow || G.dkc < 0.0) continue;
     pending &= ~gm;
@@ -1308,7 +1337,7 @@ void knn_chunk_big_kernel(KnnArgs a) {
     // bins from 0 unless GI_KNN_DBG & 64: dkc here is the dk upper bound, and the origin
     // (dkc - |q - c|)^2 from it can lie above the K-th key (measured 33.3 -> 32.1 ms/launch)
     float O = A;
-    if (a.dbg & 64) {
+    if (G.dkc_exact || (a.dbg & 64)) {
       double ex = (double)qx - G.cx, ey = (double)qy - G.cy, ez = (double)qz - G.cz;
       double lo = G.dkc - sqrt(ex * ex + ey * ey + ez * ez);
       if (lo > 0.0) {

@@ -351,6 +351,9 @@ __device__ __forceinline__ uint32_t walk_within(const float *nodes, int L, float
 // the exact K-th distance from c (the chunk centre): every photon within RA2 (an upper bound of
 // d_K(c)^2) gathered into the LDS candidate arrays, then a wave select; false (dk2 untouched)
 // when they overflow the arrays or fewer than K lie within RA2
+#ifndef DK_EXACT_MAXCAP
+#define DK_EXACT_MAXCAP 1024  // the large-K instances that refine the centre bound (KnnArgs::dk_exact)
+#endif
 template <int CAPC>
 __device__ __forceinline__ bool exact_dk2(const KnnArgs &a, int lane, float cx, float cy, float cz,
                                           float RA2, const Cands<CAPC> &cpos, uint32_t *cidx,
@@ -486,7 +489,7 @@ __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, b
         // large-K chunk kernel (KnnArgs::dk_exact): the bound refined to the exact d_K(c) from
         // the photons within it, so U = d_K(c) + rho as in the lane kernel (a tighter gather,
         // fewer overflowing chunks); the dk bound stays when they overflow the LDS arrays
-        if (CAPC <= 512 && a.dk_exact && K <= (int)CAPC) {
+        if (CAPC <= DK_EXACT_MAXCAP && a.dk_exact && K <= (int)CAPC) {
           float dk2 = 0.0f;
           const float RA2 = __double2float_ru(G.dkc * G.dkc * (1.0 + 1e-5));
           if (exact_dk2<CAPC>(a, lane, cx, cy, cz, RA2, cpos, cidx, hist, stk, P, dk2)) {

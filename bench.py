@@ -128,13 +128,26 @@ KNN_KINDS = {
 
 # CPU-baseline calibration: the restatement vs the reference binary on the
 # survey's C2 sample (cornell 64x64 aa=0, 1M + 1M photons, 8 threads) in the build container.
-# Round-5 measurement (tools/cpu_calibration.py -> profiles/r05_cpu_calibration.json): restatement
-# render 81.42 s (best of two), reference 72.62 s. ratio = restatement time /
-# reference time, inside BASELINE.md's 0.8-1.25 band; DESIGN.md section 7 explains the drift from
-# round 2's 52.70 s. reference_equivalent_value = value x ratio (the reference's rate).
-CPU_CALIBRATION = {"ratio": round(81.417 / 72.62, 3), "restatement_s": 81.417, "reference_s": 72.62,
+# NOT a same-session measurement: the reference's 72.62 s is the survey session's
+# (SURVEY.md section 6), and the reference cannot be rebuilt since (it needs GL/glu.h, DESIGN.md
+# section 6), while the restatement's 81.42 s is round 5's. The container's per-core speed moved
+# ~1.9x between those sessions (round 2's own restatement: 52.70 s then, ~100 s in round 5;
+# profiles/r05_cpu_calibration.json drift_check), so the ratio is only known within
+# [81.42 / (72.62 x 1.9), 81.42 / 72.62] = [0.59, 1.12]. No reference-equivalent rate is derived.
+CPU_CALIBRATION = {"same_session": False, "restatement_s": 81.417, "restatement_session": "r05",
+                   "reference_s": 72.62, "reference_session": "survey (SURVEY.md section 6)",
+                   "cross_session_ratio": round(81.417 / 72.62, 3),
+                   "container_drift": 1.9,
+                   "ratio_band": [round(81.417 / (72.62 * 1.9), 2), round(81.417 / 72.62, 2)],
+                   "status": "unpinned: no same-session reference timing is possible here",
                    "measured": "r05, profiles/r05_cpu_calibration.json",
                    "sample": "cornell 64x64 aa=0 1M+1M photons, 8 threads, build container"}
+
+# image_sha16 of the 1-GPU frame per workload (BENCH_r05 and the GPU suite's C2 hash): a run on N
+# GPUs must compose the same image (tiles dealt over the GPUs, the same RNG streams per sample)
+EXPECTED_SHA16 = {
+    ("cornell.scn", 1024, 2, 1000000, 1000000, 1, ""): "8b2810dafe63a3e9",
+}
 
 
 def load_traffic(a, qpl):
@@ -204,7 +217,6 @@ def cpu_baseline(a):
     samples = a.cpu_res * a.cpu_res * 4 ** a.aa * dof
     value = samples / st["render_s"] / 1e6
     full = a.res * a.res * 4 ** a.aa * dof
-    ratio = CPU_CALIBRATION["ratio"] if a.scene == "cornell.scn" else None
     return {"value": value, "unit": "Mpixel-samples/s",
             "cores": threads, "kind": "port", "cpu_model": cpu_model(),
             "host_cpus_visible": os.cpu_count(),
@@ -212,9 +224,7 @@ def cpu_baseline(a):
                       f"{a.global_photons}+{a.caustic_photons} photons; render {st['render_s']:.2f} s, "
                       f"photon map {st['trace_s'] + st['kd_s']:.2f} s on {threads} threads",
             "full_frame_s_extrapolated": round(full / (value * 1e6), 1),
-            "calibration_ratio": ratio,
-            "reference_equivalent_value": value * ratio if ratio else None,
-            "calibration": CPU_CALIBRATION if ratio else None}
+            "calibration": CPU_CALIBRATION if a.scene == "cornell.scn" else None}
 
 
 def device_list(n):
@@ -364,6 +374,20 @@ def main():
     value = samples_per_step * a.steps / elapsed / 1e6
     ms_per_step = elapsed / a.steps * 1000.0
 
+    # what ran where: every rank's HIP device and PCI bus, the RCCL
+    # communicator's rank count, so a multi-GPU line proves N distinct GPUs took part
+    info = r.device_info()
+    if dist is not None:
+        import torch
+        me = {"rank": rank, "local_rank": local, "device": info["devices"][0],
+              "pci_bus": info["pci_bus"][0], "hostname": os.uname().nodename}
+        allr = [None] * world
+        dist.all_gather_object(allr, me)
+        topo = {"mode": "torchrun", "backend": dist.get_backend(), "comm_count": dist.get_world_size(),
+                "ranks": allr, "distinct_pci_bus": len({(x["hostname"], x["pci_bus"]) for x in allr})}
+    else:
+        topo = dict(info, mode=mode, distinct_pci_bus=len(set(info["pci_bus"])))
+
     if rank == 0:
         # roofline of the dominant kernel: the global-map k-NN radiance estimate
         # (knn_chunk_kernel + per-lane fallback, K=50), HIP-event timed in-library on the
@@ -407,6 +431,12 @@ def main():
         if not a.no_cpu_baseline and n_gpus == 1:
             cpu = cpu_baseline(a)
         rgb = last.get("rgb")
+        sha = hashlib.sha256(rgb.tobytes()).hexdigest()[:16] if rgb is not None else None
+        want = EXPECTED_SHA16.get((a.scene, a.res, a.aa, a.global_photons, a.caustic_photons,
+                                   a.seed, a.extra.strip()))
+        check = None
+        if sha is not None and want is not None:
+            check = {"expected_1gpu": want, "equal": sha == want}
         par = {"single": "1 GPU",
                "device-set": f"one process, device set {devices}: tiles{a.tile}x{a.tile} % {n_gpus}, "
                              "ncclSend/ncclRecv tile gather onto device 0",
@@ -427,8 +457,9 @@ def main():
                        "photon_map_s": round(photon_s, 3),
                        "global_stored": pst["global_stored"],
                        "caustic_stored": pst["caustic_stored"]},
-            "image_sha16": (hashlib.sha256(rgb.tobytes()).hexdigest()[:16]
-                            if rgb is not None else None),
+            "image_sha16": sha,
+            "image_check": check,
+            "topology": topo,
             "roofline": roofline, "cpu_baseline": cpu,
             "step_ms": step_ms,
             # the first (cold) frame, what the drop-in CLI renders: first warmup step
@@ -451,6 +482,9 @@ def main():
     r.close()
     if dist is not None:
         dist.destroy_process_group()
+    if rank == 0 and check is not None and not check["equal"]:
+        raise SystemExit(f"image_sha16 {sha} differs from the 1-GPU frame's {want} "
+                         f"({n_gpus} GPUs, {mode})")
 
 
 if __name__ == "__main__":

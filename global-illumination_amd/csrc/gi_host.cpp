@@ -247,6 +247,8 @@ struct Rccl {
   ncclResult_t (*send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   const char *(*errString)(ncclResult_t) = nullptr;
+  ncclResult_t (*commCount)(const ncclComm_t, int *) = nullptr;
+  ncclResult_t (*commUserRank)(const ncclComm_t, int *) = nullptr;
   bool load() {
     static std::mutex mu;
     std::lock_guard<std::mutex> g(mu);
@@ -262,6 +264,8 @@ struct Rccl {
     send = (decltype(send))dlsym(h, "ncclSend");
     recv = (decltype(recv))dlsym(h, "ncclRecv");
     errString = (decltype(errString))dlsym(h, "ncclGetErrorString");
+    commCount = (decltype(commCount))dlsym(h, "ncclCommCount");
+    commUserRank = (decltype(commUserRank))dlsym(h, "ncclCommUserRank");
     ok = commInitAll && commDestroy && groupStart && groupEnd && send && recv && errString;
     return ok;
   }
@@ -1791,6 +1795,37 @@ int gi_create_devices(gi_ctx **out, const gi_device_set *set) {
   }
   hipSetDevice(c->device);
   *out = c;
+  return GI_OK;
+}
+
+int gi_device_info(const gi_ctx *c, int max, int *ndev, int *devices, int *pci_bus,
+                   int *comm_rank, int *comm_count) {
+  if (!c || !ndev || max < 0) return GI_ERR_ARG;
+  const int nd = 1 + (int)c->peers.size();
+  *ndev = nd;
+  for (int k = 0; k < nd && k < max; k++) {
+    const gi_ctx *d = k ? c->peers[k - 1] : c;
+    if (devices) devices[k] = d->device;
+    if (pci_bus) {
+      int bus = -1;
+      if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, d->device) != hipSuccess) bus = -1;
+      pci_bus[k] = bus;
+    }
+    if (comm_rank) {
+      int r = -1;
+      if (k < (int)c->comms.size() && c->comms[k] && g_rccl.commUserRank &&
+          g_rccl.commUserRank(c->comms[k], &r) != ncclSuccess)
+        r = -1;
+      comm_rank[k] = r;
+    }
+  }
+  if (comm_count) {
+    int n = 0;
+    if (!c->comms.empty() && c->comms[0] && g_rccl.commCount &&
+        g_rccl.commCount(c->comms[0], &n) != ncclSuccess)
+      n = 0;
+    *comm_count = n;
+  }
   return GI_OK;
 }
 

@@ -25,8 +25,8 @@ DISK, CONE, GAUSS = 0, 1, 2
 GLOBAL, CAUSTIC = 0, 1
 
 EXPORTED = [
-    "gi_params_default", "gi_parse_args", "gi_create", "gi_create_devices", "gi_destroy",
-    "gi_last_error",
+    "gi_params_default", "gi_parse_args", "gi_create", "gi_create_devices", "gi_device_info",
+    "gi_destroy", "gi_last_error",
     "gi_set_params", "gi_read_scene", "gi_scene_info", "gi_map_photons", "gi_set_photon_map",
     "gi_get_photon_map", "gi_get_kd_tree", "gi_set_progress", "gi_render_image", "gi_render_tiles",
     "gi_render_tiles_packed", "gi_compose_tiles", "gi_quantize",
@@ -122,6 +122,8 @@ def lib():
                                     P(C.c_int), P(C.c_char_p)]
         L.gi_create.argtypes = [P(C.c_void_p), C.c_int]
         L.gi_create_devices.argtypes = [P(C.c_void_p), P(DeviceSet)]
+        L.gi_device_info.argtypes = [C.c_void_p, C.c_int, P(C.c_int), C.c_void_p, C.c_void_p,
+                                     C.c_void_p, P(C.c_int)]
         L.gi_destroy.argtypes = [C.c_void_p]
         L.gi_destroy.restype = None
         L.gi_last_error.argtypes = [C.c_void_p]
@@ -210,6 +212,18 @@ class Renderer:
                 raise GiError(f"gi_create failed (rc={rc}): no usable HIP device {device}")
         self.params = params if params is not None else default_params()
         self._check(lib().gi_set_params(self._ctx, C.byref(self.params)))
+
+    def device_info(self):
+        """What the context drives (gi_device_info): HIP ordinals, PCI bus ids, RCCL user rank
+        per device, and the RCCL communicator's rank count (0 without RCCL)."""
+        n = C.c_int(0)
+        self._check(lib().gi_device_info(self._ctx, 0, C.byref(n), None, None, None, None))
+        k = n.value
+        dev, bus, rk = (C.c_int * k)(), (C.c_int * k)(), (C.c_int * k)()
+        cc = C.c_int(0)
+        self._check(lib().gi_device_info(self._ctx, k, C.byref(n), dev, bus, rk, C.byref(cc)))
+        return {"devices": list(dev), "pci_bus": list(bus), "comm_rank": list(rk),
+                "comm_count": cc.value}
 
     def release_scratch(self):
         """Free the device scratch of renders and map builds; scene and maps stay resident."""

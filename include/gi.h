@@ -181,6 +181,14 @@ typedef struct gi_device_set {
   int32_t devices[GI_MAX_DEVICES];
 } gi_device_set;
 int gi_create_devices(gi_ctx **out, const gi_device_set *set);
+/* What a context really drives, so that a multi-GPU run can prove it (no reference
+ * counterpart: the reference's threads share one host). *ndev = the context's device count;
+ * for each (up to max): devices[k] = its HIP ordinal, pci_bus[k] = that device's PCI bus id
+ * (hipDeviceAttributePciBusId; -1 if unknown), comm_rank[k] = ncclCommUserRank of its RCCL
+ * communicator (-1 without one). *comm_count = ncclCommCount of the first communicator (0 when
+ * the set gathers without RCCL: one device, or entries naming the same device). */
+int gi_device_info(const gi_ctx *ctx, int max, int *ndev, int *devices, int *pci_bus,
+                   int *comm_rank, int *comm_count);
 void gi_destroy(gi_ctx *ctx);
 const char *gi_last_error(const gi_ctx *ctx);
 int gi_set_params(gi_ctx *ctx, const gi_params *p);

@@ -16,8 +16,28 @@
 //     would be; host-side setup (light power, camera, direction LUT) keeps the C library.
 #include "oracle_scene.h"
 #include "../include/gi.h"
+#ifdef ORACLE_LIBM
+// Independent-math build (liboracle_libm.so): the C library's
+// transcendentals, as the reference calls them (graphics_utils.cpp:95-216, photon_utils.cpp:56-60),
+// instead of the sequences shared with the device, so that a defect of gi_math.h cannot hide
+// behind both sides agreeing (tests/test_cpu_oracle_libm.py).
+#include <cmath>
+namespace gm_libm {
+inline double sin(double x) { return std::sin(x); }
+inline double cos(double x) { return std::cos(x); }
+inline double tan(double x) { return std::tan(x); }
+inline double asin(double x) { return std::asin(x); }
+inline double acos(double x) { return std::acos(x); }
+inline double atan2(double y, double x) { return std::atan2(y, x); }
+inline double pow(double x, double y) { return std::pow(x, y); }
+inline double pow2(double x) { return std::pow(x, 2.0); }
+inline double pow5(double x) { return std::pow(x, 5.0); }
+}  // namespace gm_libm
+namespace gm = gm_libm;
+#else
 // the fp64 transcendentals the device evaluates (shared operation sequence: same bits as the GPU)
 #include "../global-illumination_amd/csrc/gi_math.h"
+#endif
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -40,6 +60,24 @@ namespace oracle {
 // emission direction's cosine to the light normal does, 300 + c the path class c (photon_trace).
 static bool g_tagging = false;
 static int g_tag_select = -100;   // -100: every photon
+// Diagnostic only (oracle_set_diag): the Monte Carlo contributions of a render
+// split by path class. A path of a primary hit's bounce fan (bounce_illumination) has fan
+// t_fan (0 transmissive, 1 the Fresnel-reflected fan of a transparent surface, 2 another
+// specular fan) and event bits t_evt (1: it took a Fresnel reflection at a transparent surface,
+// 2: a total internal reflection), and every contribution it adds has class
+// 4 * t_fan + t_evt (+ 16 when the hit surface is emissive); the primary hit's own terms are
+// class 63. With g_mc_class = c >= 0 only class-c contributions are added, so the classes of
+// one seed add up to the full render (before clamping and quantisation). g_diag_win limits the
+// render to a window of output pixels [x0, x1) x [y0, y1) (row 0 = bottom); the rest is black.
+static int g_mc_class = -1;
+static int g_diag_win[4] = {0, 0, 0, 0};
+// g_diag_flags bit 0: no Fresnel split inside MonteCarlo_PathTrace (R = 0 there; the primary
+// hit's split in RayTrace stays) -- a hypothesis test for fig_12, never a default
+static int g_diag_flags = 0;
+static thread_local int t_fan = 0, t_evt = 0;
+static inline bool mc_keep(bool emissive) {
+  return g_mc_class < 0 || g_mc_class == 4 * t_fan + t_evt + (emissive ? 16 : 0);
+}
 
 // ---------------------------------------------------------------------------------------
 // Per-thread counters (render.cpp:26-41)
@@ -268,7 +306,8 @@ static V3 reflective_bounce(V3 normal, V3 view, double cos_theta) {
   return normalize(r);
 }
 // TransmissiveBounce, :121-154
-static V3 transmissive_bounce(double ir_air, V3 normal, V3 view, double cos_theta, double ir_mat) {
+static V3 transmissive_bounce(double ir_air, V3 normal, V3 view, double cos_theta, double ir_mat,
+                              bool *tir = nullptr) {
   double eta;
   if (cos_theta < 0) {
     eta = ir_mat / ir_air;
@@ -279,7 +318,10 @@ static V3 transmissive_bounce(double ir_air, V3 normal, V3 view, double cos_thet
   }
   double theta = gm::acos(cos_theta);
   double sin_phi = eta * gm::sin(theta);
-  if (sin_phi < -1.0 || 1.0 < sin_phi) return reflective_bounce(normal, view, cos_theta);
+  if (sin_phi < -1.0 || 1.0 < sin_phi) {
+    if (tir) *tir = true;
+    return reflective_bounce(normal, view, cos_theta);
+  }
   double phi = gm::asin(sin_phi);
   V3 par = normalize(view + normal * cos_theta);
   V3 refr = par * gm::tan(phi) - normal;
@@ -846,9 +888,11 @@ static void mc_path_trace(const Ctx &c, V3 org, V3 dir, Rgb &color, Rng &rng, Co
         direct_illumination(c, h.point, h.normal, ray_start, cb, brdf, cos_theta, true, rng, cnt);
       if (P.caustic_illum && brdf.isDiffuse())
         caustic_illumination(c, h.point, h.normal, cb, brdf, view, cos_theta, cnt);
-      color += cb * tw;
+      const bool emis = max_channel(brdf.e) > 0;
+      if (mc_keep(emis)) color += cb * tw;
       double R = 0;
-      if (P.specular_illum && P.transmissive_illum && P.fresnel && brdf.isTransparent())
+      if (P.specular_illum && P.transmissive_illum && P.fresnel && brdf.isTransparent() &&
+          !(g_diag_flags & 1))
         R = reflection_coeff(P.ir_air, cos_theta, brdf.ir);
       double pd = max_channel(brdf.kd);
       double pt = max_channel(brdf.kt);
@@ -863,21 +907,24 @@ static void mc_path_trace(const Ctx &c, V3 org, V3 dir, Rgb &color, Rng &rng, Co
         if (P.indirect_illum) {
           cb = Rgb();
           indirect_illumination(c, h.point, h.normal, cb, brdf, cos_theta, true, &rng, 0, cnt);
-          color += cb * brdf.kd * tw / pd;
+          if (mc_keep(emis)) color += cb * brdf.kd * tw / pd;
         } else if (P.fast_global) {
           cb = Rgb();
           estimate_global_illumination(c, h.point, h.normal, cb, brdf, view, cos_theta, cnt);
-          color += cb * brdf.kd * tw / pd;
+          if (mc_keep(emis)) color += cb * brdf.kd * tw / pd;
         }
         break;
       } else if (rnd < pd + pt) {
         if (!P.transmissive_illum) break;
-        V3 ex = transmissive_bounce(P.ir_air, h.normal, view, cos_theta, brdf.ir);
+        bool tir = false;
+        V3 ex = transmissive_bounce(P.ir_air, h.normal, view, cos_theta, brdf.ir, &tir);
+        if (tir) t_evt |= 2;
         sb = P.distrib_transmissive ? specular_sample(ex, brdf.n, cos_theta, rng) : ex;
         cnt.trans++;
         tw *= (1.0 - R) * brdf.kt / pt;
       } else if (rnd < pd + pt + ps) {
         if (!P.specular_illum) break;
+        if (brdf.isTransparent() && R > 0) t_evt |= 1;
         V3 ex = reflective_bounce(h.normal, view, cos_theta);
         sb = P.distrib_specular ? specular_sample(ex, brdf.n, cos_theta, rng) : ex;
         cnt.spec++;
@@ -889,7 +936,7 @@ static void mc_path_trace(const Ctx &c, V3 org, V3 dir, Rgb &color, Rng &rng, Co
       org = ray_start;
       dir = sb;
     } else {
-      color += tw * c.scene.background;
+      if (mc_keep(false)) color += tw * c.scene.background;
       break;
     }
   }
@@ -980,6 +1027,8 @@ static void bounce_illumination(const Ctx &c, bool trans, V3 p, V3 normal, Rgb &
   for (int i = 0; i < n; i++) {
     Rng rng(P.seed, trans ? KIND_TRANS : KIND_SPEC, psample, i);
     V3 sb = distrib ? specular_sample(exact, brdf.n, cos_theta, rng) : exact;
+    t_fan = trans ? 0 : (brdf.isTransparent() && coeff > 0 ? 1 : 2);
+    t_evt = 0;
     mc_path_trace(c, p + sb * EPS, sb, buf, rng, cnt);
     if (trans) cnt.trans++; else cnt.spec++;
   }
@@ -999,6 +1048,10 @@ static void ray_trace(const Ctx &c, const Hit &h, V3 eye, Rgb &color, Rng &rng,
   if (P.ambient && brdf.isAmbient()) color += brdf.ka;
   if (P.direct_illum && (brdf.isDiffuse() || brdf.isSpecular()))
     direct_illumination(c, point, normal, eye, color, brdf, cos_theta, false, rng, cnt);
+  if (g_mc_class >= 0) {  // diagnostic class split (oracle_set_diag): 63 = the primary's terms
+    if (g_mc_class == 63) return;
+    color = Rgb();
+  }
   if (P.transmissive_illum && brdf.isTransparent()) {
     if (P.specular_illum && P.fresnel) R = reflection_coeff(P.ir_air, cos_theta, brdf.ir);
     if (R < 1.0)
@@ -1333,6 +1386,9 @@ static void render_image(const Ctx &c, int aa, int width, int height, Image &img
     for (int i = 0; i < W; i++) {
       if (i % T != id) continue;  // column interleave, render.cpp:90
       for (int j = 0; j < H; j++) {
+        if (g_diag_win[2] > 0 && (i / af < g_diag_win[0] || i / af >= g_diag_win[2] ||
+                                  j / af < g_diag_win[1] || j / af >= g_diag_win[3]))
+          continue;  // diagnostic window (oracle_set_diag): buf stays black
         Rgb acc;
         double dx = (double)(2 * (i - xc)) / (double)W;
         double dy = (double)(2 * (j - yc)) / (double)H;
@@ -1632,6 +1688,18 @@ int oracle_run_tags(int argc, char **argv, const int *tags, int ntags, float *rg
   }
   g_tag_select = -100;
   delete c;
+  return 0;
+}
+
+// Diagnostic switches (never used by a parity test): the Monte Carlo path class
+// kept in renders (-1 = all) and an output-pixel window (x1 <= 0 = the whole image).
+int oracle_set_diag_flags(int flags) {
+  g_diag_flags = flags;
+  return 0;
+}
+int oracle_set_diag(int mc_class, int x0, int y0, int x1, int y1) {
+  g_mc_class = mc_class;
+  g_diag_win[0] = x0; g_diag_win[1] = y0; g_diag_win[2] = x1; g_diag_win[3] = y1;
   return 0;
 }
 

@@ -18,20 +18,40 @@ tools/mc_figs_fit.py, profiles/r05_mc_figs_explore.txt):
       specular (the default) the same statistic fails (z_frac 0.61): `specular+ds`, the
       evidence row, must miss.
   fig_12a / fig_12b  README.md:242-246, "Fresnel Off / Fresnel On": input/jensen.scn's glass and
-      mirror spheres (ir 1.5, n 1000) under the rect light, 512^2, no photon layers. The
+      mirror spheres (ir 1.5, n 1000) under the rect light, 512^2, aa 1, no photon layers. The
       figures come from a revision of the scene or lighting that is not shipped: their walls
       differ from the current code's by a spatial pattern (0.89-1.09 by surface, the same in
       fig_9b and fig_14), so their levels cannot be pinned. Their DIFFERENCE isolates the
       renderer's Fresnel split (raytracer.cpp:174-233 passes R to Transmissive / Specular
-      Illumination): over the glass sphere's 8 x 8 blocks it correlates 0.98 with the
-      restatement's (fresnel on - off), the mirror sphere and the walls do not change in either.
-      Its magnitude is 0.36 of ours: the caption names the cause ("the front of the Cornell Box
-      is very softly reflected on the front of the glass sphere"), a front wall that
-      jensen.scn does not have (its box is open towards the camera, so our Fresnel reflection on
-      the sphere's front shows the black background). Pinned: the pattern, not the magnitude.
-  Not pinnable (measured, profiles/r05_mc_figs_explore.txt): fig_14a-c (Monte Carlo noise at
-      8 / 32 / 128 samples; same scene revision as fig_12: the mirror's noise matches aa 1 within
-      3 %, the glass's is 1.9x ours at every sample count), fig_9b (same revision), fig_15 (its
+      Illumination). r05 pinned its pattern only (correlation 0.98) because its magnitude was
+      0.36 of ours. r06 found why (tools/glass_decompose.py): splitting our
+      (on - off) change by path class and fitting the figure's change gives weight 1.00 to the
+      primary hit's Fresnel-reflected fan and 0.60 to the transmitted light's loss, and the paths
+      that took a Fresnel reflection inside MonteCarlo_PathTrace (montecarlo.cpp:87-91, 139-155)
+      weight 0.09 -- the figures were rendered by a revision whose path tracer did not split at
+      transparent surfaces. With the restatement's split at the primary hit only (the oracle's
+      diagnostic flag), the figure's change is reproduced in magnitude and pattern: block
+      scale 1.01, correlation 0.995, residual 1 % of the figure's (fresnel_magnitude). That pins
+      Schlick's R at the primary hit (graphics_utils.cpp:95-101), the (1 - R) transmissive
+      weight and the Fresnel-reflected fan with its ceil((ST R + ST) / 2) samples. Evidence row
+      (`fig_12 + mc fresnel`): the shipped code's change misses the same criterion (scale 0.76,
+      correlation 0.975, residual 10 %).
+  fig_14a / 14b / 14c  README.md:255-259, Monte Carlo noise at 8 / 32 / 128 samples (-tt = -st),
+      jensen.scn, aa 1, Fresnel on, distributed transmission and specular on (the defaults). The
+      three figures are independent draws of one image, so the per-pixel noise variance of
+      each is solved from their three pairwise differences (no reference draw needed): glass
+      26.9 / 6.69 / 1.80, mirror (pixels whose reflection hits a wall) 23.8 / 5.95 / 2.24 -- both
+      fall as 1/N. Absolute noise is not pinnable: both spheres are ~2.2x ours and the walls'
+      direct-light noise 0.56x ours, the light revision again (r05's high-pass measure said the
+      mirror matched within 3 %, but that measure was dominated by the reflected image's detail,
+      not noise). The glass-to-mirror ratio cancels the in-path light estimator both spheres'
+      paths end in, and pins TransmissiveIllumination's fan and path statistics against
+      SpecularIllumination's with the default Phong-lobe sampling (graphics_utils.cpp:189-216):
+      figure 1.13 / 1.12 at 8 / 32 against the restatement's 0.97 / 1.00 (noise_pin), and the 1/N
+      fall within 15 % for both. Evidence row: without the split inside the paths (fig_12's
+      revision) the ratio is 0.47 / 0.49 and misses -- fig_14 was rendered with it, like the
+      shipped montecarlo.cpp.
+  Not pinnable (measured, profiles/r05_mc_figs_explore.txt): fig_9b (same revision), fig_15 (its
       scene -- glass cube, gloss sphere -- is not shipped), fig_11a-e (screenshots of the
       OpenGL ray viewer, not renders), gallery/tests/fourspheres.png (level 0.35 of the shipped
       scene's: an older file).
@@ -139,4 +159,120 @@ def fresnel_delta_pin(on_imgs, off_imgs, intersect):
     out["ok"] = (corr >= FRESNEL_CORR and np.sign(a.mean()) == np.sign(b.mean())
                  and max(abs(out["fig_delta_mirror"]), abs(out["our_delta_mirror"]),
                          abs(out["fig_delta_other"]), abs(out["our_delta_other"])) <= 0.25)
+    return out
+
+
+# ---- fig_12's magnitude (r06): the split at the primary hit only ------------------------------
+FRESNEL_MAG_CFG = ("jensen.scn", 512, 1, _NOPM + ["-no_dt", "-no_ds"])
+FRESNEL_MAG = {"scale_tol": 0.10, "corr": 0.99, "resid": 0.03}
+
+
+def fresnel_mag_args(on, seed, threads=None):
+    sc, res, aa, flags = FRESNEL_MAG_CFG
+    args = [os.path.join(SCN, sc), "/tmp/mf.png", "-resolution", str(res), str(res), "-aa",
+            str(aa), "-seed", str(seed)] + flags
+    if not on:
+        args.append("-no_fresnel")
+    if threads:
+        args += ["-threads", str(threads)]
+    return args, res, res
+
+
+def fresnel_magnitude(on_gray, off_gray, intersect):
+    """fig_12b - fig_12a against the mean over seeds of (on - off) renders (top-down gray images,
+    8-bit units) over the glass sphere's 8 x 8 blocks: the least-squares scale of ours onto the
+    figure's, the correlation, and the residual as a fraction of the figure's sum of squares.
+    ok = scale within 10 % of 1, correlation >= 0.99, residual <= 3 %."""
+    glass, _mirror, _other = sphere_blocks(intersect)
+    fd = blocks(figure(FRESNEL[1]), FRESNEL_B) - blocks(figure(FRESNEL[0]), FRESNEL_B)
+    od = np.mean([blocks(np.repeat(a[..., None], 3, -1), FRESNEL_B) -
+                  blocks(np.repeat(b[..., None], 3, -1), FRESNEL_B)
+                  for a, b in zip(on_gray, off_gray)], 0)
+    a, b = fd[glass].ravel(), od[glass].ravel()
+    scale = float((a * b).sum() / (b * b).sum())
+    out = {"scale": scale, "corr": float(np.corrcoef(a, b)[0, 1]),
+           "resid_frac": float(((a - scale * b) ** 2).sum() / (a * a).sum()),
+           "fig_mean": float(a.mean()), "our_mean": float(b.mean()), "glass_blocks": int(glass.sum())}
+    out["ok"] = (abs(scale - 1) <= FRESNEL_MAG["scale_tol"] and out["corr"] >= FRESNEL_MAG["corr"]
+                 and out["resid_frac"] <= FRESNEL_MAG["resid"])
+    return out
+
+
+# ---- fig_14's Monte Carlo noise (r06): glass-to-mirror ratio and the 1/N fall ------------------
+NOISE_FIGS = ("fig_14a", "fig_14b", "fig_14c")
+NOISE_N = (8, 32, 128)
+NOISE_CFG = ("jensen.scn", 512, 1, _NOPM)
+NOISE_SEEDS = (1, 2)
+NOISE_RATIO_TOL = (0.8, 1.25)   # figure ratio / our ratio
+NOISE_FALL = (3.4, 4.6)         # v(8) / v(32), 4 for a 1/N fall
+
+
+def noise_args(n, seed, threads=None):
+    sc, res, aa, flags = NOISE_CFG
+    args = [os.path.join(SCN, sc), "/tmp/mf.png", "-resolution", str(res), str(res), "-aa",
+            str(aa), "-seed", str(seed), "-tt", str(n), "-st", str(n)] + flags
+    if threads:
+        args += ["-threads", str(threads)]
+    return args, res, res
+
+
+def noise_masks(intersect):
+    """Top-down pixel masks of jensen.scn at 512^2: the glass sphere's interior ("glass") and the
+    mirror sphere's pixels whose reflected primary ray hits a wall ("mirror"), both away from
+    edges and from saturated or dark pixels of fig_14c (where clamping and truncation, not
+    noise, would dominate a difference)."""
+    from scipy.ndimage import binary_erosion, maximum_filter, minimum_filter
+    sc, res, _aa, _f = NOISE_CFG
+    path = os.path.join(SCN, sc)
+    o, d = pf.camera_rays(path, res, res)
+    hit, _t, p, n, m = intersect(path, o, d)
+    r = d - 2 * (d * n).sum(1, keepdims=True) * n
+    h2, _t2, _p2, _n2, m2 = intersect(path, p + r * 1e-6, r)
+    mat = np.where(hit > 0, m, -9).reshape(res, res)[::-1]
+    sec = np.where(h2 > 0, m2, -9).reshape(res, res)[::-1]
+    ref = figure(NOISE_FIGS[2]).astype(float).mean(-1)
+    smooth = (maximum_filter(ref, 7) - minimum_filter(ref, 7) < 40) & (ref > 8) & (ref < 230)
+    wall = np.isin(sec, [0, 1, 2])
+    return {"glass": binary_erosion(mat == 3, iterations=4) & smooth,
+            "mirror": binary_erosion(mat == 4, iterations=3) & wall & binary_erosion(wall, iterations=2)}
+
+
+def window(mask):
+    """Output-pixel window (x0, y0, x1, y1; row 0 = bottom) around a top-down mask."""
+    ys, xs = np.nonzero(mask[::-1])
+    return (int(xs.min()), int(ys.min()), int(xs.max()) + 1, int(ys.max()) + 1)
+
+
+def figure_noise(masks):
+    """Per-pixel noise variance (8-bit gray) of each fig_14 figure per region, from the three
+    independent figures' pairwise difference variances: v_a + v_b = var(a - b)."""
+    out = {}
+    for k, mk in masks.items():
+        a, b, c = (figure(f).astype(float).mean(-1)[mk] for f in NOISE_FIGS)
+        ab, ac, bc = (a - b).var(), (a - c).var(), (b - c).var()
+        out[k] = {8: (ab + ac - bc) / 2, 32: (ab + bc - ac) / 2, 128: (ac + bc - ab) / 2}
+    return out
+
+
+def render_noise(pairs, masks):
+    """Per-pixel noise variance of our renders: pairs[region][n] = (seed-1 image, seed-2 image),
+    top-down gray 8-bit; v = var(a - b) / 2 over the region."""
+    return {k: {n: float((a - b)[masks[k]].var() / 2) for n, (a, b) in d.items()}
+            for k, d in pairs.items()}
+
+
+def noise_pin(fig_v, our_v):
+    """ok = at 8 and 32 samples the figure's glass-to-mirror noise ratio is within NOISE_RATIO_TOL
+    of ours, and v(8) / v(32) lies in NOISE_FALL for both regions of both."""
+    out = {"fig": fig_v, "ours": our_v}
+    rel = []
+    for n in (8, 32):
+        rf = fig_v["glass"][n] / fig_v["mirror"][n]
+        ro = our_v["glass"][n] / our_v["mirror"][n]
+        out[f"ratio_fig_{n}"], out[f"ratio_ours_{n}"] = rf, ro
+        rel.append(rf / ro)
+    falls = [v[8] / v[32] for d in (fig_v, our_v) for v in d.values()]
+    out["rel"], out["falls"] = rel, falls
+    out["ok"] = (all(NOISE_RATIO_TOL[0] <= x <= NOISE_RATIO_TOL[1] for x in rel)
+                 and all(NOISE_FALL[0] <= f <= NOISE_FALL[1] for f in falls))
     return out

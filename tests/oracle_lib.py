@@ -152,3 +152,31 @@ def math(fn, x, y=None):
     rc = lib().oracle_math(MATH_FNS[fn], len(x), x.ctypes.data, y.ctypes.data, out.ctypes.data)
     assert rc == 0
     return out
+
+
+def set_diag(mc_class=-1, window=None, flags=0):
+    """Diagnostic switches of the restatement (oracle_set_diag / oracle_set_diag_flags; DESIGN.md
+    6.2): keep only Monte Carlo contributions of one path class (-1 = all), render only the
+    output-pixel window (x0, y0, x1, y1; row 0 = bottom; None = whole image), flags bit 0 = no
+    Fresnel split inside MonteCarlo_PathTrace. Hypothesis tests only: every parity test runs
+    with the defaults, which are restored by set_diag()."""
+    L = lib()
+    L.oracle_set_diag.argtypes = [C.c_int] * 5
+    L.oracle_set_diag_flags.argtypes = [C.c_int]
+    L.oracle_set_diag(mc_class, *(window or (0, 0, 0, 0)))
+    L.oracle_set_diag_flags(flags)
+
+
+def render_float(args, width, height):
+    """One render (no photon map unless the flags need one) returning the box-filtered clamped
+    float image [H, W, 3] (row 0 = bottom) and the 8-bit one."""
+    L = lib()
+    L.oracle_run_tags.argtypes = [C.c_int, C.POINTER(C.c_char_p), C.c_void_p, C.c_int,
+                                  C.c_void_p, C.c_void_p, C.c_int64]
+    n, argv = _argv(args)
+    tags = (C.c_int * 1)(-100)
+    f = np.zeros((height, width, 3), np.float32)
+    rgb = np.zeros((height, width, 3), np.uint8)
+    rc = L.oracle_run_tags(n, argv, tags, 1, f.ctypes.data, rgb.ctypes.data, width * height)
+    assert rc == 0, rc
+    return f, rgb

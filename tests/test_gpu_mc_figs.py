@@ -6,8 +6,10 @@ renders the Monte Carlo figure configurations through the C ABI.
   seed 1 as closely as two draws agree; with distributed specular it must miss.
 - fig_12a / fig_12b (Fresnel off / on, jensen.scn): the figures' difference correlates with the
   device's (fresnel on - off) over the glass sphere (>= 0.95), same sign, and neither changes
-  the mirror sphere or the walls (mc_figs.fresnel_delta_pin; the magnitude is not pinned, see
-  mc_figs' docstring)."""
+  the mirror sphere or the walls (mc_figs.fresnel_delta_pin); its magnitude needs the split at
+  the primary hit only (the figures' revision, test_cpu_mc_figs), so the device's shipped-code
+  change must miss mc_figs.fresnel_magnitude.
+- fig_14a-c: the glass-to-mirror noise ratio and its 1/N fall (mc_figs.noise_pin)."""
 import json
 import os
 
@@ -61,3 +63,35 @@ def test_device_fresnel_split_pattern(renderer):
     r = mf.fresnel_delta_pin(on, off, oracle_lib.intersect)
     _log(r, "fig_12b-fig_12a")
     assert r["ok"], r
+
+
+def _dev_gray(renderer, args):
+    rgb, _st, _ps = run_gpu(renderer, args)
+    return rgb[::-1].astype(float).mean(-1)
+
+
+def test_device_fig_14_glass_to_mirror_noise(renderer):
+    """fig_14a-c noise pin (mc_figs.noise_pin) on the device's full-frame renders: glass-to-mirror
+    per-pixel noise ratio within NOISE_RATIO_TOL of the figures' at 8 and 32 samples, 1/N fall."""
+    masks = mf.noise_masks(oracle_lib.intersect)
+    pairs = {k: {} for k in masks}
+    for n in (8, 32):
+        imgs = [_dev_gray(renderer, mf.noise_args(n, s)[0]) for s in mf.NOISE_SEEDS]
+        for k in masks:
+            pairs[k][n] = tuple(imgs)
+    r = mf.noise_pin(mf.figure_noise(masks), mf.render_noise(pairs, masks))
+    _log(r, "fig_14 noise")
+    assert r["ok"], r
+
+
+def test_device_fig_12_magnitude_needs_the_primary_split(renderer):
+    """The device renders the shipped code (the split inside the paths too): the fig_12 pattern
+    holds (test_device_fresnel_split_pattern) but the magnitude pin misses, as the restatement's
+    does (test_cpu_mc_figs: only the primary-hit split reproduces the figures)."""
+    on, off = [], []
+    for s in mf.FRESNEL_SEEDS:
+        on.append(_dev_gray(renderer, mf.fresnel_mag_args(True, s)[0]))
+        off.append(_dev_gray(renderer, mf.fresnel_mag_args(False, s)[0]))
+    r = mf.fresnel_magnitude(on, off, oracle_lib.intersect)
+    _log(r, "fig_12 + mc fresnel")
+    assert not r["ok"] and r["scale"] < 0.85 and r["resid_frac"] > 0.05, r

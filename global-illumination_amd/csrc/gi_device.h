@@ -655,12 +655,6 @@ __device__ __forceinline__ bool scene_intersect(const SceneView &S, V org, V dir
                                                 int hint = -1) {
   return scene_intersect_b<KINDS>(S, org, dir, h, kInf, -1.0, hint) == 1;
 }
-// the same walk out of line (register footprint of the path kernels' loops)
-template <uint32_t KINDS = KINDS_ALL>
-__device__ __noinline__ bool scene_intersect_ool(const SceneView &S, V org, V dir, Hit &h,
-                                                 int hint) {
-  return scene_intersect_b<KINDS>(S, org, dir, h, kInf, -1.0, hint) == 1;
-}
 
 // ---------------------------------------------------------------------------------------
 // Optics and sampling (utils/graphics_utils.cpp)
@@ -1071,9 +1065,8 @@ __device__ __noinline__ void direct_illumination(const SceneView &S, const Flags
 // hard_lights), inlined: no light sampling, so no calls, and the caller's registers are not
 // spilled around them. Same operations as direct_illumination -> compute_illumination ->
 // illum_test / light_reflection for those light kinds (TestLightIntersection is 0 for them).
-#ifndef HARD_ILLUM_OOL
-#define HARD_ILLUM_OOL 0  // measured r05: C4 shard 0/8 5,862 -> 6,271 ms with it on (spills 48 -> 20)
-#endif
+// (r05: the shadow walk out of line where the scene has boxes or meshes cut mc_kernel's spills
+// 48 -> 20 VGPRs but ran slower, C4 shard 0/8 5,862 -> 6,271 ms; removed)
 template <uint32_t KINDS = KINDS_ALL>
 __device__ __forceinline__ void direct_illumination_hard(const SceneView &S, const Flags &F, V p,
                                                          V nrm, V eye, C3 &color,
@@ -1089,13 +1082,7 @@ __device__ __forceinline__ void direct_illumination_hard(const SceneView &S, con
     V pol = (L.kind == LK_DIR) ? p - ld3(L.dir) * S.radius * 3.0 : ld3(L.pos);
     double side = dot(nrm, pol - p);
     if ((side > 0 && ct < 0) || (side < 0 && ct > 0)) continue;
-    // HARD_ILLUM_OOL: the shadow ray's scene walk out of line where the scene has boxes or
-    // meshes (mc_kernel<boxes|meshes, hard lights>: 48 -> 20 spilled VGPRs), measured slower
-    // than the spills it removes (C4 shard 0/8 +7 %), so off
-    bool lit;
-    if constexpr (HARD_ILLUM_OOL && (KINDS & ~KINDS_TRI_SPHERE) != 0) lit = illum_test<KINDS>(S, p, pol, cnt);
-    else lit = illum_test_inl<KINDS>(S, p, pol, cnt);
-    if (lit && L.active)
+    if (illum_test_inl<KINDS>(S, p, pol, cnt) && L.active)
       color += light_reflection_hard(L, m, eye, p, nrm);
   }
   color += ldc(m.e);

@@ -34,13 +34,22 @@ namespace {
 // Device buffer that only grows. A growth re-allocates with 1.5x headroom: hipMalloc of tens of
 // GB takes seconds on MI355X, and a frame whose batches grow a little at a time (C5's first
 // render: query lists 365 M -> 431 M -> 449 M) would otherwise pay that at every step
-// (GI_BATCH_LOG showed 3.9 s and 3.2 s batches; C5 shard 1/8 cold 64.0 s vs 16.5 s warm).
-// GI_ALLOC_LOG=1: one stderr line per device allocation of >= 64 MiB (size, time; first-frame
-// diagnostics)
-static bool alloc_log() {
-  static const bool on = [] { const char *s = getenv("GI_ALLOC_LOG"); return s && atoi(s) != 0; }();
-  return on;
+// (the batch log showed 3.9 s and 3.2 s batches; C5 shard 1/8 cold 64.0 s vs 16.5 s warm).
+// Environment knobs: tests and measurements only (every default is the measured best). All of
+// them are read here, through env_num: GI_LOG (bit 1 device allocations >= 64 MiB, bit 2 one
+// line per batch, bit 4 one line per chunk k-NN launch; stderr), GI_KNN_DBG (k-NN kernel
+// diagnostics, KnnArgs::dbg), GI_DBG (render-kernel diagnostics, RenderArgs::dbg), GI_SLOT_LIMIT,
+// and the exactness-tested alternatives gi_create lists (the tests select them to show that the
+// default's result does not depend on them).
+static double env_num(const char *name, double def) {
+  const char *s = getenv(name);
+  return (s && *s) ? atof(s) : def;
 }
+static int log_bits() {
+  static const int bits = (int)env_num("GI_LOG", 0);
+  return bits;
+}
+static bool alloc_log() { return (log_bits() & 1) != 0; }
 struct DBuf {
   void *p = nullptr;
   size_t cap = 0;
@@ -315,7 +324,7 @@ struct gi_ctx {
   DevMap dmap[2];
   bool map_valid[2] = {false, false};
   int leaf_size[2] = {64, 256};  // photons per kd leaf, per map (global, caustic)
-  bool gpu_kd = true;            // kd trees built on the device (gi_kdbuild.hip); GI_KD_BUILD=host
+  bool gpu_kd = true;            // kd trees built on the device (gi_kdbuild.hip); GI_HOST_KD=1: host
   KdBuildScratch kdb;            // its scratch
   DBuf kd_ph;                    // emission-ordered photons uploaded for the device build
   int wave_cap_mul = 1;
@@ -331,15 +340,16 @@ struct gi_ctx {
   double p2_ms[2] = {0, 0};       // second chunk pass's time and queries per map
   uint64_t p2_q[2] = {0, 0};
   int last_kind[2] = {-1, -1};
-  bool knn_log = false;            // GI_KNN_LOG: one stderr line per chunk k-NN launch
+  bool knn_log = false;            // GI_LOG & 4: one stderr line per chunk k-NN launch
+  int knn_dbg = 0;                 // GI_KNN_DBG: k-NN kernel diagnostics (KnnArgs::dbg)
+  int render_dbg = 0;              // GI_DBG: render-kernel diagnostics (RenderArgs::dbg)
+  int64_t slot_limit = 0;          // GI_SLOT_LIMIT: path slots per batch (tests; 0 = 2^31)
   int elem_pretest = -1;           // GI_ELEM_PRETEST: -1 auto (make_view), 0 off, 1 on
   gi_progress_fn progress = nullptr;  // gi_set_progress
   void *progress_user = nullptr;
   int64_t progress_done = 0, progress_total = 0;  // output pixels of the current RenderImage     // k-NN kind run_knn chose last, per map (gi_render_stats)
   int sel_slack = 64;
   int knn_qpl = 1;
-  int ind_waves = 4;              // indirect-path kernel occupancy target (launch_ind)
-  uint32_t dump_fb_max = 0;       // GI_DUMP_FB diagnostics: largest fallback list written
   DBuf ind_cont, ind_ncont;       // indirect paths that continue past their first bounce
   DBuf mc_cont, mc_ncont;         // Monte Carlo paths' indirect sub-paths
   DBuf mc_cont2, mc_ncont2;       // ... those continuing past a glass / mirror first hit
@@ -356,9 +366,9 @@ struct gi_ctx {
   DBuf spawn, npaths, path_off, nmc, mc_off, nind, ind_off, base, pixels, rgbf, rgb8, qcount, stats_bak;
   DBuf qpos[2], qshade[2], qkey[2], qout[2];
   bool chunk_big2 = true;            // large-K chunk k-NN: further chunk passes
-  // ... the second pass's LDS candidates (GI_CHUNK_CAP_BIG2; kernel instances: 384, 512, 1024)
-  // and a third pass's (GI_CHUNK_CAP_BIG3; 0: none). r05: a 576-candidate pass at two waves per
-  // SIMD, alone or before the 1024 one, was not faster (profiles/r05_chunk_pass_chain_ab.txt)
+  // ... the second pass's LDS candidates (1024) and a third pass's (GI_CHUNK_CAP_BIG3, test knob;
+  // 0: none). r05: a 576-candidate pass at two waves per SIMD, alone or before the 1024 one, was
+  // not faster (profiles/r05_chunk_pass_chain_ab.txt)
   int chunk_cap_big2 = 1024;
   int chunk_cap_big3 = 0;
   bool chunk_lane2 = true;           // lane-select chunk k-NN: second pass (480, GI_CHUNK_LANE2)
@@ -369,9 +379,8 @@ struct gi_ctx {
   // and after an instance without it met a query that needed it), -1 test knob: claim that no
   // render query needs it (GI_KNN_GENERAL=-1; exercises render_common's re-run)
   int knn_general_mode = 0;
-  bool sort_all = false;  // GI_SORT_ALL=1: sort / search every list slot, empty ones included
-  // launch-order cells per axis for the global / caustic list (GI_KEY_BITS_G / _C; > 10: 64-bit
-  // keys, gi_sort.hip curve64_valid_kernel). The caustic queries crowd into foci far smaller than
+  // launch-order cells per axis for the global / caustic list (> 10: 64-bit keys, gi_sort.hip
+  // curve64_valid_kernel). The caustic queries crowd into foci far smaller than
   // a 10-bit cell of the scene box, where a cell's queries stay in slot order: 16-bit cells cut
   // the C4 shard's caustic k-NN 207 -> 155 ms per launch (second-pass queries 37.8 % -> 14.9 %).
   // The global list (C2: 400 M slots, one query per ~cell) keeps 32-bit keys: a 64-bit sort
@@ -380,11 +389,6 @@ struct gi_ctx {
   // GI_ROW_ORDER (default 1): the global list's valid slots compacted from the row masks before
   // the sort (gi_sort.h curve_order_rows) instead of sorting every slot with the empty ones last
   bool row_order = true;
-  // GI_EARLY_KNN=1: in a batch with Monte Carlo paths on the side stream, the k-NN of the
-  // deterministic query slots runs before the join, beside the side stream's tail (off by
-  // default: C2 -0.4 % per frame, but the global k-NN launches that share the GPU with the
-  // Monte Carlo kernel then take 45.3 -> 47.0 ms on average; render_pixels)
-  bool early_knn = false;
   bool use_dk = true;              // wave k-NN kernel starts from per-photon K-th bounds
   DBuf qseg[2];  // K-best lists of the query-per-wave k-NN path
   size_t qcap_hint[2] = {0, 0};
@@ -405,7 +409,7 @@ struct gi_ctx {
   // query budget below (queries per primary sample vary ~10x between scenes).
   int64_t prim_per_batch = 1 << 21;
   int64_t batch_reruns = 0;          // batches re-run smaller for 32-bit path slots (render_pixels)
-  bool batch_log = false;            // GI_BATCH_LOG: per-batch sizes and times on stderr
+  bool batch_log = false;            // GI_LOG & 2: per-batch sizes and times on stderr
   int64_t query_budget = 400000000;  // photon-map queries per batch (~120 B each: ~48 GB)
   double q_per_prim = 0.0;           // largest queries per primary sample seen so far
   double mc_app_rate[2] = {0.0, 0.0};  // per list: largest appends per Monte Carlo path seen
@@ -909,7 +913,7 @@ KnnArgs knn_args(gi_ctx *c, int mi) {
   k.chunk_minsub = c->chunk_minsub;
   k.qpl = c->knn_qpl;
   k.general = c->knn_general_mode > 0 ? 1 : c->knn_general_mode < 0 ? 0 : knn_general(c->scene.mats, k.filter);
-  if (const char *s = getenv("GI_KNN_DBG")) k.dbg = atoi(s);
+  k.dbg = c->knn_dbg;
   return k;
 }
 
@@ -1037,26 +1041,6 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
       HIPCHK(c, hipMemcpyAsync(&nfb2, dense + nin, 4, hipMemcpyDeviceToHost, X.st));
       HIPCHK(c, hipStreamSynchronize(X.st));
     }
-    bool dumped = false;
-    if (const char *dp = getenv("GI_DUMP_FB"); dp && ran2 && nfb2 > c->dump_fb_max) {
-      // diagnostics (tools/caustic_fb_dump.py): the launch with the most fallback queries, as
-      // float4 positions of the final fallback list, then of the second pass's list. Its copies
-      // and file writes sit between the events, so this launch is left out of the timings.
-      dumped = true;
-      c->dump_fb_max = nfb2;
-      std::vector<uint32_t> i1(nfb), i2(nfb2);
-      HIPCHK(c, hipMemcpy(i1.data(), X.fb_dense.p, (size_t)nfb * 4, hipMemcpyDeviceToHost));
-      HIPCHK(c, hipMemcpy(i2.data(), dense, (size_t)nfb2 * 4, hipMemcpyDeviceToHost));
-      std::vector<float> qp((size_t)nq * 4);
-      HIPCHK(c, hipMemcpy(qp.data(), k.qpos, (size_t)nq * 16, hipMemcpyDeviceToHost));
-      if (FILE *f = fopen(dp, "wb")) {
-        int64_t hdr[4] = {nq, (int64_t)nfb, (int64_t)nfb2, k.stat_off ? 1 : 0};
-        fwrite(hdr, 8, 4, f);
-        for (uint32_t q : i2) fwrite(&qp[(size_t)q * 4], 4, 4, f);
-        for (uint32_t q : i1) fwrite(&qp[(size_t)q * 4], 4, 4, f);
-        fclose(f);
-      }
-    }
     HIPCHK(c, hipEventRecord(X.ev3, X.st));
     if (nfb2) {
       KnnArgs f = k;
@@ -1068,7 +1052,7 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
       HIPCHK(c, hipGetLastError());
     }
     HIPCHK(c, hipEventRecord(X.ev1, X.st));
-    if (ms && !dumped) {
+    if (ms) {
       HIPCHK(c, hipEventSynchronize(X.ev1));
       float t = 0, tf = 0, t2 = 0;
       HIPCHK(c, hipEventElapsedTime(&t, X.ev0, X.ev1));
@@ -1288,12 +1272,9 @@ int knn_list(gi_ctx *c, int mi, const float4 *qpos, const QShade *qshade, int64_
     // only the valid queries are sorted and searched: the empty deterministic slots (indirect
     // paths absorbed, escaped, or whose continuation left no query; primaries without their own
     // query; Monte Carlo paths that deferred none) are ~46 % of C2's global list, and the
-    // reduction never reads their outputs (their keys / row-mask bits mark them). GI_SORT_ALL=1:
-    // the r04 behaviour (every slot sorted, empties skipped inside the k-NN kernels).
+    // reduction never reads their outputs (their keys / row-mask bits mark them).
     uint32_t *perm = nullptr;
-    if (c->sort_all) {
-      HIPCHK(c, morton_order(qpos, nq, c->sbmin, c->sbmax, X.sorter, &perm, X.st));
-    } else if (rows && c->row_order && c->key_bits[mi] <= 10) {
+    if (rows && c->row_order && c->key_bits[mi] <= 10) {
       // compacted from the row masks: the empty slots are never read or sorted
       int64_t nv = 0;
       HIPCHK(c, curve_order_rows(qpos, rows->nprim, rows->qmask, rows->trows, rows->qbase, nq,
@@ -1330,7 +1311,7 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
   // is re-run at half the primary samples, as often as needed (slot_limit: GI_SLOT_LIMIT, tests)
   int64_t shrink = 1;
   uint64_t slot_limit = 0xFFFFFFF0ull;
-  if (const char *s = getenv("GI_SLOT_LIMIT")) slot_limit = std::max(1ULL, strtoull(s, nullptr, 10));
+  if (c->slot_limit > 0) slot_limit = (uint64_t)c->slot_limit;
   int64_t nbatch = 0;
   for (int64_t p0 = 0, npix = 0; p0 < npix_total; p0 += npix) {
     auto tb0 = std::chrono::steady_clock::now();
@@ -1359,9 +1340,8 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     a.out_w = w;
     a.nprim = nprim;
     a.stats = c->d_stats.as<unsigned long long>();
-    a.ind_waves = c->ind_waves;
     a.split_ind = c->split_ind;
-    if (const char *s = getenv("GI_DBG")) a.dbg = atoi(s);
+    a.dbg = c->render_dbg;
     HIPCHK(c, c->spawn.ensure((size_t)nprim * sizeof(Spawn)));
     HIPCHK(c, c->npaths.ensure((size_t)nprim * 4));
     HIPCHK(c, c->path_off.ensure((size_t)(nprim + 1) * 4));
@@ -1473,18 +1453,6 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     // paths' tiled slots; Monte Carlo paths append after qbase[l]
     uint32_t qbase[2] = {(uint32_t)(nprim + tind), (uint32_t)nprim};
     a.qind_base = nprim;
-    // Early k-NN (batches with Monte Carlo paths on the side stream): the deterministic slots
-    // [0, qbase[l]) are written only by the main stream's kernels (slot0, ind, ind_cont; the
-    // Monte Carlo paths only append, PathCtx::fixed = -1), so their estimates run on the main
-    // stream as soon as its path kernels end, while the side stream's Monte Carlo tail is still
-    // running; the appends [qbase[l], nq[l]) are estimated after the join. Each query's result
-    // is independent of the launch it is in, so the image is the same. Not beside the
-    // persistent Monte Carlo kernel (mc_next: soft-light scenes), whose waves hold every SIMD's
-    // registers until its last path ends: there the k-NN only waits for CUs (C3 2,485 -> 2,513
-    // ms with it; C2, plain mc_kernel, 1,460.7 -> 1,455.5 ms; profiles/r05_early_knn_ab.txt:
-    // the plain kernel fills the chip too, so there is little tail to hide).
-    const bool early = c->early_knn && a.total_mc > 0 && !a.mc_next && c->stream2 && c->ev_fork &&
-                       c->ev_join;
     for (int attempt = 0; attempt < 3; attempt++) {
       for (int l = 0; l < 2; l++) {
         // capacity: the largest list seen so far (+25 %), or this batch's primaries at the
@@ -1519,20 +1487,8 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
       a.qcount = c->qcount.as<uint32_t>();
       HIPCHK(c, hipMemcpyAsync(c->qcount.p, qbase, 8, hipMemcpyHostToDevice, c->stream));
       if (tind > (uint64_t)a.total_ind) launch_ind_pad(a, c->stream);  // (never when tind = 0)
-      if (early)  // outputs for the whole capacity: the appends' part is written after the join
-        for (int l = 0; l < 2; l++)
-          if (c->map_valid[l]) HIPCHK(c, c->qout[l].ensure((size_t)a.qcap[l] * 24));
-      launch_path(a, c->stream, c->stream2, c->ev_fork, c->ev_join, !early);
+      launch_path(a, c->stream, c->stream2, c->ev_fork, c->ev_join, true);
       HIPCHK(c, hipGetLastError());
-      if (early) {
-        for (int l = 0; l < 2; l++) {
-          if (!c->map_valid[l] || qbase[l] == 0) continue;
-          int rc = knn_list(c, l, a.qpos[l], a.qshade[l], qbase[l], c->qout[l].as<double>(),
-                            rs ? &knn_ms[l] : nullptr);
-          if (rc) return rc;
-        }
-        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
-      }
       HIPCHK(c, hipMemcpyAsync(nq, c->qcount.p, 8, hipMemcpyDeviceToHost, c->stream));
       uint32_t fills[IND_QS * 32];
       if (a.split_ind && a.total_ind > 0)
@@ -1567,7 +1523,7 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
       a.qapp[l] = qbase[l];
       a.qout[l] = nullptr;
       if (nq[l]) {
-        if (!early || !c->map_valid[l]) HIPCHK(c, c->qout[l].ensure((size_t)nq[l] * 24));
+        HIPCHK(c, c->qout[l].ensure((size_t)nq[l] * 24));
         a.qout[l] = c->qout[l].as<double>();
         if (!c->map_valid[l])
           HIPCHK(c, hipMemsetAsync(c->qout[l].p, 0, (size_t)nq[l] * 24, c->stream));
@@ -1580,14 +1536,11 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     int rcm[2] = {GI_OK, GI_OK};
     for (int l = 0; l < 2; l++) {
       if (!run[l]) continue;
-      const uint32_t q0 = early ? qbase[l] : 0u;  // early: the deterministic part is done
       // the global list's launch order from its row masks (GI_ROW_ORDER, default on)
       ListRows lr{nprim, a.ind_qmask, (int64_t)(tind / 64), qbase[0]};
-      const bool use_rows = l == 0 && q0 == 0 && a.ind_qmask && (a.total_ind > 0 || tind == 0);
-      if (nq[l] > q0)
-        rcm[l] = knn_list(c, l, a.qpos[l] + q0, a.qshade[l] + q0, nq[l] - q0,
-                          c->qout[l].as<double>() + 3 * (size_t)q0, rs ? &knn_ms[l] : nullptr,
-                          use_rows ? &lr : nullptr);
+      const bool use_rows = l == 0 && a.ind_qmask && (a.total_ind > 0 || tind == 0);
+      rcm[l] = knn_list(c, l, a.qpos[l], a.qshade[l], nq[l], c->qout[l].as<double>(),
+                        rs ? &knn_ms[l] : nullptr, use_rows ? &lr : nullptr);
       if (rcm[l]) break;
     }
     for (int l = 0; l < 2; l++) {
@@ -1623,7 +1576,7 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     launch_reduce(a, c->stream);
     HIPCHK(c, hipGetLastError());
     if (c->progress) c->progress(0, (double)(p0 + npix) / (double)npix_total, c->progress_user);
-    if (c->batch_log) {  // GI_BATCH_LOG: one stderr line per batch (synchronises the batch)
+    if (c->batch_log) {  // GI_LOG & 2: one stderr line per batch (synchronises the batch)
       HIPCHK(c, hipStreamSynchronize(c->stream));
       double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count();
       fprintf(stderr, "[gi] batch %lld: pixels %lld primaries %lld paths %u tiled %llu mc %lld "
@@ -1726,38 +1679,31 @@ int gi_create(gi_ctx **out, int dev) {
     return GI_ERR_HIP;
   }
   hipStreamSynchronize(c->stream);
-  if (const char *s = getenv("GI_PRIM_PER_BATCH")) c->prim_per_batch = std::max(1LL, atoll(s));
-  if (const char *s = getenv("GI_QUERY_BUDGET")) c->query_budget = std::max(1LL, atoll(s));
-  // tuning knobs (measurement only; defaults are the measured best)
-  if (const char *s = getenv("GI_LEAF_SIZE")) c->leaf_size[0] = c->leaf_size[1] = std::max(1, atoi(s));
-  if (const char *s = getenv("GI_KD_BUILD")) c->gpu_kd = strcmp(s, "host") != 0;
-  if (const char *s = getenv("GI_PHOTON_2PASS")) c->photon_2pass = atoi(s) != 0;
-  if (const char *s = getenv("GI_PHOTON_RATE0"))  // test knob: first launch's slots per photon
-    c->prate[0] = c->prate[1] = std::max(0.0, atof(s));
-  if (const char *s = getenv("GI_CHUNK_MINSUB_BIG")) c->chunk_minsub_big = std::min(64, std::max(1, atoi(s)));
-  if (const char *s = getenv("GI_CHUNK_CAP_BIG")) c->chunk_cap_big = std::max(1, atoi(s));
-  if (const char *s = getenv("GI_CHUNK_DK_EXACT")) c->chunk_dk_exact = atoi(s) != 0;
-  if (const char *s = getenv("GI_CHUNK_CAP_BIG2")) c->chunk_cap_big2 = atoi(s);
-  if (const char *s = getenv("GI_CHUNK_CAP_BIG3")) c->chunk_cap_big3 = atoi(s);
-  if (const char *s = getenv("GI_CHUNK_MINSUB")) c->chunk_minsub = std::min(64, std::max(1, atoi(s)));
-  if (const char *s = getenv("GI_SPLIT_IND")) c->split_ind = atoi(s) != 0;
-  if (const char *s = getenv("GI_KNN_GENERAL")) c->knn_general_mode = std::max(-1, std::min(1, atoi(s)));
-  if (const char *s = getenv("GI_KNN_DK")) c->use_dk = atoi(s) != 0;
-  if (const char *s = getenv("GI_CHUNK_DK")) c->chunk_dk = atoi(s) != 0;
-  if (const char *s = getenv("GI_MC_SUB")) c->mc_sub = atoi(s) != 0;
-  if (const char *s = getenv("GI_MC_PERSIST")) c->mc_persist = std::max(-1, atoi(s));
-  if (const char *s = getenv("GI_BATCH_LOG")) c->batch_log = atoi(s) != 0;
-  if (const char *s = getenv("GI_KNN_LOG")) c->knn_log = atoi(s) != 0;
-  if (const char *s = getenv("GI_ELEM_PRETEST")) c->elem_pretest = atoi(s) != 0;
-  if (const char *s = getenv("GI_CHUNK_FB_ALL")) c->chunk_fb_all = atoi(s) != 0;
-  if (const char *s = getenv("GI_IND_FRAC")) c->ind_frac = std::min(1.0, std::max(1e-6, atof(s)));
-  if (const char *s = getenv("GI_IND_WAVES")) c->ind_waves = std::min(4, std::max(2, atoi(s)));
-  if (const char *s = getenv("GI_KNN_KERNEL")) c->knn_kernel_kind = atoi(s);
-  if (const char *s = getenv("GI_SORT_ALL")) c->sort_all = atoi(s) != 0;
-  if (const char *s = getenv("GI_ROW_ORDER")) c->row_order = atoi(s) != 0;
-  if (const char *s = getenv("GI_KEY_BITS_G")) c->key_bits[0] = std::max(1, std::min(20, atoi(s)));
-  if (const char *s = getenv("GI_KEY_BITS_C")) c->key_bits[1] = std::max(1, std::min(20, atoi(s)));
-  if (const char *s = getenv("GI_EARLY_KNN")) c->early_knn = atoi(s) != 0;
+  // diagnostics and the exactness-tested alternatives (tests/test_gpu_*.py select them)
+  c->batch_log = (log_bits() & 2) != 0;
+  c->knn_log = (log_bits() & 4) != 0;
+  c->knn_dbg = (int)env_num("GI_KNN_DBG", 0);
+  c->render_dbg = (int)env_num("GI_DBG", 0);
+  c->slot_limit = (int64_t)env_num("GI_SLOT_LIMIT", 0);
+  if (const int ls = (int)env_num("GI_LEAF_SIZE", 0); ls > 0) c->leaf_size[0] = c->leaf_size[1] = ls;
+  c->gpu_kd = env_num("GI_HOST_KD", 0) == 0;                      // 1: the host kd build
+  c->photon_2pass = env_num("GI_PHOTON_2PASS", c->photon_2pass) != 0;
+  c->prate[0] = c->prate[1] = std::max(0.0, env_num("GI_PHOTON_RATE0", c->prate[0]));
+  c->chunk_minsub_big = std::min(64, std::max(1, (int)env_num("GI_CHUNK_MINSUB_BIG", c->chunk_minsub_big)));
+  c->chunk_dk_exact = env_num("GI_CHUNK_DK_EXACT", c->chunk_dk_exact) != 0;
+  c->chunk_cap_big3 = (int)env_num("GI_CHUNK_CAP_BIG3", c->chunk_cap_big3);
+  c->chunk_minsub = std::min(64, std::max(1, (int)env_num("GI_CHUNK_MINSUB", c->chunk_minsub)));
+  c->split_ind = env_num("GI_SPLIT_IND", c->split_ind) != 0;
+  c->knn_general_mode = std::max(-1, std::min(1, (int)env_num("GI_KNN_GENERAL", c->knn_general_mode)));
+  c->use_dk = env_num("GI_KNN_DK", c->use_dk) != 0;
+  c->chunk_dk = env_num("GI_CHUNK_DK", c->chunk_dk) != 0;
+  c->mc_sub = env_num("GI_MC_SUB", c->mc_sub) != 0;
+  c->mc_persist = std::max(-1, (int)env_num("GI_MC_PERSIST", c->mc_persist));
+  c->elem_pretest = env_num("GI_ELEM_PRETEST", c->elem_pretest) != 0;
+  c->chunk_fb_all = env_num("GI_CHUNK_FB_ALL", c->chunk_fb_all) != 0;
+  c->ind_frac = std::min(1.0, std::max(1e-6, env_num("GI_IND_FRAC", c->ind_frac)));
+  c->knn_kernel_kind = (int)env_num("GI_KNN_KERNEL", c->knn_kernel_kind);
+  c->row_order = env_num("GI_ROW_ORDER", c->row_order) != 0;
   *out = c;
   return GI_OK;
 }
@@ -1779,8 +1725,7 @@ int gi_create_devices(gi_ctx **out, const gi_device_set *set) {
     c->peers.push_back(d);
     for (int j = 0; j < k; j++) distinct = distinct && set->devices[j] != set->devices[k];
   }
-  const char *g = getenv("GI_GATHER");  // "peer": hipMemcpyPeer instead of RCCL (diagnostics)
-  if (set->count > 1 && distinct && !(g && !strcmp(g, "peer"))) {
+  if (set->count > 1 && distinct) {
     if (!g_rccl.load()) {
       gi_destroy(c);
       return GI_ERR_UNSUPPORTED;
@@ -2215,7 +2160,7 @@ static int render_common(gi_ctx *c, int aa, int w, int h, const std::vector<int3
   if (rgbf) HIPCHK(c, hipMemcpyAsync(rgbf, c->rgbf.p, npx * 4, hipMemcpyDeviceToHost, c->stream));
   if (rgb8) HIPCHK(c, hipMemcpyAsync(rgb8, c->rgb8.p, npx, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (const char *kd = getenv("GI_KNN_DBG"); kd && (atoi(kd) & 16)) {
+  if (c->knn_dbg & 16) {
     fprintf(stderr, "[gi] k-NN phase cycles (sum over waves):");
     for (int i = 0; i < 16; i++) fprintf(stderr, " %llu", s[ST_PHASE + i]);
     fprintf(stderr, "\n");
@@ -2496,9 +2441,21 @@ int gi_estimate_radiance_batch(gi_ctx *c, int map, int64_t n, const gi_radiance_
   k.out = dout.as<double>();
   k.out_n = dn.as<int32_t>();
   k.out_maxd2 = dmd.as<float>();
-  k.stats = nullptr;
-  int rc = run_knn(c, k, n, nullptr);
-  if (rc) return rc;
+  // an instance without the general estimate form counts the queries it cannot answer
+  // (ST_GEN_MISS; the batch's own materials decide, so none is expected): re-run those batches
+  // with the general instances instead of returning NaN
+  unsigned long long *miss = c->d_stats.as<unsigned long long>() + ST_GEN_MISS;
+  for (int pass = 0;; pass++) {
+    HIPCHK(c, hipMemsetAsync(miss, 0, 8, c->stream));
+    int rc = run_knn(c, k, n, nullptr);
+    if (rc) return rc;
+    unsigned long long nm = 0;
+    HIPCHK(c, hipMemcpyAsync(&nm, miss, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (nm == 0) break;
+    if (pass > 0 || k.general) return fail(c, GI_ERR_STATE, "k-NN estimate: general-form miss");
+    k.general = 1;
+  }
   HIPCHK(c, hipMemcpyAsync(rgb_out, dout.p, (size_t)n * 24, hipMemcpyDeviceToHost, c->stream));
   if (nfound) HIPCHK(c, hipMemcpyAsync(nfound, dn.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
   if (maxd2) HIPCHK(c, hipMemcpyAsync(maxd2, dmd.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
@@ -2601,7 +2558,9 @@ int gi_knn_bench(gi_ctx *c, int map, int64_t n, const double *pts, const double 
   if (rc) return rc;
   unsigned long long st[ST_COUNT];
   HIPCHK(c, read_stats(c, st));
-  if (const char *kd = getenv("GI_KNN_DBG"); kd && (atoi(kd) & 16)) {
+  // a measurement over wrong (NaN) estimates would be meaningless
+  if (st[ST_GEN_MISS]) return fail(c, GI_ERR_STATE, "k-NN bench: queries needed the general estimate form");
+  if (c->knn_dbg & 16) {
     fprintf(stderr, "[gi] k-NN phase cycles (sum over waves):");
     for (int i = 0; i < 16; i++) fprintf(stderr, " %llu", st[ST_PHASE + i]);
     fprintf(stderr, "\n");

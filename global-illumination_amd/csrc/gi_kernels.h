@@ -98,7 +98,6 @@ struct RenderArgs {
   const uint32_t *mc_tab;    // same for the Monte Carlo paths
   int64_t total_mc, total_ind;
   int64_t tind;               // tiled indirect entries (64 per row, >= total_ind; RenderArgs::ind_rows)
-  int32_t ind_waves;    // occupancy target of the indirect-path kernel (waves per SIMD)
   int32_t dbg;          // diagnostics: 1 = skip the indirect trace, 2 = skip diffuse sampling too
   int32_t split_ind;    // 1: indirect paths trace their first bounce, continuations are queued
   IndCont *ind_cont;    // continuation queue: IND_QS stripes of ind_cap_s entries

@@ -373,9 +373,6 @@ __device__ __forceinline__ void mc_begin(McLoop &L, V org, V dir, const Rng &rng
   L.iter = 0;
 }
 
-#ifndef MC_ISECT_OOL
-#define MC_ISECT_OOL 0
-#endif
 // One iteration of MonteCarlo_PathTrace's loop (DEFER: indirect sub-paths go to the mc_cont
 // queue). Returns false when the path has ended.
 template <uint32_t KINDS = KINDS_ALL, bool DEFER = false, bool HARD = false>
@@ -388,12 +385,7 @@ __device__ __forceinline__ bool mc_step(PathCtx &P, McLoop &L) {
   Rng &rng = L.rng;
   C3 &tw = L.tw;
   Hit h;
-  bool hit;
-  if constexpr (MC_ISECT_OOL && (KINDS & ~KINDS_TRI_SPHERE) != 0)
-    hit = scene_intersect_ool<KINDS>(S, L.org, L.dir, h, P.hint);
-  else
-    hit = scene_intersect<KINDS>(S, L.org, L.dir, h, P.hint);
-  if (!hit) {
+  if (!scene_intersect<KINDS>(S, L.org, L.dir, h, P.hint)) {
     P.base += W * (tw * ldc(S.background));
     return false;
   }
@@ -1894,13 +1886,12 @@ void launch_primary(const RenderArgs &a, hipStream_t st) {
 }
 // occupancy: 4 waves per SIMD where the kernel fits 128 VGPRs without spills (triangles and
 // spheres only; C2 ind_kernel 37.8 -> 31.3 ms, frame -2.6 %), else 3 (the 4-wave instances of
-// the other element sets spill 74-129 VGPRs)
+// the other element sets spill 74-129 VGPRs; 3 or 5 waves for triangles and spheres measured
+// slower, profiles/r05_ind_waves_ab.txt)
 template <uint32_t KINDS>
 void launch_ind(const RenderArgs &a, unsigned g, hipStream_t st) {
-  const int w = KINDS == KINDS_TRI_SPHERE ? a.ind_waves : (a.ind_waves < 3 ? a.ind_waves : 3);
-  if (w <= 2) ind_kernel<2, true, KINDS><<<g, 128, 0, st>>>(a);
-  else if (w == 3) ind_kernel<3, true, KINDS><<<g, 128, 0, st>>>(a);
-  else ind_kernel<4, true, KINDS><<<g, 128, 0, st>>>(a);
+  if (KINDS == KINDS_TRI_SPHERE) ind_kernel<4, true, KINDS><<<g, 128, 0, st>>>(a);
+  else ind_kernel<3, true, KINDS><<<g, 128, 0, st>>>(a);
 }
 void launch_cont(const RenderArgs &a, const IndCont *q, const uint32_t *fill, uint32_t cap_s,
                  hipStream_t st) {

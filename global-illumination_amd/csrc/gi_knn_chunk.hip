@@ -95,9 +95,6 @@ struct Cands {
   }
 };
 
-#ifndef D2X8_PHASED
-#define D2X8_PHASED 1
-#endif
 // d2 of the 8 candidates s0 .. s0 + 7 (s0 % 8 == 0, s0 + 8 <= CAPC): six broadcast reads
 template <int CAPC>
 __device__ __forceinline__ void cand_d2x8(const Cands<CAPC> &C, uint32_t s0, float qx, float qy,
@@ -105,7 +102,6 @@ __device__ __forceinline__ void cand_d2x8(const Cands<CAPC> &C, uint32_t s0, flo
   const float4 x0 = C.quad(0, s0), x1 = C.quad(0, s0 + 4);
   const float4 y0 = C.quad(1, s0), y1 = C.quad(1, s0 + 4);
   const float4 z0 = C.quad(2, s0), z1 = C.quad(2, s0 + 4);
-#if D2X8_PHASED
   // metric() in packed pairs, each operation on all four pairs before the next one: no packed
   // result is read by the next instruction (the dependent v_pk_* pairs otherwise take s_nop)
   typedef float f2 __attribute__((ext_vector_type(2)));
@@ -131,16 +127,6 @@ __device__ __forceinline__ void cand_d2x8(const Cands<CAPC> &C, uint32_t s0, flo
     d[2 * i] = r[i].x;
     d[2 * i + 1] = r[i].y;
   }
-#else
-  d[0] = metric(qx, qy, qz, make_float4(x0.x, y0.x, z0.x, 0.f));
-  d[1] = metric(qx, qy, qz, make_float4(x0.y, y0.y, z0.y, 0.f));
-  d[2] = metric(qx, qy, qz, make_float4(x0.z, y0.z, z0.z, 0.f));
-  d[3] = metric(qx, qy, qz, make_float4(x0.w, y0.w, z0.w, 0.f));
-  d[4] = metric(qx, qy, qz, make_float4(x1.x, y1.x, z1.x, 0.f));
-  d[5] = metric(qx, qy, qz, make_float4(x1.y, y1.y, z1.y, 0.f));
-  d[6] = metric(qx, qy, qz, make_float4(x1.z, y1.z, z1.z, 0.f));
-  d[7] = metric(qx, qy, qz, make_float4(x1.w, y1.w, z1.w, 0.f));
-#endif
 }
 
 // squared gap between a point/box and box B, same fp32 operation order as the photon metric
@@ -269,7 +255,7 @@ struct ChunkProf {
 // (scalar loads, ld_node) and pushes one, so backtracking reads nothing from memory. leaf(l)
 // returns true to stop the walk. Returns the number of node records read.
 //
-// WALK2: an expansion whose children are internal also reads the four grandchildren (128
+// Two levels per round trip: an expansion whose children are internal also reads the four grandchildren (128
 // contiguous bytes, issued with the children's 64): two levels per dependent round trip. A
 // grandchild is taken when its parent and its own box pass, as two single-level expansions
 // would take it, and the in-grandchildren are pushed right to left, so leaves are still visited
@@ -283,9 +269,6 @@ struct ChunkProf {
 // pass are exactly those the node-by-node walk reaches, in the same left-to-right order: the
 // candidate order, and every result, are unchanged; the bottom levels' dependent node loads
 // become one round trip per subtree.
-#ifndef WALK2
-#define WALK2 1
-#endif
 #ifndef CHUNK_SWEEP_H
 #define CHUNK_SWEEP_H 6
 #endif
@@ -315,7 +298,7 @@ __device__ __forceinline__ uint32_t walk_within(const float *nodes, int L, float
     } else {
       const int c = 2 * node;
       KdNode c0 = ld_node(nodes, c), c1 = ld_node(nodes, c + 1);
-      if (WALK2 && h > CHUNK_SWEEP_H + 1) {
+      if (h > CHUNK_SWEEP_H + 1) {
         KdNode g0 = ld_node(nodes, 2 * c), g1 = ld_node(nodes, 2 * c + 1);
         KdNode g2 = ld_node(nodes, 2 * c + 2), g3 = ld_node(nodes, 2 * c + 3);
         reads += 6;
@@ -450,9 +433,9 @@ __device__ __forceinline__ void chunk_bound_gather(const KnnArgs &a, int lane, b
   if (N > 0 && K > 0) {
     int node = 1;
     while (node < L) {
-      // (WALK2) the node's children are read with it: two levels per round trip
+      // the node's children are read with it: two levels per round trip
       KdNode nd = ld_node(a.map.nodes, node), k0, k1;
-      const bool two = WALK2 && 2 * node < L;
+      const bool two = 2 * node < L;
       if (two) { k0 = ld_node(a.map.nodes, 2 * node); k1 = ld_node(a.map.nodes, 2 * node + 1); }
       const int ax = __float_as_int(nd.hi.w);
       if (lane == depth) { path_split = nd.lo.w; path_axis = ax; }
@@ -1008,9 +991,6 @@ __device__ __forceinline__ bool in_bracket(float d2, uint32_t ab, uint32_t span)
 __device__ __forceinline__ float next_up(float x) { return __uint_as_float(__float_as_uint(x) + 1u); }
 __device__ __forceinline__ float next_down(float x) { return __uint_as_float(__float_as_uint(x) - 1u); }
 
-#ifndef LS_ONE_STORE
-#define LS_ONE_STORE 1  // lane select: one LDS store per collected candidate (r05)
-#endif
 // CAPC = 240 (first pass): 10,112 B of LDS per wave, so 16 waves (4 per SIMD, the VGPR limit)
 // fit in a CU's 160 KiB (256 candidates took 10,752 B: 14 waves); u8 slots and u8 counters.
 // CAPC = 480 (second pass over the first's overflowing chunks): u16 slots and counters, 19.8 KB.
@@ -1032,10 +1012,10 @@ void knn_chunk_lane_kernel(KnnArgs a) {
   // bound phase the centre select's 256-bin histogram. One spare slot row (row 64): a lane that
   // keeps exactly K = 64 photons without a bracket stores its later, unkept candidates there
   // (the collect's branch-free store always writes entry n).
-  // counting-pass layout (LS_ONE_STORE): lane-major with a stride of NWC + 1 words (coprime with
+  // counting-pass layout (r05): lane-major with a stride of NWC + 1 words (coprime with
   // the banks: conflict-free), so a counter's address is base + (b & ~(PERW - 1)) / PERW words
   // -- one and + add instead of the word-major layout's shift, and, add
-  constexpr int CST = LS_ONE_STORE ? NWC + 1 : 64;   // counter row stride (words)
+  constexpr int CST = NWC + 1;   // counter row stride (words)
   __shared__ uint32_t selh[(16 * SB * 64 + 16 * SB) > 64 * (NWC + 1) ? (16 * SB * 64 + 16 * SB) : 64 * (NWC + 1)];
   SlotT *sel = reinterpret_cast<SlotT *>(selh);
   uint32_t *hist = selh;
@@ -1107,7 +1087,7 @@ void knn_chunk_lane_kernel(KnnArgs a) {
         // LS_NB = 64 bins per lane: u8 counters packed four per LDS word [w][lane] (w = bin / 4;
         // conflict-free, one ds_add per candidate; at most 255 members, so no byte carries)
 #pragma unroll
-        for (int w = 0; w < NWC; w++) selh[LS_ONE_STORE ? lane * CST + w : w * 64 + lane] = 0u;
+        for (int w = 0; w < NWC; w++) selh[lane * CST + w] = 0u;
         // groups of 8 candidates: the group's (broadcast) LDS reads are issued together and the
         // loop body has no branches (non-members, and the +inf padding past `count`, add 0)
         constexpr uint32_t PERW = 4 / SB;  // counters per word
@@ -1118,11 +1098,7 @@ void knn_chunk_lane_kernel(KnnArgs a) {
           for (int u = 0; u < 8; u++) {
             const uint32_t b = binN<LS_NB>(dg[u], sc, off);
             const uint32_t inc = in_bracket(dg[u], ab, span) ? (1u << ((b & (PERW - 1u)) * 8u * SB)) : 0u;
-#if LS_ONE_STORE
             atomicAdd(&selh[lane * CST + b / PERW], inc);
-#else
-            atomicAdd(&selh[(b / PERW) * 64 + lane], inc);
-#endif
           }
         }
         if (on) {
@@ -1131,7 +1107,7 @@ void knn_chunk_lane_kernel(KnnArgs a) {
           constexpr uint32_t CM = SB == 1 ? 255u : 65535u;
 #pragma unroll
           for (int w = 0; w < NWC; w++) {
-            const uint32_t c4 = selh[LS_ONE_STORE ? lane * CST + w : w * 64 + lane];
+            const uint32_t c4 = selh[lane * CST + w];
             const uint32_t ws = SB == 1 ? __builtin_amdgcn_sad_u8(c4, 0u, 0u) : (c4 & 65535u) + (c4 >> 16);
             if (bs == LS_NB) {
               if (before + ws >= (uint32_t)need) {
@@ -1204,54 +1180,58 @@ void knn_chunk_lane_kernel(KnnArgs a) {
         const float d2 = dg[u];
         const bool kf = d2 < acol;
         const bool kb = in_bracket(d2, ab, span);
-#if LS_ONE_STORE
         // one store per candidate: a bracket member to the back entry bm, anything else to the
         // front entry n (a kept one stays there, an unkept one is overwritten by the next kept
         // one or never read; a lane without a bracket may fill all 64 entries, row 64 spare)
         sel[(kb ? bm : n) * 64 + lane] = (SlotT)s;
-#else
-        // (a lane without a bracket may fill all 64 entries: its bracket store goes to n too,
-        // before the front store of the same value)
-        sel[(inb_on ? bm : n) * 64 + lane] = (SlotT)s;
-        sel[n * 64 + lane] = (SlotT)s;
-#endif
         n += kf ? 1 : 0;
         bm -= kb ? 1 : 0;
         km = fmaxf(km, kf ? d2 : 0.0f);
       }
     }
     m = 63 - bm;
-    if (inb_on) {
-      // sort the bracket by (d2, kd index) and keep `need` of it
+    // keep the `need` smallest (d2, kd index) of the bracket, appended in that order: each
+    // member's rank among the lane's members (keys are unique: kd indices differ) is its offset
+    // in the kept list. Unrolled over LS_BR_L entries, but every step past the wave's largest
+    // bracket is skipped by a uniform branch, so a wave pays mw (mw - 1) / 2 compares for its
+    // largest bracket mw instead of a full sorting network.
+    {
+      int mw = inb_on ? m : 0;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mw = max(mw, __shfl_xor(mw, o, 64));
       uint64_t fk[LS_BR_L];
-      uint32_t sl[LS_BR_L];
+      uint32_t sl[LS_BR_L], rk[LS_BR_L];
 #pragma unroll
       for (int i = 0; i < LS_BR_L; i++) {
         sl[i] = 0u;
         fk[i] = ~0ull;
-        if (i < m) {
+        rk[i] = 0u;
+        if (i >= mw) continue;
+        if (inb_on && i < m) {
           sl[i] = sel[(63 - i) * 64 + lane];
           float d2 = cpos.d2(qx, qy, qz, sl[i]);
           fk[i] = ((uint64_t)__float_as_uint(d2) << 32) | (uint64_t)cidx[sl[i]];
         }
       }
-      // (a Batcher network sized to the wave's largest bracket, 4 / 8 / 12 keys, was measured
-      // slower, r05: 10 -> 35 spilled VGPRs, global k-NN 45.0 -> 47.1 ms per C2 launch)
 #pragma unroll
-      for (int i = 0; i < LS_BR_L; i++)
+      for (int i = 1; i < LS_BR_L; i++) {
+        if (i < mw) {
 #pragma unroll
-        for (int j = 0; j + 1 < LS_BR_L - i; j++)
-          if (fk[j + 1] < fk[j]) {
-            uint64_t t = fk[j]; fk[j] = fk[j + 1]; fk[j + 1] = t;
-            uint32_t u = sl[j]; sl[j] = sl[j + 1]; sl[j + 1] = u;
+          for (int j = 0; j < i; j++) {
+            const bool lt = fk[j] < fk[i];
+            rk[i] += lt ? 1u : 0u;
+            rk[j] += lt ? 0u : 1u;
           }
+        }
+      }
 #pragma unroll
-      for (int i = 0; i < LS_BR_L; i++)
-        if (i < need) {
-          sel[n * 64 + lane] = (SlotT)sl[i];
-          n++;
+      for (int i = 0; i < LS_BR_L; i++) {
+        if (i < mw && inb_on && i < m && rk[i] < (uint32_t)need) {
+          sel[(n + (int)rk[i]) * 64 + lane] = (SlotT)sl[i];
           km = fmaxf(km, __uint_as_float((uint32_t)(fk[i] >> 32)));
         }
+      }
+      if (inb_on) n += need;
     }
     P.lap(2);
     // ---- 4. estimate
@@ -1444,33 +1424,44 @@ void knn_chunk_big_kernel(KnnArgs a) {
       selw[w0 * 64 + lane] = bits;
       n += __popc(bits);
     }
-    if (inb_on) {
+    // the `need` smallest (d2, kd index) of the bracket by rank (the kept set is a bitmask, so
+    // only membership matters); steps past the wave's largest bracket skipped (uniform branch)
+    {
+      int mw = inb_on ? m : 0;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mw = max(mw, __shfl_xor(mw, o, 64));
       uint64_t fk[BRB];
-      uint32_t sl[BRB];
+      uint32_t sl[BRB], rk[BRB];
 #pragma unroll
       for (int i = 0; i < BRB; i++) {
         sl[i] = 0u;
         fk[i] = ~0ull;
-        if (i < m) {
+        rk[i] = 0u;
+        if (i >= mw) continue;
+        if (inb_on && i < m) {
           sl[i] = brl[i * 64 + lane];
           fk[i] = ((uint64_t)__float_as_uint(cpos.d2(qx, qy, qz, sl[i])) << 32) | (uint64_t)cidx[sl[i]];
         }
       }
 #pragma unroll
-      for (int i = 0; i < BRB; i++)
+      for (int i = 1; i < BRB; i++) {
+        if (i < mw) {
 #pragma unroll
-        for (int j = 0; j + 1 < BRB - i; j++)
-          if (fk[j + 1] < fk[j]) {
-            uint64_t t = fk[j]; fk[j] = fk[j + 1]; fk[j + 1] = t;
-            uint32_t u = sl[j]; sl[j] = sl[j + 1]; sl[j + 1] = u;
+          for (int j = 0; j < i; j++) {
+            const bool lt = fk[j] < fk[i];
+            rk[i] += lt ? 1u : 0u;
+            rk[j] += lt ? 0u : 1u;
           }
+        }
+      }
 #pragma unroll
-      for (int i = 0; i < BRB; i++)
-        if (i < need) {
+      for (int i = 0; i < BRB; i++) {
+        if (i < mw && inb_on && i < m && rk[i] < (uint32_t)need) {
           selw[(sl[i] / 32) * 64 + lane] |= 1u << (sl[i] % 32);
-          n++;
           km = fmaxf(km, __uint_as_float((uint32_t)(fk[i] >> 32)));
         }
+      }
+      if (inb_on) n += need;
     }
     P.lap(2);
     // ---- estimate: the lane walks its bitmask in slot order

@@ -7,9 +7,9 @@ namespace gi {
 struct SortScratch {
   void *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *v1 = nullptr, *tmp = nullptr;
   size_t k0_cap = 0, k1_cap = 0, v0_cap = 0, v1_cap = 0, tmp_cap = 0;
-  // curve_order_rows: the row masks, their counts / offsets and the compacted slot list
-  void *rows = nullptr, *cnt = nullptr, *vl = nullptr;
-  size_t rows_cap = 0, cnt_cap = 0, vl_cap = 0;
+  // curve_order_rows: the row masks and their counts / offsets
+  void *rows = nullptr, *cnt = nullptr;
+  size_t rows_cap = 0, cnt_cap = 0;
 };
 // returns a device permutation (sorted position -> query index) valid until the next call
 hipError_t morton_order(const float4 *q, int64_t n, const float bmin[3], const float bmax[3],

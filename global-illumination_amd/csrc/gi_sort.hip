@@ -10,10 +10,6 @@
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
 #include "gi_sort.h"
-#ifndef FUSED_ROW_KEYS
-#define FUSED_ROW_KEYS 1
-#endif
-#define FUSED_ROW_KEYS_ON FUSED_ROW_KEYS
 
 namespace gi {
 
@@ -26,17 +22,13 @@ __device__ __forceinline__ uint32_t spread10(uint32_t v) {
   return v;
 }
 
-#ifndef KEY_HILBERT
-#define KEY_HILBERT 1
-#endif
-// 30-bit space-filling-curve key of a 10-bit cell (x, y, z). KEY_HILBERT: the 3-D Hilbert curve
+// 30-bit space-filling-curve key of a 10-bit cell (x, y, z): the 3-D Hilbert curve
 // (Skilling's axes-to-transpose, "Programming the Hilbert curve", AIP Conf. Proc. 707, 2004),
 // its transposed bits interleaved as Morton's are: consecutive keys are face-adjacent cells, so
 // a 64-query chunk of the sorted list is more compact than a Z-order run (a floor patch at C2's
 // query density: chunk radius 0.00170 -> 0.00133, photons gathered per chunk 87 -> 77;
 // tools/sim_chunks.py). Only the order of the k-NN launches changes, never a result.
 __device__ __forceinline__ uint32_t curve_key10(uint32_t x, uint32_t y, uint32_t z) {
-#if KEY_HILBERT
   uint32_t X[3] = {x, y, z};
   for (uint32_t Q = 1u << 9; Q > 1u; Q >>= 1) {
     const uint32_t P = Q - 1u;
@@ -60,9 +52,6 @@ __device__ __forceinline__ uint32_t curve_key10(uint32_t x, uint32_t y, uint32_t
   X[1] ^= t;
   X[2] ^= t;
   return (spread10(X[0]) << 2) | (spread10(X[1]) << 1) | spread10(X[2]);
-#else
-  return (spread10(x) << 2) | (spread10(y) << 1) | spread10(z);
-#endif
 }
 
 // the same curve on B bits per axis (11 <= B <= 20) as a 64-bit key (3B bits)
@@ -111,30 +100,34 @@ __global__ void morton_kernel(const float4 *q, int64_t n, float ox, float oy, fl
   vals[i] = (uint32_t)i;
 }
 
+// A sort scratch buffer that only grows, with the headroom rule of gi_host.cpp's DBuf: 1/8 above
+// the request (at most 1.5x the old capacity), and none when the device is short of memory.
+static hipError_t grow_scratch(void *&p, size_t &cap, size_t bytes) {
+  if (bytes <= cap && p) return hipSuccess;
+  size_t want = cap ? std::max(bytes, std::min(cap + cap / 2, bytes + bytes / 8)) : bytes;
+  if (p) hipFree(p);
+  p = nullptr;
+  cap = 0;
+  if (want > bytes) {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < want + tot / 4) want = bytes;
+  }
+  hipError_t r = hipMalloc(&p, want);
+  if (r != hipSuccess && want > bytes) {
+    (void)hipGetLastError();
+    want = bytes;
+    r = hipMalloc(&p, want);
+  }
+  if (r == hipSuccess) cap = want;
+  return r;
+}
+
 hipError_t morton_order(const float4 *q, int64_t n, const float bmin[3], const float bmax[3],
                         SortScratch &s, uint32_t **perm_out, hipStream_t st) {
   *perm_out = nullptr;
   if (n <= 0) return hipSuccess;
   hipError_t e;
-  auto grow = [&](void *&p, size_t &cap, size_t bytes) -> hipError_t {
-    if (bytes <= cap && p) return hipSuccess;
-    size_t want = cap ? std::max(bytes, std::min(cap + cap / 2, bytes + bytes / 8)) : bytes;  // headroom (gi_host.cpp DBuf)
-    if (p) hipFree(p);
-    p = nullptr;
-    cap = 0;
-    if (want > bytes) {
-      size_t fr = 0, tot = 0;
-      if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < want + tot / 4) want = bytes;
-    }
-    hipError_t r = hipMalloc(&p, want);
-    if (r != hipSuccess && want > bytes) {
-      (void)hipGetLastError();
-      want = bytes;
-      r = hipMalloc(&p, want);
-    }
-    if (r == hipSuccess) cap = want;
-    return r;
-  };
+  auto grow = grow_scratch;
   size_t b4 = (size_t)n * 4;
   if ((e = grow(s.k0, s.k0_cap, b4)) != hipSuccess) return e;
   if ((e = grow(s.k1, s.k1_cap, b4)) != hipSuccess) return e;
@@ -196,16 +189,18 @@ __global__ void curve64_valid_kernel(const float4 *q, int64_t n, float ox, float
   keys[i] = valid ? curve_key64<B>((uint32_t)fx, (uint32_t)fy, (uint32_t)fz) : (1ull << (3 * B));
   vals[i] = (uint32_t)i;
 }
-__global__ void __launch_bounds__(64) first_empty64_kernel(const uint64_t *k, int64_t n,
-                                                           uint64_t empty,
-                                                           unsigned long long *out) {
-  int64_t lo = 0, hi = n;
+// first sorted key >= empty (the valid keys sort before the empty slots' key): one wave, 64
+// probes per round
+template <typename KeyT>
+__global__ void __launch_bounds__(64) first_empty_kernel(const KeyT *k, int64_t n, KeyT empty,
+                                                         unsigned long long *out) {
+  int64_t lo = 0, hi = n;  // the answer lies in [lo, hi]
   const int lane = threadIdx.x;
   while (lo < hi) {
     const int64_t step = (hi - lo + 63) / 64;
     const int64_t p = lo + lane * step;
     const uint64_t m = __ballot(p >= hi || k[p] >= empty);
-    if (m == 0) {
+    if (m == 0) {  // every probe valid: past lane 63's
       lo += 63 * step + 1;
       continue;
     }
@@ -228,39 +223,9 @@ __global__ void row_popc_kernel(const uint64_t *rows, int64_t R, uint32_t *cnt) 
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r < R) cnt[r] = (uint32_t)__popcll(rows[r]);
 }
-// lane b of row r's wave writes slot(r, b) to its rank among the row's set bits
-__global__ void row_scatter_kernel(const uint64_t *rows, const uint32_t *off, int64_t Rp,
-                                   int64_t R, int64_t nprim, uint32_t *vl) {
-  const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (r >= R) return;
-  const uint64_t m = rows[r];
-  if ((m >> lane) & 1ull) {
-    const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-    const int64_t slot = r < Rp ? 64 * r + lane : nprim + 64 * (r - Rp) + lane;
-    vl[off[r] + rank] = (uint32_t)slot;
-  }
-}
-// keys of the compacted list: entries [0, ndet) from vl, then the appends qbase + (i - ndet)
-__global__ void curve_list_kernel(const float4 *q, const uint32_t *vl, int64_t ndet,
-                                  uint32_t qbase, int64_t n, float ox, float oy, float oz,
-                                  float sx, float sy, float sz, float cmax, uint32_t *keys,
-                                  uint32_t *vals) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t slot = i < ndet ? vl[i] : qbase + (uint32_t)(i - ndet);
-  const float4 p = q[slot];
-  const bool valid = __float_as_uint(p.w) != 0xffffffffu;  // (always, by the masks)
-  float fx = fminf(fmaxf((p.x - ox) * sx, 0.0f), cmax);
-  float fy = fminf(fmaxf((p.y - oy) * sy, 0.0f), cmax);
-  float fz = fminf(fmaxf((p.z - oz) * sz, 0.0f), cmax);
-  keys[i] = valid ? curve_key10((uint32_t)fx, (uint32_t)fy, (uint32_t)fz) : (1u << 30);
-  vals[i] = slot;
-}
-
-// the scatter and the keys in one pass (FUSED_ROW_KEYS): lane b of row r's wave writes the key
-// and slot of its query at the query's compacted position; the appends get theirs in
-// append_keys_kernel. Same keys at the same positions as row_scatter + curve_list.
+// the scatter and the keys in one pass (r05): lane b of row r's wave writes the key and slot of
+// its query at the query's compacted position (its rank among the row's set bits after the
+// rows before it); the appends get theirs in append_keys_kernel
 __device__ __forceinline__ uint32_t slot_key10(const float4 *q, uint32_t slot, float ox, float oy,
                                                float oz, float sx, float sy, float sz, float cmax) {
   const float4 p = q[slot];
@@ -298,25 +263,6 @@ __global__ void append_keys_kernel(const float4 *q, uint32_t qbase, int64_t napp
 // the number of valid queries = the first sorted key >= 2^30, by a 64-way search in one wave
 // (a per-wave atomic count in morton_valid_kernel serialised 6M same-address atomics: r05i,
 // +32 ms per list)
-__global__ void __launch_bounds__(64) first_empty_kernel(const uint32_t *k, int64_t n,
-                                                         unsigned long long *out) {
-  int64_t lo = 0, hi = n;  // the answer lies in [lo, hi]
-  const int lane = threadIdx.x;
-  while (lo < hi) {
-    const int64_t step = (hi - lo + 63) / 64;
-    const int64_t p = lo + lane * step;
-    const uint64_t m = __ballot(p >= hi || k[p] >= (1u << 30));
-    if (m == 0) {  // every probe valid: past lane 63's
-      lo += 63 * step + 1;
-      continue;
-    }
-    const int f = __ffsll((unsigned long long)m) - 1;
-    const int64_t nhi = lo + f * step;
-    lo = f ? lo + (f - 1) * step + 1 : lo;
-    hi = nhi < hi ? nhi : hi;
-  }
-  if (lane == 0) *out = (unsigned long long)lo;
-}
 
 hipError_t morton_order_valid(const float4 *q, int64_t n, const float bmin[3], const float bmax[3],
                               SortScratch &s, uint32_t **perm_out, int64_t *nvalid, hipStream_t st,
@@ -325,25 +271,7 @@ hipError_t morton_order_valid(const float4 *q, int64_t n, const float bmin[3], c
   *nvalid = 0;
   if (n <= 0) return hipSuccess;
   hipError_t e;
-  auto grow = [&](void *&p, size_t &cap, size_t bytes) -> hipError_t {
-    if (bytes <= cap && p) return hipSuccess;
-    size_t want = cap ? std::max(bytes, std::min(cap + cap / 2, bytes + bytes / 8)) : bytes;  // headroom (gi_host.cpp DBuf)
-    if (p) hipFree(p);
-    p = nullptr;
-    cap = 0;
-    if (want > bytes) {
-      size_t fr = 0, tot = 0;
-      if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < want + tot / 4) want = bytes;
-    }
-    hipError_t r = hipMalloc(&p, want);
-    if (r != hipSuccess && want > bytes) {
-      (void)hipGetLastError();
-      want = bytes;
-      r = hipMalloc(&p, want);
-    }
-    if (r == hipSuccess) cap = want;
-    return r;
-  };
+  auto grow = grow_scratch;
   size_t b4 = (size_t)n * 4;
   const bool wide = key_bits > 10;
   const size_t kb = wide ? 2 * b4 : b4;
@@ -384,7 +312,7 @@ hipError_t morton_order_valid(const float4 *q, int64_t n, const float bmin[3], c
                                            (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0,
                                            3 * B + 1, st);
     if (e != hipSuccess) return e;
-    first_empty64_kernel<<<1, 64, 0, st>>>((const uint64_t *)s.k1, n, 1ull << (3 * B), d_cnt);
+    first_empty_kernel<uint64_t><<<1, 64, 0, st>>>((const uint64_t *)s.k1, n, 1ull << (3 * B), d_cnt);
   } else {
   constexpr int bits = 10;
   const float cmax = (float)((1 << bits) - 1);
@@ -407,7 +335,7 @@ hipError_t morton_order_valid(const float4 *q, int64_t n, const float bmin[3], c
                                          (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0,
                                          3 * bits + 1, st);
   if (e != hipSuccess) return e;
-  first_empty_kernel<<<1, 64, 0, st>>>((const uint32_t *)s.k1, n, d_cnt);
+  first_empty_kernel<uint32_t><<<1, 64, 0, st>>>((const uint32_t *)s.k1, n, 1u << 30, d_cnt);
   }
   unsigned long long nv = 0;
   if ((e = hipMemcpyAsync(&nv, d_cnt, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
@@ -428,25 +356,7 @@ hipError_t key_order(const uint64_t *keys, int64_t n, int key_bits, KeySortScrat
   *sslots = nullptr;
   if (n <= 0) return hipSuccess;
   hipError_t e;
-  auto grow = [&](void *&p, size_t &cap, size_t bytes) -> hipError_t {
-    if (bytes <= cap && p) return hipSuccess;
-    size_t want = cap ? std::max(bytes, std::min(cap + cap / 2, bytes + bytes / 8)) : bytes;  // headroom (gi_host.cpp DBuf)
-    if (p) hipFree(p);
-    p = nullptr;
-    cap = 0;
-    if (want > bytes) {
-      size_t fr = 0, tot = 0;
-      if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < want + tot / 4) want = bytes;
-    }
-    hipError_t r = hipMalloc(&p, want);
-    if (r != hipSuccess && want > bytes) {
-      (void)hipGetLastError();
-      want = bytes;
-      r = hipMalloc(&p, want);
-    }
-    if (r == hipSuccess) cap = want;
-    return r;
-  };
+  auto grow = grow_scratch;
   if ((e = grow(s.k1, s.k1_cap, (size_t)n * 8)) != hipSuccess) return e;
   if ((e = grow(s.v0, s.v0_cap, (size_t)n * 4)) != hipSuccess) return e;
   if ((e = grow(s.v1, s.v1_cap, (size_t)n * 4)) != hipSuccess) return e;
@@ -474,7 +384,7 @@ void sort_scratch_release(KeySortScratch &s) {
 }
 
 void sort_scratch_release(SortScratch &s) {
-  void *ps[] = {s.k0, s.k1, s.v0, s.v1, s.tmp, s.rows, s.cnt, s.vl};
+  void *ps[] = {s.k0, s.k1, s.v0, s.v1, s.tmp, s.rows, s.cnt};
   for (void *p : ps)
     if (p) hipFree(p);
   s = SortScratch();
@@ -487,25 +397,7 @@ hipError_t curve_order_rows(const float4 *q, int64_t nprim, const uint64_t *qmas
   *nvalid = 0;
   if (nq <= 0) return hipSuccess;
   hipError_t e;
-  auto grow = [&](void *&p, size_t &cap, size_t bytes) -> hipError_t {
-    if (bytes <= cap && p) return hipSuccess;
-    size_t want = cap ? std::max(bytes, std::min(cap + cap / 2, bytes + bytes / 8)) : bytes;  // headroom (gi_host.cpp DBuf)
-    if (p) hipFree(p);
-    p = nullptr;
-    cap = 0;
-    if (want > bytes) {
-      size_t fr = 0, tot = 0;
-      if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < want + tot / 4) want = bytes;
-    }
-    hipError_t r = hipMalloc(&p, want);
-    if (r != hipSuccess && want > bytes) {
-      (void)hipGetLastError();
-      want = bytes;
-      r = hipMalloc(&p, want);
-    }
-    if (r == hipSuccess) cap = want;
-    return r;
-  };
+  auto grow = grow_scratch;
   const int64_t Rp = (nprim + 63) / 64, R = Rp + trows;
   if ((e = grow(s.rows, s.rows_cap, (size_t)(R + 1) * 8)) != hipSuccess) return e;
   if ((e = grow(s.cnt, s.cnt_cap, (size_t)(2 * R + 2) * 4)) != hipSuccess) return e;
@@ -531,7 +423,6 @@ hipError_t curve_order_rows(const float4 *q, int64_t nprim, const uint64_t *qmas
   const int64_t n = (int64_t)ndet + napp;
   if (n == 0) return hipSuccess;
   size_t b4 = (size_t)n * 4;
-  if (!FUSED_ROW_KEYS_ON && (e = grow(s.vl, s.vl_cap, (size_t)ndet * 4 + 4)) != hipSuccess) return e;
   if ((e = grow(s.k0, s.k0_cap, b4 + 16)) != hipSuccess) return e;
   if ((e = grow(s.k1, s.k1_cap, b4)) != hipSuccess) return e;
   if ((e = grow(s.v0, s.v0_cap, b4)) != hipSuccess) return e;
@@ -543,23 +434,14 @@ hipError_t curve_order_rows(const float4 *q, int64_t nprim, const uint64_t *qmas
     float ext = bmax[i] - bmin[i];
     sc[i] = ext > 0 ? cmax / ext : 0.0f;
   }
-  if (FUSED_ROW_KEYS) {
-    if (R > 0)
-      row_keys_kernel<<<(unsigned)((R + 3) / 4), 256, 0, st>>>(
-          rows, off, Rp, R, nprim, q, bmin[0], bmin[1], bmin[2], sc[0], sc[1], sc[2], cmax,
-          (uint32_t *)s.k0, (uint32_t *)s.v0);
-    if (napp > 0)
-      append_keys_kernel<<<(unsigned)((napp + 255) / 256), 256, 0, st>>>(
-          q, qbase, napp, (int64_t)ndet, bmin[0], bmin[1], bmin[2], sc[0], sc[1], sc[2], cmax,
-          (uint32_t *)s.k0, (uint32_t *)s.v0);
-  } else {
-    if (R > 0)
-      row_scatter_kernel<<<(unsigned)((R + 3) / 4), 256, 0, st>>>(rows, off, Rp, R, nprim,
-                                                                   (uint32_t *)s.vl);
-    curve_list_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(
-        q, (const uint32_t *)s.vl, (int64_t)ndet, qbase, n, bmin[0], bmin[1], bmin[2], sc[0],
-        sc[1], sc[2], cmax, (uint32_t *)s.k0, (uint32_t *)s.v0);
-  }
+  if (R > 0)
+    row_keys_kernel<<<(unsigned)((R + 3) / 4), 256, 0, st>>>(
+        rows, off, Rp, R, nprim, q, bmin[0], bmin[1], bmin[2], sc[0], sc[1], sc[2], cmax,
+        (uint32_t *)s.k0, (uint32_t *)s.v0);
+  if (napp > 0)
+    append_keys_kernel<<<(unsigned)((napp + 255) / 256), 256, 0, st>>>(
+        q, qbase, napp, (int64_t)ndet, bmin[0], bmin[1], bmin[2], sc[0], sc[1], sc[2], cmax,
+        (uint32_t *)s.k0, (uint32_t *)s.v0);
   auto *d_cnt = reinterpret_cast<unsigned long long *>((char *)s.k0 + ((b4 + 7) & ~(size_t)7));
   tb = 0;
   e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t *)s.k0, (uint32_t *)s.k1,
@@ -571,7 +453,7 @@ hipError_t curve_order_rows(const float4 *q, int64_t nprim, const uint64_t *qmas
                                          (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0,
                                          3 * bits + 1, st);
   if (e != hipSuccess) return e;
-  first_empty_kernel<<<1, 64, 0, st>>>((const uint32_t *)s.k1, n, d_cnt);
+  first_empty_kernel<uint32_t><<<1, 64, 0, st>>>((const uint32_t *)s.k1, n, 1u << 30, d_cnt);
   unsigned long long nv = 0;
   if ((e = hipMemcpyAsync(&nv, d_cnt, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
   if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;

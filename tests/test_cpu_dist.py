@@ -101,7 +101,7 @@ def _worker(rank, world, port, w, h, tile, q, packed=False):
 
 @pytest.mark.parametrize("packed", [False, True, "device_only"],
                          ids=["host", "packed", "cpu_device_host_path"])
-@pytest.mark.parametrize("world,w,h,tile", [(2, 70, 45, 16), (3, 64, 64, 16)])
+@pytest.mark.parametrize("world,w,h,tile", [(2, 70, 45, 16), (3, 64, 64, 16), (8, 130, 72, 16)])
 def test_sharded_gather_equals_full_frame(world, w, h, tile, packed):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

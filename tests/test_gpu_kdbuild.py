@@ -6,7 +6,7 @@ Checked on the tree the k-NN kernels read (gi_get_kd_tree):
   internal box is the union of its children; split = the median pivot (the smallest coordinate
   of the upper half), the left child's photons <= split <= the right child's along the axis; the
   axis is the longest extent of the node's box (x, then y / z only when strictly longer);
-- k-NN sets through the device-built tree equal the host-built tree's (GI_KD_BUILD=host) and
+- k-NN sets through the device-built tree equal the host-built tree's (GI_HOST_KD=1) and
   the oracle's, up to photons tied at the K-th distance;
 - a full-GI render on the device-built maps matches the oracle like the host-built ones did.
 """
@@ -69,15 +69,15 @@ def check_tree(nodes, perm, L, ph):
 
 @pytest.fixture(scope="module")
 def host_renderer():
-    old = os.environ.get("GI_KD_BUILD")
-    os.environ["GI_KD_BUILD"] = "host"
+    old = os.environ.get("GI_HOST_KD")
+    os.environ["GI_HOST_KD"] = "1"
     try:
         r = gi_amd.Renderer(0)
     finally:
         if old is None:
-            del os.environ["GI_KD_BUILD"]
+            del os.environ["GI_HOST_KD"]
         else:
-            os.environ["GI_KD_BUILD"] = old
+            os.environ["GI_HOST_KD"] = old
     yield r
     r.close()
 

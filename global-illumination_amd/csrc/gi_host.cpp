@@ -67,11 +67,14 @@ struct DBuf {
     return grow(bytes);
   }
   hipError_t grow(size_t bytes) {
-    // headroom for a buffer that has grown before: 1.5x the old capacity, but at most 1/8 above
-    // the request (the device memory a process leaves behind is cleared by the driver before
-    // another process can use it: a next process that needs more than the clean remainder waits
-    // seconds, so the footprint is kept near what a frame needs)
-    size_t grown = cap ? std::min(cap + cap / 2, bytes + bytes / 8) : 0;
+    // headroom for a buffer that has grown before: at least 1/8 above the request and at least
+    // twice the old capacity. Freed device memory is cleared by the driver before it is handed
+    // out again, and an allocation that finds no clean memory waits for it: C5's first frame
+    // (fresh box, first process) grew its buffers in 1/8 steps to 467 GB of cumulative
+    // allocation, 377 GB of it freed again, and one 32.9 GB step then waited 6.0 s (DESIGN.md
+    // 3.3). Doubling (capped at 1.5x the request, so that a buffer that needs just over its old
+    // capacity does not take twice that: C2's 33 GB shading list) keeps the steps few.
+    size_t grown = cap ? std::max(std::min(cap * 2, bytes + bytes / 2), bytes + bytes / 8) : 0;
     if (p) hipFree(p);
     p = nullptr;
     cap = 0;
@@ -335,6 +338,7 @@ struct gi_ctx {
   bool chunk_dk_exact = true;
   int chunk_minsub_big = 64;      // large-K chunk kernel: overflowing chunks retried down to this (64: none, measured best)
   int chunk_minsub = 32;          // chunk kernel: overflowing chunks retried as halves (measured best with the dk bound)
+  int chunk_minsub2 = 32;         // ... in its second (480) pass
   double fb_ms[2] = {0, 0};       // final fallback kernel's time and queries per map (since the
   uint64_t fb_q[2] = {0, 0};      // last reset)
   double p2_ms[2] = {0, 0};       // second chunk pass's time and queries per map
@@ -389,6 +393,7 @@ struct gi_ctx {
   // GI_ROW_ORDER (default 1): the global list's valid slots compacted from the row masks before
   // the sort (gi_sort.h curve_order_rows) instead of sorting every slot with the empty ones last
   bool row_order = true;
+  bool surf_key = false;            // global list: surface keys (gi_sort.hip surface_key) instead of the 3-D curve
   bool use_dk = true;              // wave k-NN kernel starts from per-photon K-th bounds
   DBuf qseg[2];  // K-best lists of the query-per-wave k-NN path
   size_t qcap_hint[2] = {0, 0};
@@ -1130,6 +1135,7 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
       s2.fb_count = X.fb_count2.as<uint32_t>();
       s2.fb_cap_s = cap2;
       s2.dbg &= ~16;
+      s2.chunk_minsub = c->chunk_minsub2;
       launch_knn_chunk2(s2, X.st);
       HIPCHK(c, hipGetLastError());
       dense = X.fb_dense2.as<uint32_t>();
@@ -1278,7 +1284,8 @@ int knn_list(gi_ctx *c, int mi, const float4 *qpos, const QShade *qshade, int64_
       // compacted from the row masks: the empty slots are never read or sorted
       int64_t nv = 0;
       HIPCHK(c, curve_order_rows(qpos, rows->nprim, rows->qmask, rows->trows, rows->qbase, nq,
-                                 c->sbmin, c->sbmax, X.sorter, &perm, &nv, X.st));
+                                 c->sbmin, c->sbmax, X.sorter, &perm, &nv, X.st,
+                                 c->surf_key ? qshade->n : nullptr, (int)(sizeof(QShade) / 8)));
       nq = nv;
       k.nq = nv;
       if (nv == 0) return GI_OK;
@@ -1660,8 +1667,19 @@ int gi_create(gi_ctx **out, int dev) {
   c->device = dev;
   gi_params_default(&c->P);
   if (hipSetDevice(dev) != hipSuccess) { delete c; return GI_ERR_HIP; }
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return GI_ERR_HIP; }
-  if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) c->stream2 = nullptr;
+  {
+    int lo = 0, hi = 0;
+    const bool prio = env_num("GI_SIDE_PRIO", 0) < 0 && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess;
+    if ((prio ? hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi)
+              : hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) { delete c; return GI_ERR_HIP; }
+  }
+  {
+    int lo = 0, hi = 0;  // priorities: lo = least urgent, hi = most urgent
+    const bool prio = env_num("GI_SIDE_PRIO", 0) > 0 && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess;
+    if ((prio ? hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, hi)
+              : hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking)) != hipSuccess)
+      c->stream2 = nullptr;
+  }
   hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
   hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
   for (int m = 0; m < 2; m++) {
@@ -1693,6 +1711,7 @@ int gi_create(gi_ctx **out, int dev) {
   c->chunk_dk_exact = env_num("GI_CHUNK_DK_EXACT", c->chunk_dk_exact) != 0;
   c->chunk_cap_big3 = (int)env_num("GI_CHUNK_CAP_BIG3", c->chunk_cap_big3);
   c->chunk_minsub = std::min(64, std::max(1, (int)env_num("GI_CHUNK_MINSUB", c->chunk_minsub)));
+  c->chunk_minsub2 = std::min(64, std::max(1, (int)env_num("GI_CHUNK_MINSUB2", c->chunk_minsub2)));
   c->split_ind = env_num("GI_SPLIT_IND", c->split_ind) != 0;
   c->knn_general_mode = std::max(-1, std::min(1, (int)env_num("GI_KNN_GENERAL", c->knn_general_mode)));
   c->use_dk = env_num("GI_KNN_DK", c->use_dk) != 0;
@@ -1704,6 +1723,7 @@ int gi_create(gi_ctx **out, int dev) {
   c->ind_frac = std::min(1.0, std::max(1e-6, env_num("GI_IND_FRAC", c->ind_frac)));
   c->knn_kernel_kind = (int)env_num("GI_KNN_KERNEL", c->knn_kernel_kind);
   c->row_order = env_num("GI_ROW_ORDER", c->row_order) != 0;
+  c->surf_key = env_num("GI_SURF_KEY", c->surf_key) != 0;
   *out = c;
   return GI_OK;
 }

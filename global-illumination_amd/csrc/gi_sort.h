@@ -27,11 +27,22 @@ hipError_t morton_order_valid(const float4 *q, int64_t n, const float bmin[3], c
 // own masks, gi_kernels.hip ind_kernel / ind_cont_kernel), then the appends [qbase, nq), all
 // valid. The valid slots are compacted (row popcounts, a scan, a scatter: no per-slot pass over
 // the empty ones), keyed like morton_order_valid and sorted: the first *nvalid entries of the
-// permutation are the same queries, in the same order, as morton_order_valid's.
+// permutation are the same queries, in the same order, as morton_order_valid's. With nrm (the
+// queries' surface normals, nstride doubles apart) the keys are surface keys instead (gi_sort.hip
+// surface_key: normal face, depth slab, 2-D Hilbert curve in the face's plane).
 hipError_t curve_order_rows(const float4 *q, int64_t nprim, const uint64_t *qmask, int64_t trows,
                             uint32_t qbase, int64_t nq, const float bmin[3], const float bmax[3],
-                            SortScratch &s, uint32_t **perm_out, int64_t *nvalid, hipStream_t st);
+                            SortScratch &s, uint32_t **perm_out, int64_t *nvalid, hipStream_t st,
+                            const double *nrm = nullptr, int nstride = 0);
 void sort_scratch_release(SortScratch &s);
+// key parameters: the 3-D curve's 10-bit cells (origin o, scale s per axis, cmax), or, with nrm,
+// the surface key's square 11-bit cells (siso) and 32 depth slabs per axis (sdep)
+struct KeyGeom {
+  float o[3], s[3], cmax;
+  float siso, sdep[3];
+  const double *nrm;
+  int nstride;
+};
 
 struct KeySortScratch {
   void *k1 = nullptr, *v0 = nullptr, *v1 = nullptr, *tmp = nullptr;

@@ -100,11 +100,11 @@ __global__ void morton_kernel(const float4 *q, int64_t n, float ox, float oy, fl
   vals[i] = (uint32_t)i;
 }
 
-// A sort scratch buffer that only grows, with the headroom rule of gi_host.cpp's DBuf: 1/8 above
-// the request (at most 1.5x the old capacity), and none when the device is short of memory.
+// A sort scratch buffer that only grows, with the headroom rule of gi_host.cpp's DBuf: at least
+// 1/8 above the request and twice the old capacity, none when the device is short of memory.
 static hipError_t grow_scratch(void *&p, size_t &cap, size_t bytes) {
   if (bytes <= cap && p) return hipSuccess;
-  size_t want = cap ? std::max(bytes, std::min(cap + cap / 2, bytes + bytes / 8)) : bytes;
+  size_t want = cap ? std::max(std::min(cap * 2, bytes + bytes / 2), bytes + bytes / 8) : bytes;
   if (p) hipFree(p);
   p = nullptr;
   cap = 0;
@@ -223,21 +223,56 @@ __global__ void row_popc_kernel(const uint64_t *rows, int64_t R, uint32_t *cnt) 
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r < R) cnt[r] = (uint32_t)__popcll(rows[r]);
 }
+// 30-bit surface key (r06): the query surface's dominant normal axis and side (6 faces, 3 bits),
+// its coordinate along that axis in 32 slabs of the scene box (5 bits), and the 2-D Hilbert
+// curve of the other two coordinates on square 11-bit cells (22 bits). Queries on a plane (every
+// global-map query of a cornell wall) then follow a 2-D curve in that plane instead of the plane's
+// cut through the 3-D curve, which leaves and re-enters it: 64 consecutive queries cover a
+// more compact patch, and the chunk gathers fewer photons.
+__device__ __forceinline__ uint32_t hilbert2_11(uint32_t x, uint32_t y) {
+  uint32_t d = 0;
+  for (uint32_t s = 1u << 10; s > 0u; s >>= 1) {
+    const uint32_t rx = (x & s) ? 1u : 0u, ry = (y & s) ? 1u : 0u;
+    d += s * s * ((3u * rx) ^ ry);
+    if (ry == 0u) {
+      if (rx == 1u) {
+        x = s - 1u - (x & (s - 1u));
+        y = s - 1u - (y & (s - 1u));
+      }
+      const uint32_t t = x;
+      x = y;
+      y = t;
+    }
+  }
+  return d;
+}
+__device__ __forceinline__ uint32_t surface_key(const float4 &p, const double *n, const KeyGeom &g) {
+  const double ax = fabs(n[0]), ay = fabs(n[1]), az = fabs(n[2]);
+  const int a = (ax >= ay && ax >= az) ? 0 : (ay >= az ? 1 : 2);
+  const int u = a == 0 ? 1 : 0, v = a == 2 ? 1 : 2;
+  const float c[3] = {p.x - g.o[0], p.y - g.o[1], p.z - g.o[2]};
+  const uint32_t face = 2u * (uint32_t)a + (n[a] < 0.0 ? 1u : 0u);
+  const uint32_t dep = (uint32_t)fminf(fmaxf(c[a] * g.sdep[a], 0.0f), 31.0f);
+  const uint32_t cu = (uint32_t)fminf(fmaxf(c[u] * g.siso, 0.0f), 2047.0f);
+  const uint32_t cv = (uint32_t)fminf(fmaxf(c[v] * g.siso, 0.0f), 2047.0f);
+  return (face << 27) | (dep << 22) | hilbert2_11(cu, cv);
+}
+
 // the scatter and the keys in one pass (r05): lane b of row r's wave writes the key and slot of
 // its query at the query's compacted position (its rank among the row's set bits after the
 // rows before it); the appends get theirs in append_keys_kernel
-__device__ __forceinline__ uint32_t slot_key10(const float4 *q, uint32_t slot, float ox, float oy,
-                                               float oz, float sx, float sy, float sz, float cmax) {
+__device__ __forceinline__ uint32_t slot_key10(const float4 *q, uint32_t slot, const KeyGeom &g) {
   const float4 p = q[slot];
   const bool valid = __float_as_uint(p.w) != 0xffffffffu;  // (always, by the masks)
-  float fx = fminf(fmaxf((p.x - ox) * sx, 0.0f), cmax);
-  float fy = fminf(fmaxf((p.y - oy) * sy, 0.0f), cmax);
-  float fz = fminf(fmaxf((p.z - oz) * sz, 0.0f), cmax);
-  return valid ? curve_key10((uint32_t)fx, (uint32_t)fy, (uint32_t)fz) : (1u << 30);
+  if (!valid) return 1u << 30;
+  if (g.nrm) return surface_key(p, g.nrm + (size_t)slot * g.nstride, g);
+  float fx = fminf(fmaxf((p.x - g.o[0]) * g.s[0], 0.0f), g.cmax);
+  float fy = fminf(fmaxf((p.y - g.o[1]) * g.s[1], 0.0f), g.cmax);
+  float fz = fminf(fmaxf((p.z - g.o[2]) * g.s[2], 0.0f), g.cmax);
+  return curve_key10((uint32_t)fx, (uint32_t)fy, (uint32_t)fz);
 }
 __global__ void row_keys_kernel(const uint64_t *rows, const uint32_t *off, int64_t Rp, int64_t R,
-                                int64_t nprim, const float4 *q, float ox, float oy, float oz,
-                                float sx, float sy, float sz, float cmax, uint32_t *keys,
+                                int64_t nprim, const float4 *q, KeyGeom g, uint32_t *keys,
                                 uint32_t *vals) {
   const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -246,17 +281,16 @@ __global__ void row_keys_kernel(const uint64_t *rows, const uint32_t *off, int64
   if ((m >> lane) & 1ull) {
     const uint32_t at = off[r] + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
     const uint32_t slot = (uint32_t)(r < Rp ? 64 * r + lane : nprim + 64 * (r - Rp) + lane);
-    keys[at] = slot_key10(q, slot, ox, oy, oz, sx, sy, sz, cmax);
+    keys[at] = slot_key10(q, slot, g);
     vals[at] = slot;
   }
 }
 __global__ void append_keys_kernel(const float4 *q, uint32_t qbase, int64_t napp, int64_t ndet,
-                                   float ox, float oy, float oz, float sx, float sy, float sz,
-                                   float cmax, uint32_t *keys, uint32_t *vals) {
+                                   KeyGeom g, uint32_t *keys, uint32_t *vals) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= napp) return;
   const uint32_t slot = qbase + (uint32_t)i;
-  keys[ndet + i] = slot_key10(q, slot, ox, oy, oz, sx, sy, sz, cmax);
+  keys[ndet + i] = slot_key10(q, slot, g);
   vals[ndet + i] = slot;
 }
 
@@ -392,7 +426,8 @@ void sort_scratch_release(SortScratch &s) {
 
 hipError_t curve_order_rows(const float4 *q, int64_t nprim, const uint64_t *qmask, int64_t trows,
                             uint32_t qbase, int64_t nq, const float bmin[3], const float bmax[3],
-                            SortScratch &s, uint32_t **perm_out, int64_t *nvalid, hipStream_t st) {
+                            SortScratch &s, uint32_t **perm_out, int64_t *nvalid, hipStream_t st,
+                            const double *nrm, int nstride) {
   *perm_out = nullptr;
   *nvalid = 0;
   if (nq <= 0) return hipSuccess;
@@ -428,20 +463,25 @@ hipError_t curve_order_rows(const float4 *q, int64_t nprim, const uint64_t *qmas
   if ((e = grow(s.v0, s.v0_cap, b4)) != hipSuccess) return e;
   if ((e = grow(s.v1, s.v1_cap, b4)) != hipSuccess) return e;
   constexpr int bits = 10;
-  const float cmax = (float)((1 << bits) - 1);
-  float sc[3];
+  KeyGeom g;
+  g.cmax = (float)((1 << bits) - 1);
+  float emax = 0.0f;
   for (int i = 0; i < 3; i++) {
     float ext = bmax[i] - bmin[i];
-    sc[i] = ext > 0 ? cmax / ext : 0.0f;
+    g.o[i] = bmin[i];
+    g.s[i] = ext > 0 ? g.cmax / ext : 0.0f;
+    g.sdep[i] = ext > 0 ? 32.0f / ext : 0.0f;
+    emax = std::max(emax, ext);
   }
+  g.siso = emax > 0 ? 2048.0f / emax : 0.0f;
+  g.nrm = nrm;
+  g.nstride = nstride;
   if (R > 0)
-    row_keys_kernel<<<(unsigned)((R + 3) / 4), 256, 0, st>>>(
-        rows, off, Rp, R, nprim, q, bmin[0], bmin[1], bmin[2], sc[0], sc[1], sc[2], cmax,
-        (uint32_t *)s.k0, (uint32_t *)s.v0);
+    row_keys_kernel<<<(unsigned)((R + 3) / 4), 256, 0, st>>>(rows, off, Rp, R, nprim, q, g,
+                                                             (uint32_t *)s.k0, (uint32_t *)s.v0);
   if (napp > 0)
     append_keys_kernel<<<(unsigned)((napp + 255) / 256), 256, 0, st>>>(
-        q, qbase, napp, (int64_t)ndet, bmin[0], bmin[1], bmin[2], sc[0], sc[1], sc[2], cmax,
-        (uint32_t *)s.k0, (uint32_t *)s.v0);
+        q, qbase, napp, (int64_t)ndet, g, (uint32_t *)s.k0, (uint32_t *)s.v0);
   auto *d_cnt = reinterpret_cast<unsigned long long *>((char *)s.k0 + ((b4 + 7) & ~(size_t)7));
   tb = 0;
   e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t *)s.k0, (uint32_t *)s.k1,

@@ -2,7 +2,8 @@
 """Chunk compactness of the k-NN launch order (gi_sort.hip curve_key10), simulated on the CPU:
 the global photon map of cornell.scn (oracle restatement, 1M photons), queries uniform on a 0.1 x
 0.1 floor patch at a given density (C2's global list: ~36 M valid queries per unit^2 per batch),
-sorted by 10-bit-per-axis Morton or Hilbert keys and cut into chunks of 64. Per chunk: rho (the
+sorted by 10-bit-per-axis Morton or Hilbert keys or by the surface key (gi_sort.hip
+surface_key: 2-D Hilbert curve in the floor's plane, r06) and cut into chunks of 64. Per chunk: rho (the
 largest query distance from the box centre) and the photons the chunk kernel gathers (a: within
 d_K(centre) + rho of the chunk box, gi_knn_chunk.hip chunk_bound_gather), with three tighter
 regions for reference (b: ball of d_K(c) + 2 rho around the centre; d: union of the balls
@@ -55,12 +56,29 @@ def hilbert(f, bits=10):
         for i in range(3):
             key=(key<<1)|((X[i]>>b)&1)
     return key
+def hilbert2(x, y, bits=11):
+    # gi_sort.hip hilbert2_11 (the surface key's in-plane curve), vectorized
+    x=x.astype(np.int64).copy(); y=y.astype(np.int64).copy(); d=np.zeros_like(x)
+    s=1<<(bits-1)
+    while s>0:
+        rx=((x&s)!=0).astype(np.int64); ry=((y&s)!=0).astype(np.int64)
+        d+=s*s*((3*rx)^ry)
+        flip=(ry==0)&(rx==1)
+        x=np.where(flip, s-1-(x&(s-1)), x); y=np.where(flip, s-1-(y&(s-1)), y)
+        sw=ry==0
+        x,y=np.where(sw,y,x),np.where(sw,x,y)
+        s>>=1
+    return d
 rng=np.random.default_rng(0)
 K=50; D=float(sys.argv[1]) if len(sys.argv)>1 else 36e6
 n=int(D*0.01)
 q=np.zeros((n,3),np.float32); q[:,0]=0.4+0.1*rng.random(n); q[:,2]=0.4+0.1*rng.random(n)
 f=np.clip((q-bmin)*(1023/(bmax-bmin)),0,1023).astype(np.uint32)
-for name,key in (('morton',morton(f)),('hilbert',hilbert(f))):
+# the surface key of a floor query (normal +y): face 2, depth slab, 2-D curve over (x, z)
+fi=np.clip((q-bmin)*(2048/float((bmax-bmin).max())),0,2047).astype(np.uint32)
+dep=np.clip((q[:,1]-bmin[1])*(32/(bmax[1]-bmin[1])),0,31).astype(np.int64)
+surf=(2<<27)|(dep<<22)|hilbert2(fi[:,0],fi[:,2])
+for name,key in (('morton',morton(f)),('hilbert',hilbert(f)),('surface',surf)):
     qs=q[np.argsort(key,kind='stable')]
     nch=min(n//64-2,2000)
     sel=np.random.default_rng(1).choice(n//64-2, nch, replace=False)+1

@@ -338,7 +338,6 @@ struct gi_ctx {
   bool chunk_dk_exact = true;
   int chunk_minsub_big = 64;      // large-K chunk kernel: overflowing chunks retried down to this (64: none, measured best)
   int chunk_minsub = 32;          // chunk kernel: overflowing chunks retried as halves (measured best with the dk bound)
-  int chunk_minsub2 = 32;         // ... in its second (480) pass
   double fb_ms[2] = {0, 0};       // final fallback kernel's time and queries per map (since the
   uint64_t fb_q[2] = {0, 0};      // last reset)
   double p2_ms[2] = {0, 0};       // second chunk pass's time and queries per map
@@ -393,7 +392,8 @@ struct gi_ctx {
   // GI_ROW_ORDER (default 1): the global list's valid slots compacted from the row masks before
   // the sort (gi_sort.h curve_order_rows) instead of sorting every slot with the empty ones last
   bool row_order = true;
-  bool surf_key = false;            // global list: surface keys (gi_sort.hip surface_key) instead of the 3-D curve
+  bool surf_key = true;             // global list: surface keys (gi_sort.hip surface_key) instead of the 3-D curve
+  bool surf_key_c = false;          // caustic list: 64-bit surface keys (surf64_valid_kernel)
   bool use_dk = true;              // wave k-NN kernel starts from per-photon K-th bounds
   DBuf qseg[2];  // K-best lists of the query-per-wave k-NN path
   size_t qcap_hint[2] = {0, 0};
@@ -1135,7 +1135,6 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
       s2.fb_count = X.fb_count2.as<uint32_t>();
       s2.fb_cap_s = cap2;
       s2.dbg &= ~16;
-      s2.chunk_minsub = c->chunk_minsub2;
       launch_knn_chunk2(s2, X.st);
       HIPCHK(c, hipGetLastError());
       dense = X.fb_dense2.as<uint32_t>();
@@ -1285,14 +1284,14 @@ int knn_list(gi_ctx *c, int mi, const float4 *qpos, const QShade *qshade, int64_
       int64_t nv = 0;
       HIPCHK(c, curve_order_rows(qpos, rows->nprim, rows->qmask, rows->trows, rows->qbase, nq,
                                  c->sbmin, c->sbmax, X.sorter, &perm, &nv, X.st,
-                                 c->surf_key ? qshade->n : nullptr, (int)(sizeof(QShade) / 8)));
+                                 c->surf_key));
       nq = nv;
       k.nq = nv;
       if (nv == 0) return GI_OK;
     } else {
       int64_t nv = 0;
       HIPCHK(c, morton_order_valid(qpos, nq, c->sbmin, c->sbmax, X.sorter, &perm, &nv, X.st,
-                                   c->key_bits[mi]));
+                                   c->key_bits[mi], c->surf_key_c));
       nq = nv;
       k.nq = nv;
       if (nv == 0) return GI_OK;
@@ -1607,6 +1606,7 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
 
 int upload_scene(gi_ctx *c) {
   HostScene &H = c->scene;
+  if (H.mats.size() >= (size_t)QMETA_MAX_MATS) return fail(c, GI_ERR_UNSUPPORTED, "more than 2^26 materials");
   HIPCHK(c, upload(c->d_nodes, H.nodes.data(), H.nodes.size() * sizeof(DNode), c->stream));
   HIPCHK(c, upload(c->d_elems, H.elems.data(), H.elems.size() * sizeof(DElement), c->stream));
   HIPCHK(c, upload(c->d_shapes, H.shapes.data(), H.shapes.size() * sizeof(DShape), c->stream));
@@ -1711,7 +1711,6 @@ int gi_create(gi_ctx **out, int dev) {
   c->chunk_dk_exact = env_num("GI_CHUNK_DK_EXACT", c->chunk_dk_exact) != 0;
   c->chunk_cap_big3 = (int)env_num("GI_CHUNK_CAP_BIG3", c->chunk_cap_big3);
   c->chunk_minsub = std::min(64, std::max(1, (int)env_num("GI_CHUNK_MINSUB", c->chunk_minsub)));
-  c->chunk_minsub2 = std::min(64, std::max(1, (int)env_num("GI_CHUNK_MINSUB2", c->chunk_minsub2)));
   c->split_ind = env_num("GI_SPLIT_IND", c->split_ind) != 0;
   c->knn_general_mode = std::max(-1, std::min(1, (int)env_num("GI_KNN_GENERAL", c->knn_general_mode)));
   c->use_dk = env_num("GI_KNN_DK", c->use_dk) != 0;
@@ -1724,6 +1723,7 @@ int gi_create(gi_ctx **out, int dev) {
   c->knn_kernel_kind = (int)env_num("GI_KNN_KERNEL", c->knn_kernel_kind);
   c->row_order = env_num("GI_ROW_ORDER", c->row_order) != 0;
   c->surf_key = env_num("GI_SURF_KEY", c->surf_key) != 0;
+  c->surf_key_c = env_num("GI_SURF_KEY_C", c->surf_key_c) != 0;
   *out = c;
   return GI_OK;
 }
@@ -2418,6 +2418,7 @@ int gi_estimate_radiance_batch(gi_ctx *c, int map, int64_t n, const gi_radiance_
   for (int64_t i = 1; i < n; i++)
     if (q[i].k != q[0].k || q[i].max_dist != q[0].max_dist || q[i].filter != q[0].filter)
       return fail(c, GI_ERR_ARG, "estimate_size / estimate_dist / filter must be uniform");
+  if (n > QMETA_MAX_MATS) return fail(c, GI_ERR_ARG, "at most 2^26 queries per call");
   // one material per query carries its brdf terms
   std::vector<DMaterial> mats(n);
   std::vector<float> qp(4 * n);

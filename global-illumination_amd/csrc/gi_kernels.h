@@ -269,6 +269,12 @@ __device__ __forceinline__ void wave_add(unsigned long long *dst, uint64_t v) {
 
 // query-list slot with no query (deterministic slots a path did not use): qpos.w bits
 constexpr uint32_t QMETA_NONE = 0xffffffffu;
+// a query's qpos.w bits: side of the surface (bits 0-1), material (bits 2-27), and the face of
+// its normal for the launch order (bits 28-30: dominant axis * 2 + negative; gi_sort.hip
+// surface_key); bit 31 is clear, so no query's bits equal QMETA_NONE
+constexpr uint32_t QMETA_MAT_MASK = 0x03ffffffu;
+constexpr int QMETA_MAX_MATS = 1 << 26;
+__host__ __device__ __forceinline__ uint32_t qmeta_mat(uint32_t meta) { return (meta >> 2) & QMETA_MAT_MASK; }
 
 enum { KNN_MODE_RADIANCE = 0, KNN_MODE_IRRADIANCE = 1, KNN_MODE_LIST = 2, KNN_MODE_DK = 3 };
 

@@ -261,7 +261,11 @@ __device__ __forceinline__ void put_query(PathCtx &P, int list, V p, V n, V ex, 
                  (uint64_t)(P.j++ & 0xffffu);
   if (slot >= a.qcap[list]) return;  // overflow: the host grows the lists and re-runs
   uint32_t sign = (ct > 0) ? 1u : ((ct < 0) ? 2u : 0u);
-  uint32_t meta = sign | ((uint32_t)mat << 2);
+  const double ax = fabs(n.x), ay = fabs(n.y), az = fabs(n.z);
+  const bool a0 = ax >= ay && ax >= az, a1 = !a0 && ay >= az;
+  const double nw = a0 ? n.x : a1 ? n.y : n.z;
+  const uint32_t face = (a0 ? 0u : a1 ? 2u : 4u) + (nw < 0.0 ? 1u : 0u);
+  uint32_t meta = sign | ((uint32_t)mat << 2) | (face << 28);
   a.qpos[list][slot] = make_float4((float)p.x, (float)p.y, (float)p.z, __uint_as_float(meta));
   QShade q;
   q.n[0] = n.x; q.n[1] = n.y; q.n[2] = n.z;
@@ -1260,7 +1264,7 @@ __global__ __launch_bounds__(64) void knn_kernel(KnnArgs a) {
           const QShade &sh = a.qshade[qi];
           uint32_t meta = __float_as_uint(qp.w);
           uint32_t sign = meta & 3u;
-          const DMaterial &m = a.mats[meta >> 2];
+          const DMaterial &m = a.mats[qmeta_mat(meta)];
           double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
           double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
           bool spec = (m.flags & MF_SPECULAR) || (m.n < 0);
@@ -1345,7 +1349,7 @@ __global__ __launch_bounds__(64) void cached_kernel(KnnArgs a) {
     const QShade &sh = a.qshade[q];
     uint32_t meta = __float_as_uint(qp.w);
     uint32_t sign = meta & 3u;
-    const DMaterial &m = a.mats[meta >> 2];
+    const DMaterial &m = a.mats[qmeta_mat(meta)];
     double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
     double out0 = 0, out1 = 0, out2 = 0;
     double closest = 0;

@@ -204,7 +204,7 @@ __device__ __forceinline__ void wave_estimate(const KnnArgs &a, int64_t qi, floa
       const QShade &sh = a.qshade[qi];
       uint32_t meta = __float_as_uint(qp.w);
       uint32_t sign = meta & 3u;
-      const DMaterial &m = a.mats[meta >> 2];
+      const DMaterial &m = a.mats[qmeta_mat(meta)];
       double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
       double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
       bool spec = (m.flags & MF_SPECULAR) || (m.n < 0);
@@ -896,7 +896,7 @@ __global__ __launch_bounds__(64) void knn_lane_kernel(KnnArgs a) {
           const QShade &sh = a.qshade[qi];
           uint32_t meta = __float_as_uint(qp.w);
           uint32_t sign = meta & 3u;
-          const DMaterial &m = a.mats[meta >> 2];
+          const DMaterial &m = a.mats[qmeta_mat(meta)];
           double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
           double E0 = sh.ex[0], E1 = sh.ex[1], E2 = sh.ex[2];
           bool spec = (m.flags & MF_SPECULAR) || (m.n < 0);

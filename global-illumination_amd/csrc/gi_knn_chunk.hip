@@ -626,7 +626,7 @@ __device__ __forceinline__ void chunk_estimate(const KnnArgs &a, int64_t qi, flo
       const QShade &sh = a.qshade[qi];
       uint32_t meta = __float_as_uint(qp.w);
       uint32_t sign = meta & 3u;
-      const DMaterial &mt = a.mats[meta >> 2];
+      const DMaterial &mt = a.mats[qmeta_mat(meta)];
       double N0 = sh.n[0], N1 = sh.n[1], N2 = sh.n[2];
       bool spec = (mt.flags & MF_SPECULAR) || (mt.n < 0);
       // without the specular term, ap * kd + 0 * ks == ap * kd up to the sign of a zero (for
@@ -791,7 +791,7 @@ __device__ __forceinline__ void chunk_estimate_shared(const KnnArgs &a, int lane
   const DMaterial *mt = nullptr;
   if (col && num > 0 && a.mode == KNN_MODE_RADIANCE && a.filter == 0 && !(a.dbg & 256)) {
     const uint32_t meta = __float_as_uint(qp.w);
-    mt = &a.mats[meta >> 2];
+    mt = &a.mats[qmeta_mat(meta)];
     const bool spec = (mt->flags & MF_SPECULAR) || (mt->n < 0);
     shp = !spec && isfinite(mt->ks[0]) && isfinite(mt->ks[1]) && isfinite(mt->ks[2]);
     if (shp) {

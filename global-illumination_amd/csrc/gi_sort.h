@@ -17,31 +17,31 @@ hipError_t morton_order(const float4 *q, int64_t n, const float bmin[3], const f
 // the same with the empty slots (meta == QMETA_NONE) sorted after every valid query: the first
 // *nvalid entries of the permutation are the valid queries in morton_order's order, so the k-NN
 // launch takes only those (synchronises st for the count)
-// key_bits > 10: cells of key_bits (<= 20) bits per axis and 64-bit keys
+// key_bits > 10: cells of key_bits (<= 20) bits per axis and 64-bit keys; with surf as well, 64-bit
+// surface keys with 16-bit in-plane cells (gi_sort.hip surf64_valid_kernel)
 hipError_t morton_order_valid(const float4 *q, int64_t n, const float bmin[3], const float bmax[3],
                               SortScratch &s, uint32_t **perm_out, int64_t *nvalid, hipStream_t st,
-                              int key_bits = 10);
+                              int key_bits = 10, bool surf = false);
 // The global list's launch order built from its slot layout instead of a sort over every slot:
 // primary slots [0, nprim) (validity read from q), then the tiled indirect slots [nprim,
 // nprim + 64 trows) whose row masks qmask[r] mark the entries holding a query (the reduction's
 // own masks, gi_kernels.hip ind_kernel / ind_cont_kernel), then the appends [qbase, nq), all
 // valid. The valid slots are compacted (row popcounts, a scan, a scatter: no per-slot pass over
 // the empty ones), keyed like morton_order_valid and sorted: the first *nvalid entries of the
-// permutation are the same queries, in the same order, as morton_order_valid's. With nrm (the
-// queries' surface normals, nstride doubles apart) the keys are surface keys instead (gi_sort.hip
-// surface_key: normal face, depth slab, 2-D Hilbert curve in the face's plane).
+// permutation are the same queries, in the same order, as morton_order_valid's. With surf the
+// keys are surface keys instead (gi_sort.hip surface_key: the face of the query's normal, a
+// depth slab, the 2-D Hilbert curve in the face's plane).
 hipError_t curve_order_rows(const float4 *q, int64_t nprim, const uint64_t *qmask, int64_t trows,
                             uint32_t qbase, int64_t nq, const float bmin[3], const float bmax[3],
                             SortScratch &s, uint32_t **perm_out, int64_t *nvalid, hipStream_t st,
-                            const double *nrm = nullptr, int nstride = 0);
+                            bool surf = false);
 void sort_scratch_release(SortScratch &s);
-// key parameters: the 3-D curve's 10-bit cells (origin o, scale s per axis, cmax), or, with nrm,
+// key parameters: the 3-D curve's 10-bit cells (origin o, scale s per axis, cmax), or, with surf,
 // the surface key's square 11-bit cells (siso) and 32 depth slabs per axis (sdep)
 struct KeyGeom {
   float o[3], s[3], cmax;
   float siso, sdep[3];
-  const double *nrm;
-  int nstride;
+  int surf;
 };
 
 struct KeySortScratch {

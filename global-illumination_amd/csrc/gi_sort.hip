@@ -88,6 +88,50 @@ __device__ __forceinline__ uint64_t curve_key64(uint32_t x, uint32_t y, uint32_t
   return (spread21(X[0] ^ t) << 2) | (spread21(X[1] ^ t) << 1) | spread21(X[2] ^ t);
 }
 
+// 30-bit surface key (r06): the query surface's dominant normal axis and side (6 faces, 3 bits),
+// its coordinate along that axis in 32 slabs of the scene box (5 bits), and the 2-D Hilbert
+// curve of the other two coordinates on square 11-bit cells (22 bits). Queries on a plane (every
+// global-map query of a cornell wall) then follow a 2-D curve in that plane instead of the plane's
+// cut through the 3-D curve, which leaves and re-enters it: 64 consecutive queries cover a
+// more compact patch, and the chunk gathers fewer photons (DESIGN.md 4.1).
+template <int B>
+__device__ __forceinline__ uint64_t hilbert2(uint32_t x, uint32_t y) {
+  uint64_t d = 0;
+  for (uint32_t s = 1u << (B - 1); s > 0u; s >>= 1) {
+    const uint32_t rx = (x & s) ? 1u : 0u, ry = (y & s) ? 1u : 0u;
+    d += (uint64_t)s * s * ((3u * rx) ^ ry);
+    if (ry == 0u) {
+      if (rx == 1u) {
+        x = s - 1u - (x & (s - 1u));
+        y = s - 1u - (y & (s - 1u));
+      }
+      const uint32_t t = x;
+      x = y;
+      y = t;
+    }
+  }
+  return d;
+}
+__device__ __forceinline__ uint32_t hilbert2_11(uint32_t x, uint32_t y) { return (uint32_t)hilbert2<11>(x, y); }
+// the face / slab / in-plane cells of a surface key with B-bit in-plane cells
+struct SurfCell {
+  uint32_t face, dep, cu, cv;
+};
+__device__ __forceinline__ SurfCell surface_cell(const float4 &p, float ox, float oy, float oz,
+                                                 const float sdep[3], float siso, float cmax) {
+  // the face comes with the query (qpos.w bits 28-30, put_query); selects, not indexed arrays
+  // (a lane-varying index into a local or kernel-argument array goes through scratch memory)
+  SurfCell c;
+  c.face = (__float_as_uint(p.w) >> 28) & 7u;
+  const bool a0 = c.face < 2u, a1 = c.face == 2u || c.face == 3u;
+  const float cx = p.x - ox, cy = p.y - oy, cz = p.z - oz;
+  const float cw = a0 ? cx * sdep[0] : a1 ? cy * sdep[1] : cz * sdep[2];
+  const float u = a0 ? cy : cx, v = (a0 || a1) ? cz : cy;
+  c.dep = (uint32_t)fminf(fmaxf(cw, 0.0f), 31.0f);
+  c.cu = (uint32_t)fminf(fmaxf(u * siso, 0.0f), cmax);
+  c.cv = (uint32_t)fminf(fmaxf(v * siso, 0.0f), cmax);
+  return c;
+}
 __global__ void morton_kernel(const float4 *q, int64_t n, float ox, float oy, float oz,
                               float sx, float sy, float sz, float cmax, uint32_t *keys, uint32_t *vals) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -189,6 +233,23 @@ __global__ void curve64_valid_kernel(const float4 *q, int64_t n, float ox, float
   keys[i] = valid ? curve_key64<B>((uint32_t)fx, (uint32_t)fy, (uint32_t)fz) : (1ull << (3 * B));
   vals[i] = (uint32_t)i;
 }
+// the surface key with B-bit in-plane cells as a 64-bit key (8 + 2B bits: face, slab, 2-D curve;
+// the empty slots get 2^(8 + 2B))
+template <int B>
+__global__ void surf64_valid_kernel(const float4 *q, int64_t n, KeyGeom g, uint64_t *keys,
+                                    uint32_t *vals) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float4 p = q[i];
+  const bool valid = __float_as_uint(p.w) != 0xffffffffu;  // QMETA_NONE (gi_kernels.h)
+  uint64_t key = 1ull << (8 + 2 * B);
+  if (valid) {
+    const SurfCell c = surface_cell(p, g.o[0], g.o[1], g.o[2], g.sdep, g.siso, (float)((1u << B) - 1u));
+    key = ((uint64_t)c.face << (5 + 2 * B)) | ((uint64_t)c.dep << (2 * B)) | hilbert2<B>(c.cu, c.cv);
+  }
+  keys[i] = key;
+  vals[i] = (uint32_t)i;
+}
 // first sorted key >= empty (the valid keys sort before the empty slots' key): one wave, 64
 // probes per round
 template <typename KeyT>
@@ -223,39 +284,9 @@ __global__ void row_popc_kernel(const uint64_t *rows, int64_t R, uint32_t *cnt) 
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r < R) cnt[r] = (uint32_t)__popcll(rows[r]);
 }
-// 30-bit surface key (r06): the query surface's dominant normal axis and side (6 faces, 3 bits),
-// its coordinate along that axis in 32 slabs of the scene box (5 bits), and the 2-D Hilbert
-// curve of the other two coordinates on square 11-bit cells (22 bits). Queries on a plane (every
-// global-map query of a cornell wall) then follow a 2-D curve in that plane instead of the plane's
-// cut through the 3-D curve, which leaves and re-enters it: 64 consecutive queries cover a
-// more compact patch, and the chunk gathers fewer photons (DESIGN.md 4.1).
-__device__ __forceinline__ uint32_t hilbert2_11(uint32_t x, uint32_t y) {
-  uint32_t d = 0;
-  for (uint32_t s = 1u << 10; s > 0u; s >>= 1) {
-    const uint32_t rx = (x & s) ? 1u : 0u, ry = (y & s) ? 1u : 0u;
-    d += s * s * ((3u * rx) ^ ry);
-    if (ry == 0u) {
-      if (rx == 1u) {
-        x = s - 1u - (x & (s - 1u));
-        y = s - 1u - (y & (s - 1u));
-      }
-      const uint32_t t = x;
-      x = y;
-      y = t;
-    }
-  }
-  return d;
-}
-__device__ __forceinline__ uint32_t surface_key(const float4 &p, const double *n, const KeyGeom &g) {
-  const double ax = fabs(n[0]), ay = fabs(n[1]), az = fabs(n[2]);
-  const int a = (ax >= ay && ax >= az) ? 0 : (ay >= az ? 1 : 2);
-  const int u = a == 0 ? 1 : 0, v = a == 2 ? 1 : 2;
-  const float c[3] = {p.x - g.o[0], p.y - g.o[1], p.z - g.o[2]};
-  const uint32_t face = 2u * (uint32_t)a + (n[a] < 0.0 ? 1u : 0u);
-  const uint32_t dep = (uint32_t)fminf(fmaxf(c[a] * g.sdep[a], 0.0f), 31.0f);
-  const uint32_t cu = (uint32_t)fminf(fmaxf(c[u] * g.siso, 0.0f), 2047.0f);
-  const uint32_t cv = (uint32_t)fminf(fmaxf(c[v] * g.siso, 0.0f), 2047.0f);
-  return (face << 27) | (dep << 22) | hilbert2_11(cu, cv);
+__device__ __forceinline__ uint32_t surface_key(const float4 &p, const KeyGeom &g) {
+  const SurfCell c = surface_cell(p, g.o[0], g.o[1], g.o[2], g.sdep, g.siso, 2047.0f);
+  return (c.face << 27) | (c.dep << 22) | hilbert2_11(c.cu, c.cv);
 }
 
 // the scatter and the keys in one pass (r05): lane b of row r's wave writes the key and slot of
@@ -265,24 +296,53 @@ __device__ __forceinline__ uint32_t slot_key10(const float4 *q, uint32_t slot, c
   const float4 p = q[slot];
   const bool valid = __float_as_uint(p.w) != 0xffffffffu;  // (always, by the masks)
   if (!valid) return 1u << 30;
-  if (g.nrm) return surface_key(p, g.nrm + (size_t)slot * g.nstride, g);
+  if (g.surf) return surface_key(p, g);
   float fx = fminf(fmaxf((p.x - g.o[0]) * g.s[0], 0.0f), g.cmax);
   float fy = fminf(fmaxf((p.y - g.o[1]) * g.s[1], 0.0f), g.cmax);
   float fz = fminf(fmaxf((p.z - g.o[2]) * g.s[2], 0.0f), g.cmax);
   return curve_key10((uint32_t)fx, (uint32_t)fy, (uint32_t)fz);
 }
-__global__ void row_keys_kernel(const uint64_t *rows, const uint32_t *off, int64_t Rp, int64_t R,
-                                int64_t nprim, const float4 *q, KeyGeom g, uint32_t *keys,
-                                uint32_t *vals) {
-  const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (r >= R) return;
-  const uint64_t m = rows[r];
+// one wave per 64 rows (r06; was one wave per row: C2's 6 M rows per list, half of them empty,
+// cost 2.1 ms per launch in wave dispatch): the lanes load the group's row masks and offsets
+// together, then the wave visits its non-empty rows two at a time (both rows' query loads issued
+// before either key is computed)
+__device__ __forceinline__ void row_put(const float4 *__restrict__ q, const KeyGeom &g, uint64_t m,
+                                        uint32_t o, int64_t r, int64_t Rp, int64_t nprim, int lane,
+                                        uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
   if ((m >> lane) & 1ull) {
-    const uint32_t at = off[r] + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    const uint32_t at = o + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
     const uint32_t slot = (uint32_t)(r < Rp ? 64 * r + lane : nprim + 64 * (r - Rp) + lane);
     keys[at] = slot_key10(q, slot, g);
     vals[at] = slot;
+  }
+}
+__global__ __launch_bounds__(256) void row_keys_kernel(const uint64_t *rows, const uint32_t *off,
+                                                       int64_t Rp, int64_t R, int64_t nprim,
+                                                       const float4 *__restrict__ q, KeyGeom g,
+                                                       uint32_t *__restrict__ keys,
+                                                       uint32_t *__restrict__ vals) {
+  const int64_t r0 = 64 * ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  if (r0 >= R) return;
+  const int64_t rl = r0 + lane;
+  const uint64_t mine = rl < R ? rows[rl] : 0ull;
+  const uint32_t moff = rl < R ? off[rl] : 0u;
+  uint64_t todo = __ballot(mine != 0ull);
+  while (todo) {
+    const int j = __ffsll((unsigned long long)todo) - 1;
+    todo &= todo - 1ull;
+    const uint64_t m1 = __shfl(mine, j, 64);
+    const uint32_t o1 = (uint32_t)__shfl((int)moff, j, 64);
+    if (todo) {
+      const int j2 = __ffsll((unsigned long long)todo) - 1;
+      todo &= todo - 1ull;
+      const uint64_t m2 = __shfl(mine, j2, 64);
+      const uint32_t o2 = (uint32_t)__shfl((int)moff, j2, 64);
+      row_put(q, g, m1, o1, r0 + j, Rp, nprim, lane, keys, vals);
+      row_put(q, g, m2, o2, r0 + j2, Rp, nprim, lane, keys, vals);
+    } else {
+      row_put(q, g, m1, o1, r0 + j, Rp, nprim, lane, keys, vals);
+    }
   }
 }
 __global__ void append_keys_kernel(const float4 *q, uint32_t qbase, int64_t napp, int64_t ndet,
@@ -300,7 +360,7 @@ __global__ void append_keys_kernel(const float4 *q, uint32_t qbase, int64_t napp
 
 hipError_t morton_order_valid(const float4 *q, int64_t n, const float bmin[3], const float bmax[3],
                               SortScratch &s, uint32_t **perm_out, int64_t *nvalid, hipStream_t st,
-                              int key_bits) {
+                              int key_bits, bool surf) {
   *perm_out = nullptr;
   *nvalid = 0;
   if (n <= 0) return hipSuccess;
@@ -315,7 +375,33 @@ hipError_t morton_order_valid(const float4 *q, int64_t n, const float bmin[3], c
   if ((e = grow(s.v1, s.v1_cap, b4)) != hipSuccess) return e;
   // the valid count lives past the keys (8 B, aligned)
   auto *d_cnt = reinterpret_cast<unsigned long long *>((char *)s.k0 + ((kb + 7) & ~(size_t)7));
-  if (wide) {
+  if (wide && surf) {
+    // surface keys with 16-bit in-plane cells: 8 + 32 key bits and the empty slots' bit, six
+    // radix passes (the 3-D curve's 16-bit cells take seven)
+    constexpr int B = 16;
+    KeyGeom g;
+    float emax = 0.0f;
+    for (int i = 0; i < 3; i++) {
+      float ext = bmax[i] - bmin[i];
+      g.o[i] = bmin[i];
+      g.sdep[i] = ext > 0 ? 32.0f / ext : 0.0f;
+      emax = std::max(emax, ext);
+    }
+    g.siso = emax > 0 ? (float)(1u << B) / emax : 0.0f;
+    surf64_valid_kernel<B><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(q, n, g, (uint64_t *)s.k0,
+                                                                        (uint32_t *)s.v0);
+    size_t tb = 0;
+    e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint64_t *)s.k0, (uint64_t *)s.k1,
+                                           (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0,
+                                           8 + 2 * B + 1, st);
+    if (e != hipSuccess) return e;
+    if ((e = grow(s.tmp, s.tmp_cap, tb + 256)) != hipSuccess) return e;
+    e = hipcub::DeviceRadixSort::SortPairs(s.tmp, tb, (const uint64_t *)s.k0, (uint64_t *)s.k1,
+                                           (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0,
+                                           8 + 2 * B + 1, st);
+    if (e != hipSuccess) return e;
+    first_empty_kernel<uint64_t><<<1, 64, 0, st>>>((const uint64_t *)s.k1, n, 1ull << (8 + 2 * B), d_cnt);
+  } else if (wide) {
     // B-bit cells, 64-bit keys: 3B + 1 key bits, (3B + 1) / 8 rounded up radix passes
     const int B = key_bits > 20 ? 20 : key_bits;
     const float cm = (float)((1 << B) - 1);
@@ -427,7 +513,7 @@ void sort_scratch_release(SortScratch &s) {
 hipError_t curve_order_rows(const float4 *q, int64_t nprim, const uint64_t *qmask, int64_t trows,
                             uint32_t qbase, int64_t nq, const float bmin[3], const float bmax[3],
                             SortScratch &s, uint32_t **perm_out, int64_t *nvalid, hipStream_t st,
-                            const double *nrm, int nstride) {
+                            bool surf) {
   *perm_out = nullptr;
   *nvalid = 0;
   if (nq <= 0) return hipSuccess;
@@ -474,10 +560,9 @@ hipError_t curve_order_rows(const float4 *q, int64_t nprim, const uint64_t *qmas
     emax = std::max(emax, ext);
   }
   g.siso = emax > 0 ? 2048.0f / emax : 0.0f;
-  g.nrm = nrm;
-  g.nstride = nstride;
+  g.surf = surf ? 1 : 0;
   if (R > 0)
-    row_keys_kernel<<<(unsigned)((R + 3) / 4), 256, 0, st>>>(rows, off, Rp, R, nprim, q, g,
+    row_keys_kernel<<<(unsigned)((R + 255) / 256), 256, 0, st>>>(rows, off, Rp, R, nprim, q, g,
                                                              (uint32_t *)s.k0, (uint32_t *)s.v0);
   if (napp > 0)
     append_keys_kernel<<<(unsigned)((napp + 255) / 256), 256, 0, st>>>(

@@ -246,6 +246,7 @@ int gi_compose_tiles(gi_ctx *ctx, int width, int height, int tile_px, int nshard
 int gi_quantize(int width, int height, const float *rgbf, uint8_t *rgb8);
 
 /* ---- test seams ----------------------------------------------------------------------- */
+/* n <= 2^26 queries per call (GI_ERR_ARG above). */
 int gi_estimate_radiance_batch(gi_ctx *ctx, int map, int64_t n, const gi_radiance_query *q,
                                double *rgb_out, int32_t *nfound, float *max_d2);
 int gi_knn_batch(gi_ctx *ctx, int map, int64_t n, const double *points, int k, double max_dist,

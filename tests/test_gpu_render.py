@@ -221,13 +221,15 @@ def test_element_pretest_is_exact(scene, monkeypatch):
 
 
 @pytest.mark.parametrize("scene", ["cornell.scn", "jensen.scn"])
-@pytest.mark.parametrize("var,vals", [("GI_ROW_ORDER", ("1", "0")), ("GI_SURF_KEY", ("1", "0"))])
+@pytest.mark.parametrize("var,vals", [("GI_ROW_ORDER", ("1", "0")), ("GI_SURF_KEY", ("1", "0")),
+                                      ("GI_SURF_KEY_C", ("1", "0"))])
 def test_knn_launch_order_is_exact(scene, var, vals, monkeypatch):
     """How the photon lookups (PhotonMap_EstimateRadiance, photonmap.cpp) are grouped into
     launches does not change any result: the global list's valid slots compacted from the
     indirect row masks before the sort (GI_ROW_ORDER=1, default) against the sort of every slot
     with the empty ones last (gi_sort.hip morton_order_valid), and the surface keys (face, depth
-    slab, 2-D Hilbert curve in the face's plane) against the 3-D curve. The f32 image and the -v counters
+    slab, 2-D Hilbert curve in the face's plane; global list GI_SURF_KEY, caustic list
+    GI_SURF_KEY_C) against the 3-D curve. The f32 image and the -v counters
     are equal; -tt/-st 4 give Monte Carlo paths, -it 16 many empty slots. (r06: the r04 order over
     every slot, the early estimate of the deterministic slots and other key resolutions, all
     measured slower and shown exact here in r05, were removed with their knobs.)"""

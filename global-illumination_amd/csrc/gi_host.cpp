@@ -393,7 +393,7 @@ struct gi_ctx {
   // the sort (gi_sort.h curve_order_rows) instead of sorting every slot with the empty ones last
   bool row_order = true;
   bool surf_key = true;             // global list: surface keys (gi_sort.hip surface_key) instead of the 3-D curve
-  bool surf_key_c = false;          // caustic list: 64-bit surface keys (surf64_valid_kernel)
+  bool surf_key_c = true;           // caustic list: 64-bit surface keys (surf64_valid_kernel)
   bool use_dk = true;              // wave k-NN kernel starts from per-photon K-th bounds
   DBuf qseg[2];  // K-best lists of the query-per-wave k-NN path
   size_t qcap_hint[2] = {0, 0};

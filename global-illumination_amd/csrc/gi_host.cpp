@@ -1667,19 +1667,9 @@ int gi_create(gi_ctx **out, int dev) {
   c->device = dev;
   gi_params_default(&c->P);
   if (hipSetDevice(dev) != hipSuccess) { delete c; return GI_ERR_HIP; }
-  {
-    int lo = 0, hi = 0;
-    const bool prio = env_num("GI_SIDE_PRIO", 0) < 0 && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess;
-    if ((prio ? hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi)
-              : hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) { delete c; return GI_ERR_HIP; }
-  }
-  {
-    int lo = 0, hi = 0;  // priorities: lo = least urgent, hi = most urgent
-    const bool prio = env_num("GI_SIDE_PRIO", 0) > 0 && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess;
-    if ((prio ? hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, hi)
-              : hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking)) != hipSuccess)
-      c->stream2 = nullptr;
-  }
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return GI_ERR_HIP; }
+  // (stream priorities for either stream measured no different: r06)
+  if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) c->stream2 = nullptr;
   hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
   hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
   for (int m = 0; m < 2; m++) {

@@ -1459,6 +1459,11 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
     // paths' tiled slots; Monte Carlo paths append after qbase[l]
     uint32_t qbase[2] = {(uint32_t)(nprim + tind), (uint32_t)nprim};
     a.qind_base = nprim;
+    // the empty tiled slots need their QMETA_NONE only where something reads every slot: the
+    // global list's sort over all slots (no row masks: GI_ROW_ORDER=0, or no indirect paths in a
+    // tiled batch) and the -cache lookup (thread per slot). C5 writes ~390 M of them per batch.
+    a.tiled_skip = c->row_order && c->key_bits[0] <= 10 && !P.irradiance_cache && a.ind_qmask &&
+                   (a.total_ind > 0 || tind == 0);
     for (int attempt = 0; attempt < 3; attempt++) {
       for (int l = 0; l < 2; l++) {
         // capacity: the largest list seen so far (+25 %), or this batch's primaries at the
@@ -1492,7 +1497,7 @@ int render_pixels(gi_ctx *c, int aa, int w, int h, const std::vector<int32_t> &p
       }
       a.qcount = c->qcount.as<uint32_t>();
       HIPCHK(c, hipMemcpyAsync(c->qcount.p, qbase, 8, hipMemcpyHostToDevice, c->stream));
-      if (tind > (uint64_t)a.total_ind) launch_ind_pad(a, c->stream);  // (never when tind = 0)
+      if (!a.tiled_skip && tind > (uint64_t)a.total_ind) launch_ind_pad(a, c->stream);  // (never when tind = 0)
       launch_path(a, c->stream, c->stream2, c->ev_fork, c->ev_join, true);
       HIPCHK(c, hipGetLastError());
       HIPCHK(c, hipMemcpyAsync(nq, c->qcount.p, 8, hipMemcpyDeviceToHost, c->stream));

@@ -100,6 +100,8 @@ struct RenderArgs {
   int64_t tind;               // tiled indirect entries (64 per row, >= total_ind; RenderArgs::ind_rows)
   int32_t dbg;          // diagnostics: 1 = skip the indirect trace, 2 = skip diffuse sampling too
   int32_t split_ind;    // 1: indirect paths trace their first bounce, continuations are queued
+  int32_t tiled_skip;   // 1: unused tiled indirect slots keep whatever they hold instead of QMETA_NONE
+                        // (the global list's k-NN order comes from the row masks; nothing reads them)
   IndCont *ind_cont;    // continuation queue: IND_QS stripes of ind_cap_s entries
   uint32_t *ind_ncont;  // fill of stripe s at [s * 32] (one 128-B line per counter)
   uint32_t ind_cap_s;

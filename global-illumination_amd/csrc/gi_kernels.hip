@@ -230,6 +230,7 @@ __device__ __forceinline__ bool keyed_slot(const RenderArgs &a, int list, int64_
 }
 
 __device__ __forceinline__ void put_none(const RenderArgs &a, int list, int64_t slot) {
+  if (a.tiled_skip && !keyed_slot(a, list, slot)) return;  // a tiled slot nothing reads
   a.qpos[list][slot] = make_float4(0.f, 0.f, 0.f, __uint_as_float(QMETA_NONE));
   if (keyed_slot(a, list, slot)) a.qkey[list][slot] = ~0ull;
 }

@@ -510,6 +510,26 @@ void sort_scratch_release(SortScratch &s) {
   s = SortScratch();
 }
 
+// the row path's 30-bit key sort: three onesweep passes of 10 bits (rocprim's gfx950 default for
+// 32-bit pairs is 8 bits: four passes). C2's 214 M pairs per launch: 5.8 -> 5.1 ms per launch,
+// frame -8 ms; 11 bits (two passes of 11, one of 8) was slower than either (r06,
+// profiles/r06_row_sort_ab.jsonl)
+#ifndef GI_ROW_RADIX_BITS
+#define GI_ROW_RADIX_BITS 10
+#endif
+static hipError_t row_sort(void *tmp, size_t &tb, const uint32_t *k0, uint32_t *k1, const uint32_t *v0,
+                           uint32_t *v1, int64_t n, hipStream_t st) {
+#if GI_ROW_RADIX_BITS == 8
+  return hipcub::DeviceRadixSort::SortPairs(tmp, tb, k0, k1, v0, v1, (int)n, 0, 30, st);
+#else
+  using cfg = rocprim::radix_sort_config<
+      rocprim::default_config, rocprim::default_config,
+      rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>,
+                                          GI_ROW_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>>;
+  return rocprim::radix_sort_pairs<cfg>(tmp, tb, k0, k1, v0, v1, (size_t)n, 0, 30, st);
+#endif
+}
+
 hipError_t curve_order_rows(const float4 *q, int64_t nprim, const uint64_t *qmask, int64_t trows,
                             uint32_t qbase, int64_t nq, const float bmin[3], const float bmax[3],
                             SortScratch &s, uint32_t **perm_out, int64_t *nvalid, hipStream_t st,
@@ -567,22 +587,17 @@ hipError_t curve_order_rows(const float4 *q, int64_t nprim, const uint64_t *qmas
   if (napp > 0)
     append_keys_kernel<<<(unsigned)((napp + 255) / 256), 256, 0, st>>>(
         q, qbase, napp, (int64_t)ndet, g, (uint32_t *)s.k0, (uint32_t *)s.v0);
-  auto *d_cnt = reinterpret_cast<unsigned long long *>((char *)s.k0 + ((b4 + 7) & ~(size_t)7));
+  // every compacted slot holds a query (the masks say so), so every key is below 2^30: 30 key
+  // bits, and no count of the valid ones
   tb = 0;
-  e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t *)s.k0, (uint32_t *)s.k1,
-                                         (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0,
-                                         3 * bits + 1, st);
+  e = row_sort(nullptr, tb, (const uint32_t *)s.k0, (uint32_t *)s.k1, (const uint32_t *)s.v0,
+               (uint32_t *)s.v1, n, st);
   if (e != hipSuccess) return e;
   if ((e = grow(s.tmp, s.tmp_cap, tb + 256)) != hipSuccess) return e;
-  e = hipcub::DeviceRadixSort::SortPairs(s.tmp, tb, (const uint32_t *)s.k0, (uint32_t *)s.k1,
-                                         (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0,
-                                         3 * bits + 1, st);
+  e = row_sort(s.tmp, tb, (const uint32_t *)s.k0, (uint32_t *)s.k1, (const uint32_t *)s.v0,
+               (uint32_t *)s.v1, n, st);
   if (e != hipSuccess) return e;
-  first_empty_kernel<uint32_t><<<1, 64, 0, st>>>((const uint32_t *)s.k1, n, 1u << 30, d_cnt);
-  unsigned long long nv = 0;
-  if ((e = hipMemcpyAsync(&nv, d_cnt, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
-  if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-  *nvalid = (int64_t)nv;
+  *nvalid = n;
   *perm_out = (uint32_t *)s.v1;
   return hipSuccess;
 }

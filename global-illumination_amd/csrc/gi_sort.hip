@@ -358,6 +358,25 @@ __global__ void append_keys_kernel(const float4 *q, uint32_t qbase, int64_t napp
 // (a per-wave atomic count in morton_valid_kernel serialised 6M same-address atomics: r05i,
 // +32 ms per list)
 
+// the row path's 30-bit key sort: three onesweep passes of 10 bits (rocprim's gfx950 default for
+// 32-bit pairs is 8 bits: four passes). C2's 214 M pairs per launch: 5.8 -> 5.1 ms per launch,
+// frame -8 ms; 11 bits (two passes of 11, one of 8) and sort blocks of 512 x 16 were slower, 1024
+// x 12 the same (r06, profiles/r06_row_sort_ab.jsonl)
+static hipError_t row_sort(void *tmp, size_t &tb, const uint32_t *k0, uint32_t *k1, const uint32_t *v0,
+                           uint32_t *v1, int64_t n, hipStream_t st) {
+  using cfg = rocprim::radix_sort_config<
+      rocprim::default_config, rocprim::default_config,
+      rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, 10,
+                                          rocprim::block_radix_rank_algorithm::match>>;
+  return rocprim::radix_sort_pairs<cfg>(tmp, tb, k0, k1, v0, v1, (size_t)n, 0, 30, st);
+}
+// the caustic list's 41-bit surface keys in 64-bit words: hipcub's default (8-bit passes; 10-bit
+// passes measured the same at C2 / C3 / C4)
+static hipError_t wide_sort(void *tmp, size_t &tb, const uint64_t *k0, uint64_t *k1, const uint32_t *v0,
+                            uint32_t *v1, int64_t n, int bits, hipStream_t st) {
+  return hipcub::DeviceRadixSort::SortPairs(tmp, tb, k0, k1, v0, v1, (int)n, 0, bits, st);
+}
+
 hipError_t morton_order_valid(const float4 *q, int64_t n, const float bmin[3], const float bmax[3],
                               SortScratch &s, uint32_t **perm_out, int64_t *nvalid, hipStream_t st,
                               int key_bits, bool surf) {
@@ -391,14 +410,12 @@ hipError_t morton_order_valid(const float4 *q, int64_t n, const float bmin[3], c
     surf64_valid_kernel<B><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(q, n, g, (uint64_t *)s.k0,
                                                                         (uint32_t *)s.v0);
     size_t tb = 0;
-    e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint64_t *)s.k0, (uint64_t *)s.k1,
-                                           (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0,
-                                           8 + 2 * B + 1, st);
+    e = wide_sort(nullptr, tb, (const uint64_t *)s.k0, (uint64_t *)s.k1, (const uint32_t *)s.v0,
+                  (uint32_t *)s.v1, n, 8 + 2 * B + 1, st);
     if (e != hipSuccess) return e;
     if ((e = grow(s.tmp, s.tmp_cap, tb + 256)) != hipSuccess) return e;
-    e = hipcub::DeviceRadixSort::SortPairs(s.tmp, tb, (const uint64_t *)s.k0, (uint64_t *)s.k1,
-                                           (const uint32_t *)s.v0, (uint32_t *)s.v1, (int)n, 0,
-                                           8 + 2 * B + 1, st);
+    e = wide_sort(s.tmp, tb, (const uint64_t *)s.k0, (uint64_t *)s.k1, (const uint32_t *)s.v0,
+                  (uint32_t *)s.v1, n, 8 + 2 * B + 1, st);
     if (e != hipSuccess) return e;
     first_empty_kernel<uint64_t><<<1, 64, 0, st>>>((const uint64_t *)s.k1, n, 1ull << (8 + 2 * B), d_cnt);
   } else if (wide) {
@@ -508,26 +525,6 @@ void sort_scratch_release(SortScratch &s) {
   for (void *p : ps)
     if (p) hipFree(p);
   s = SortScratch();
-}
-
-// the row path's 30-bit key sort: three onesweep passes of 10 bits (rocprim's gfx950 default for
-// 32-bit pairs is 8 bits: four passes). C2's 214 M pairs per launch: 5.8 -> 5.1 ms per launch,
-// frame -8 ms; 11 bits (two passes of 11, one of 8) was slower than either (r06,
-// profiles/r06_row_sort_ab.jsonl)
-#ifndef GI_ROW_RADIX_BITS
-#define GI_ROW_RADIX_BITS 10
-#endif
-static hipError_t row_sort(void *tmp, size_t &tb, const uint32_t *k0, uint32_t *k1, const uint32_t *v0,
-                           uint32_t *v1, int64_t n, hipStream_t st) {
-#if GI_ROW_RADIX_BITS == 8
-  return hipcub::DeviceRadixSort::SortPairs(tmp, tb, k0, k1, v0, v1, (int)n, 0, 30, st);
-#else
-  using cfg = rocprim::radix_sort_config<
-      rocprim::default_config, rocprim::default_config,
-      rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>,
-                                          GI_ROW_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>>;
-  return rocprim::radix_sort_pairs<cfg>(tmp, tb, k0, k1, v0, v1, (size_t)n, 0, 30, st);
-#endif
 }
 
 hipError_t curve_order_rows(const float4 *q, int64_t nprim, const uint64_t *qmask, int64_t trows,

@@ -77,6 +77,12 @@ def test_bench_device_set_matches_one_gpu():
     assert two["device_set"]["devices"] == [0, 0]
     assert two["device_set"]["gather_ms"] >= 0.0
     assert two["roofline"]["global"]["queries_per_launch"] > 0
+    # the line says what ran where (gi_device_info): both entries on GPU 0, one PCI bus; with
+    # distinct devices comm_count is the RCCL communicator's rank count
+    topo = two["topology"]
+    assert topo["mode"] != "single" and topo["devices"] == [0, 0]
+    assert len(topo["pci_bus"]) == 2 and topo["distinct_pci_bus"] == 1
+    assert topo["comm_count"] in (0, 2)
 
 
 def test_bench_torchrun_packed_matches_one_gpu():
@@ -88,3 +94,6 @@ def test_bench_torchrun_packed_matches_one_gpu():
                     launcher=launcher)
     assert two["n_gpus"] == 2
     assert two["image_sha16"] == one["image_sha16"]
+    topo = two["topology"]
+    assert topo["mode"] == "torchrun" and topo["comm_count"] == 2
+    assert sorted(x["rank"] for x in topo["ranks"]) == [0, 1]

@@ -12,3 +12,5 @@ tail -1 $D/c4.log | cut -c1-200
 timeout -k 10 500 python3 -u bench.py --steps 2 --warmup 1 --scene teapot.scn --res 4096 --aa 3 --global-photons 8000000 --caustic-photons 0 --extra "-dof 4 12.2282 0.025 -no_caustic" --shard 1/8 --no-cpu-baseline > $D/c5.log 2>&1 || { tail -5 $D/c5.log; exit 1; }
 tail -1 $D/c5.log | cut -c1-200
 TAG=_final bash tools/gpu_pmc_fp64.sh
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_multi.py > $D/multi.log 2>&1 || { tail -20 $D/multi.log; exit 1; }
+tail -1 $D/multi.log

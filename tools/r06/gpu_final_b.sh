@@ -14,3 +14,5 @@ tail -1 $D/c5.log | cut -c1-200
 TAG=_final bash tools/gpu_pmc_fp64.sh
 timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_multi.py > $D/multi.log 2>&1 || { tail -20 $D/multi.log; exit 1; }
 tail -1 $D/multi.log
+timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $D/smoke.log 2>&1 || { tail -20 $D/smoke.log; exit 1; }
+tail -1 $D/smoke.log

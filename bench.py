@@ -117,7 +117,7 @@ ROOFLINE_KERNELS = ["knn_chunk_lane_kernel", "knn_lane_kernel"]
 
 # k-NN launch sequences by gi_render_stats.knn_map_kind (run_knn in gi_host.cpp)
 KNN_KINDS = {
-    7: "gi::knn_chunk_lane_kernel<4,240> -> knn_chunk_lane_kernel<2,480> -> knn_lane_kernel<8,4> fallback",
+    7: "gi::knn_chunk_lane_kernel<4,240> -> knn_chunk_lane_kernel<2,480> -> knn_wave_kernel<128> fallback",
     8: "gi::knn_chunk_big_kernel<512> -> knn_chunk_big_kernel<1024> -> knn_wave_kernel<512> fallback",
     3: "gi::knn_lane_kernel<8,4>",
     1: "gi::knn_wave_kernel + knn_list_estimate_kernel",

@@ -394,6 +394,7 @@ struct gi_ctx {
   bool row_order = true;
   bool surf_key = true;             // global list: surface keys (gi_sort.hip surface_key) instead of the 3-D curve
   bool surf_key_c = true;           // caustic list: 64-bit surface keys (surf64_valid_kernel)
+  bool fb_wave = true;              // chunk kernel's last fallback: the query-per-wave kernel (r06; the per-lane one: GI_FB_WAVE=0)
   bool use_dk = true;              // wave k-NN kernel starts from per-photon K-th bounds
   DBuf qseg[2];  // K-best lists of the query-per-wave k-NN path
   size_t qcap_hint[2] = {0, 0};
@@ -1150,7 +1151,12 @@ int run_knn(gi_ctx *c, KnnArgs k, int64_t nq, double *ms) {
       f.nq = nfb2;
       f.q0 = 0;
       f.map.dk = fb_dk;
-      launch_knn_lane(f, X.st);
+      if (c->fb_wave) {
+        if (!launch_knn_wave(f, c->wave_cap_mul, X.st))
+          return fail(c, GI_ERR_ARG, "k-NN launch: unsupported estimate size for this kernel");
+      } else {
+        launch_knn_lane(f, X.st);
+      }
       HIPCHK(c, hipGetLastError());
     }
     HIPCHK(c, hipEventRecord(X.ev1, X.st));
@@ -1719,6 +1725,8 @@ int gi_create(gi_ctx **out, int dev) {
   c->row_order = env_num("GI_ROW_ORDER", c->row_order) != 0;
   c->surf_key = env_num("GI_SURF_KEY", c->surf_key) != 0;
   c->surf_key_c = env_num("GI_SURF_KEY_C", c->surf_key_c) != 0;
+  c->fb_wave = env_num("GI_FB_WAVE", c->fb_wave) != 0;
+  c->chunk_lane2 = env_num("GI_CHUNK_LANE2", c->chunk_lane2) != 0;
   *out = c;
   return GI_OK;
 }

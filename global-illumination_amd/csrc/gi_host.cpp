@@ -374,7 +374,7 @@ struct gi_ctx {
   // not faster (profiles/r05_chunk_pass_chain_ab.txt)
   int chunk_cap_big2 = 1024;
   int chunk_cap_big3 = 0;
-  bool chunk_lane2 = true;           // lane-select chunk k-NN: second pass (480, GI_CHUNK_LANE2)
+  bool chunk_lane2 = true;           // lane-select chunk k-NN: second pass (480; without it C5 +1.8 %, C2 / C4 +0.4-0.6 %, r06)
   int chunk_minsub_big2 = 64;        // ... its overflowing chunks retried down to this group size
   bool chunk_dk = true;            // chunk kernel (K <= 64): centre bound from the dk bounds (measured: fewer fallbacks)
   bool chunk_fb_all = false;       // test knob: the lane-select chunk kernel hands every query to its fallback
@@ -1726,7 +1726,6 @@ int gi_create(gi_ctx **out, int dev) {
   c->surf_key = env_num("GI_SURF_KEY", c->surf_key) != 0;
   c->surf_key_c = env_num("GI_SURF_KEY_C", c->surf_key_c) != 0;
   c->fb_wave = env_num("GI_FB_WAVE", c->fb_wave) != 0;
-  c->chunk_lane2 = env_num("GI_CHUNK_LANE2", c->chunk_lane2) != 0;
   *out = c;
   return GI_OK;
 }

@@ -8,7 +8,7 @@ wave, 0 = per-lane with global-memory heaps (any K). GI_CHUNK_MINSUB sets how fa
 overflowing chunk is split (1 = down to single queries, 64 = straight to the fallback);
 GI_KNN_DK=0 turns off the start from per-photon K-th distance bounds; GI_CHUNK_FB_ALL=1 sends
 every query of the chunk kernel to its fallback (the query-per-wave kernel; GI_FB_WAVE=0: the
-per-lane kernel); GI_CHUNK_LANE2=0 drops the second chunk pass; GI_CHUNK_DK_EXACT=0 keeps the large-K chunk
+per-lane kernel); GI_CHUNK_DK_EXACT=0 keeps the large-K chunk
 kernel's centre bound at the per-photon dk bound (default: refined to the exact d_K(c)). Each
 must return the oracle's k-NN sets exactly
 (the fp32 metric is shared; only photons tied at the k-th distance may differ) and its
@@ -36,11 +36,9 @@ VARIANTS = [
     {"GI_KNN_KERNEL": "7", "GI_CHUNK_MINSUB": "1"},
     {"GI_KNN_KERNEL": "7", "GI_CHUNK_DK": "0"},
     {"GI_KNN_KERNEL": "7", "GI_CHUNK_FB_ALL": "1", "GI_KNN_DK": "0"},
-    # the per-lane kernel as the last fallback (the query-per-wave kernel is the default), and
-    # no second chunk pass
+    # the per-lane kernel as the last fallback (the query-per-wave kernel is the default)
     {"GI_KNN_KERNEL": "7", "GI_FB_WAVE": "0"},
     {"GI_KNN_KERNEL": "7", "GI_FB_WAVE": "0", "GI_CHUNK_FB_ALL": "1", "GI_LEAF_SIZE": "32"},
-    {"GI_KNN_KERNEL": "7", "GI_CHUNK_LANE2": "0"},
     {"GI_KNN_KERNEL": "8"},
     {"GI_KNN_KERNEL": "8", "GI_CHUNK_DK_EXACT": "0"},
     {"GI_KNN_KERNEL": "8", "GI_LEAF_SIZE": "128"},

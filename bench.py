@@ -112,7 +112,9 @@ def shard_balance(a):
     r.close()
 
 
-# the roofline "launch": the chunk k-NN kernel and its per-lane fallback on the global map
+# the kernels of the FETCH_SIZE pass behind roofline.traffic (profiles/knn_traffic.json): the
+# chunk k-NN passes and, when it was taken, the per-lane last fallback (the query-per-wave
+# kernel since r06's final tree; 0.1 ms of a ~40 ms launch)
 ROOFLINE_KERNELS = ["knn_chunk_lane_kernel", "knn_lane_kernel"]
 
 # k-NN launch sequences by gi_render_stats.knn_map_kind (run_knn in gi_host.cpp)
